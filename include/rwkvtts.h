@@ -1,0 +1,300 @@
+/*
+ * rwkvtts.h -- C-ABI drop-in boundary for the RWKV-TTS inference hot path on MI355X (gfx950).
+ *
+ * Every entry point here replaces one reference interface of liuzl/rwkv-tts-rs @ 2025-12-05
+ * (paths relative to the reference root); the Rust-side binding a maintainer would add is in
+ * INTEGRATION.md. Conventions: plain pointers + sizes, opaque handles, int status (0 = OK,
+ * negative = error, message via rwkvtts_last_error()), no exceptions across the ABI, all
+ * buffers caller-owned. One engine per GPU; calls on an engine come from one owning host
+ * thread except rwkvtts_manager_submit/poll, which are thread-safe.
+ */
+#ifndef RWKVTTS_H
+#define RWKVTTS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- constants: src/rwkv_sampler.rs:294-299, src/properties_util.rs:5 ------------------ */
+#define RWKVTTS_EOS_TOKEN 8192          /* TTS_EOS_TOKEN */
+#define RWKVTTS_TAG_0 8193              /* TTS_TAG_0 */
+#define RWKVTTS_TAG_1 8194              /* TTS_TAG_1 */
+#define RWKVTTS_TAG_2 8195              /* TTS_TAG_2 */
+#define RWKVTTS_GLOBAL_TOKEN_OFFSET 8196 /* GLOBAL_TOKEN_OFFSET */
+#define RWKVTTS_SPECIAL_TOKEN_OFFSET 77823 /* TTS_SPECIAL_TOKEN_OFFSET */
+#define RWKVTTS_N_GLOBAL 32             /* normal_mode_inference.rs:220 global_tokens_size */
+#define RWKVTTS_SEMANTIC_LIMIT 2048     /* normal_mode_inference.rs:316 */
+#define RWKVTTS_HOP 320                 /* 参考/C/tts/sparktts.h:55 latent_hop_length */
+#define RWKVTTS_SAMPLE_RATE 16000       /* 参考/C/tts/sparktts.h:53 */
+
+/* status codes */
+#define RWKVTTS_OK 0
+#define RWKVTTS_EINVAL -1
+#define RWKVTTS_EHIP -2
+#define RWKVTTS_ENOMEM -3
+#define RWKVTTS_EUNSUPPORTED -4
+#define RWKVTTS_EBUSY -5
+
+/* weight storage dtypes (matrices; vectors are always f32) */
+#define RWKVTTS_DTYPE_BF16 0
+#define RWKVTTS_DTYPE_F16 1
+
+/* ---- model description ------------------------------------------------------------------ */
+/* RWKV-7 "x070" dims (tensor names A.3). web-rwkv ModelInfo analogue. */
+typedef struct {
+  int32_t n_layer;   /* L */
+  int32_t n_embd;    /* C */
+  int32_t head_size; /* N (64); H = C / N */
+  int32_t n_ffn;     /* F */
+  int32_t n_vocab;   /* V */
+  int32_t d_decay;   /* w LoRA rank */
+  int32_t d_aaa;     /* a LoRA rank */
+  int32_t d_mv;      /* v LoRA rank */
+  int32_t d_gate;    /* g LoRA rank */
+} rwkvtts_dims;
+
+/* Packed weight blob: tensor index -> byte offset. Matrices in [out][in] row-major
+ * (the LoRA matrices are stored transposed relative to the checkpoint so that every
+ * projection reads contiguous rows of its input dimension). */
+enum {
+  RWKVTTS_T_EMB = 0, RWKVTTS_T_LN0_W, RWKVTTS_T_LN0_B, RWKVTTS_T_LNOUT_W, RWKVTTS_T_LNOUT_B,
+  RWKVTTS_T_HEAD, RWKVTTS_T_GLOBAL_COUNT
+};
+enum {
+  RWKVTTS_L_LN1_W = 0, RWKVTTS_L_LN1_B, RWKVTTS_L_LN2_W, RWKVTTS_L_LN2_B,
+  RWKVTTS_L_XR, RWKVTTS_L_XW, RWKVTTS_L_XK, RWKVTTS_L_XV, RWKVTTS_L_XA, RWKVTTS_L_XG,
+  RWKVTTS_L_W0, RWKVTTS_L_A0, RWKVTTS_L_V0, RWKVTTS_L_KK, RWKVTTS_L_KA, RWKVTTS_L_RK,
+  RWKVTTS_L_LNX_W, RWKVTTS_L_LNX_B, RWKVTTS_L_FFN_XK,
+  /* ---- matrices from here on ---- */
+  RWKVTTS_L_WR, RWKVTTS_L_WK, RWKVTTS_L_WV, RWKVTTS_L_WO,
+  RWKVTTS_L_W1T, RWKVTTS_L_A1T, RWKVTTS_L_V1T, RWKVTTS_L_G1T, /* [D][C] */
+  RWKVTTS_L_W2T, RWKVTTS_L_A2T, RWKVTTS_L_V2T, RWKVTTS_L_G2T, /* [C][D] */
+  RWKVTTS_L_FFN_K, /* [F][C] */
+  RWKVTTS_L_FFN_V, /* [C][F] */
+  RWKVTTS_L_COUNT
+};
+#define RWKVTTS_L_FIRST_MAT RWKVTTS_L_WR
+
+/* Fill rows/cols of one tensor. Returns 1 for a matrix (2-byte dtype), 0 for an f32 vector. */
+static inline int rwkvtts_tensor_shape(const rwkvtts_dims* d, int layer, int t, int64_t* rows,
+                                       int64_t* cols) {
+  const int64_t C = d->n_embd, V = d->n_vocab, F = d->n_ffn;
+  if (layer < 0) {
+    switch (t) {
+      case RWKVTTS_T_EMB: *rows = V; *cols = C; return 1;
+      case RWKVTTS_T_HEAD: *rows = V; *cols = C; return 1;
+      default: *rows = 1; *cols = C; return 0;
+    }
+  }
+  switch (t) {
+    case RWKVTTS_L_WR: case RWKVTTS_L_WK: case RWKVTTS_L_WV: case RWKVTTS_L_WO:
+      *rows = C; *cols = C; return 1;
+    case RWKVTTS_L_W1T: *rows = d->d_decay; *cols = C; return 1;
+    case RWKVTTS_L_A1T: *rows = d->d_aaa; *cols = C; return 1;
+    case RWKVTTS_L_V1T: *rows = d->d_mv; *cols = C; return 1;
+    case RWKVTTS_L_G1T: *rows = d->d_gate; *cols = C; return 1;
+    case RWKVTTS_L_W2T: *rows = C; *cols = d->d_decay; return 1;
+    case RWKVTTS_L_A2T: *rows = C; *cols = d->d_aaa; return 1;
+    case RWKVTTS_L_V2T: *rows = C; *cols = d->d_mv; return 1;
+    case RWKVTTS_L_G2T: *rows = C; *cols = d->d_gate; return 1;
+    case RWKVTTS_L_FFN_K: *rows = F; *cols = C; return 1;
+    case RWKVTTS_L_FFN_V: *rows = C; *cols = F; return 1;
+    default: *rows = 1; *cols = C; return 0;
+  }
+}
+
+/* Byte offset of tensor t of `layer` (-1 = global tensors) in the packed blob; every tensor
+ * starts on a 256-byte boundary. With layer == -2 returns the total blob size. */
+static inline int64_t rwkvtts_tensor_offset(const rwkvtts_dims* d, int layer, int t) {
+  int64_t off = 256; /* header */
+  int64_t r, c;
+  for (int l = -1; l < d->n_layer; ++l) {
+    const int n = (l < 0) ? RWKVTTS_T_GLOBAL_COUNT : RWKVTTS_L_COUNT;
+    for (int i = 0; i < n; ++i) {
+      if (l == layer && i == t) return off;
+      int m = rwkvtts_tensor_shape(d, l, i, &r, &c);
+      int64_t bytes = r * c * (m ? 2 : 4);
+      off += (bytes + 255) & ~(int64_t)255;
+    }
+  }
+  return off;
+}
+static inline int64_t rwkvtts_blob_bytes(const rwkvtts_dims* d) {
+  return rwkvtts_tensor_offset(d, -2, 0);
+}
+
+/* Blob header (first 256 bytes). */
+typedef struct {
+  uint32_t magic;   /* 'RWT7' = 0x37545752 */
+  uint32_t version; /* 1 */
+  int32_t dtype;    /* RWKVTTS_DTYPE_* of the matrices */
+  int32_t pad0;
+  rwkvtts_dims dims;
+} rwkvtts_blob_header;
+#define RWKVTTS_BLOB_MAGIC 0x37545752u
+
+/* Deterministic synthetic weights (N(0, 0.02) matrices, decay w0 chosen so that
+ * w in (0.3, 0.99), lerp coefficients in [0,1]); counter-based so every tool regenerates the
+ * same blob. `out` must hold rwkvtts_blob_bytes(dims) bytes. */
+int rwkvtts_synth_weights(const rwkvtts_dims* dims, int dtype, uint64_t seed, void* out);
+
+/* ---- engine: SharedRwkvRuntime::new / v7::Bundle::new (src/shared_runtime.rs:70-208) ---- */
+typedef struct rwkvtts_engine rwkvtts_engine;
+
+typedef struct {
+  int32_t device;           /* HIP device ordinal */
+  int32_t max_slots;        /* state slots = Bundle max_batch (shared_runtime.rs:177) */
+  int32_t token_chunk_size; /* rows per forward = RnnInput token_chunk_size (lightweight_tts_pipeline.rs:799) */
+  int32_t use_graphs;       /* capture decode steps in hipGraphs */
+} rwkvtts_engine_desc;
+
+/* weights: packed blob (header included). blob_on_device != 0: `weights` is a device pointer
+ * on desc->device (e.g. a buffer filled by an RCCL broadcast); it is copied. */
+int rwkvtts_engine_create(const rwkvtts_engine_desc* desc, const void* weights, size_t bytes,
+                          int blob_on_device, rwkvtts_engine** out);
+int rwkvtts_engine_destroy(rwkvtts_engine* e);
+const char* rwkvtts_last_error(void);
+int rwkvtts_engine_dims(const rwkvtts_engine* e, rwkvtts_dims* out);
+
+/* ---- state: State::init/load/back (normal_mode_inference.rs:66-70) --------------------- */
+/* Per-slot state = per layer [att_shift C | wkv H*N*N (value-major S[i][j]) | ffn_shift C] f32. */
+int64_t rwkvtts_state_floats(const rwkvtts_engine* e);
+int rwkvtts_slot_reset(rwkvtts_engine* e, int slot);                 /* State::load(init, slot) */
+int rwkvtts_slot_read(rwkvtts_engine* e, int slot, float* host_out); /* State::back(slot) */
+int rwkvtts_slot_write(rwkvtts_engine* e, int slot, const float* host_in);
+
+/* ---- LM runtime: Runtime<Rnn>::infer (normal_mode_inference.rs:62-80) ------------------ */
+#define RWKVTTS_OPT_LAST 0 /* RnnOption::Last */
+#define RWKVTTS_OPT_FULL 1 /* RnnOption::Full (logits for every token) */
+typedef struct {
+  int32_t slot;           /* batch index == state slot */
+  const uint32_t* tokens; /* pending input tokens of this batch */
+  int32_t n_tokens;
+  int32_t option;         /* RWKVTTS_OPT_* */
+} rwkvtts_input;
+
+/* Consumes up to token_chunk_size tokens in total across `inputs` (each batch advances by
+ * consumed[i]). For every batch whose input is exhausted by this call and option == LAST,
+ * writes logits of its last token to logits[i * head_rows ... + head_rows) and sets
+ * has_logits[i] = 1 (RnnOutput[i].0.size() > 0); otherwise has_logits[i] = 0.
+ * head_rows <= n_vocab selects the leading vocabulary rows (all samplers read a prefix).
+ * OPT_FULL writes logits for every consumed token at logits[(row) * head_rows], rows in
+ * input order. logits is a HOST buffer. */
+int rwkvtts_infer(rwkvtts_engine* e, const rwkvtts_input* inputs, int n_inputs, int head_rows,
+                  float* logits, int32_t* consumed, int32_t* has_logits);
+
+/* ---- sampler: sample_logits_with_top_p_k (src/rwkv_sampler.rs:55-211) ------------------ */
+/* rand 0.8.5 StdRng (ChaCha12, seed_from_u64 via PCG32) is represented statelessly by its
+ * 32-byte key and the index of the next u32 draw. */
+typedef struct {
+  uint32_t key[8];
+  uint64_t draw_index;
+} rwkvtts_rng;
+void rwkvtts_rng_seed_from_u64(uint64_t seed, rwkvtts_rng* out); /* StdRng::seed_from_u64 */
+
+typedef struct {
+  float temperature;
+  float top_p;
+  int32_t top_k;
+  int32_t forbid_token; /* -1 = None */
+} rwkvtts_sample_args;
+
+/* Samples n_rows rows of `logits` (host, n_rows x row_len f32) on the GPU; rng[i] == NULL
+ * mirrors `rng: &mut None` (fixed StdRng(42) draw). rngs advance by one draw per row.
+ * row_len <= 16384 (or top_k in [1, 16384]). out_tokens receives the index per row. */
+int rwkvtts_sample(rwkvtts_engine* e, const float* logits, int n_rows, int row_len,
+                   const rwkvtts_sample_args* args, rwkvtts_rng* const* rngs, int32_t* out_tokens);
+
+/* ---- phase controllers + scheduler ------------------------------------------------------ */
+/* TtsBatchRequest (src/rwkv_sampler.rs:222-231) after tokenisation
+ * (dynamic_batch_manager.rs:512-515) and property-token construction (properties_util.rs:76-98). */
+#define RWKVTTS_MODE_AUTO 0      /* zero-shot iff both ref token sets present (dbm.rs:526-540) */
+typedef struct {
+  const int32_t* text_tokens;
+  int32_t n_text;
+  const int32_t* property_tokens;
+  int32_t n_property;
+  const int32_t* ref_global;   /* NULL = None */
+  int32_t n_ref_global;
+  const int32_t* ref_semantic; /* NULL = None */
+  int32_t n_ref_semantic;
+  int32_t has_seed;
+  uint64_t seed;
+  int32_t max_tokens;          /* SamplerArgs.max_tokens (semantic limit = min(max_tokens, 2048)) */
+  int32_t fixed_semantic;      /* >0: benchmark mode -- EOS masked, exactly this many semantic tokens */
+  int32_t greedy;              /* 1: top_k = 1 for both phases (config 1 plumbing check) */
+} rwkvtts_request;
+
+typedef struct {
+  int32_t status;         /* 0 ok; <0 error -> (vec![], vec![]) as dbm.rs:387-392 */
+  int32_t n_global;
+  int32_t n_semantic;
+  int32_t global_tokens[RWKVTTS_N_GLOBAL];
+  int32_t* semantic_tokens; /* caller buffer, capacity >= RWKVTTS_SEMANTIC_LIMIT */
+} rwkvtts_result;
+
+/* DynamicBatchManager::generate_tts_batch (dynamic_batch_manager.rs:124-164) with real GPU
+ * continuous batching: up to max_slots requests decode together, one slot each. Per-request
+ * outputs are identical to running the requests one at a time. */
+int rwkvtts_generate_batch(rwkvtts_engine* e, const rwkvtts_request* reqs, int n,
+                           rwkvtts_result* results);
+
+/* Step-level statistics of the last generate call (bench / roofline). */
+typedef struct {
+  int64_t steps;            /* decode steps */
+  int64_t prefill_steps;
+  double decode_ms;         /* HIP-event time of all decode steps */
+  double prefill_ms;
+  double sample_ms;         /* sampler kernels inside decode steps */
+  int64_t decode_rows;      /* sum over decode steps of active rows */
+  int32_t profile_kernel_count;
+} rwkvtts_stats;
+int rwkvtts_get_stats(rwkvtts_engine* e, rwkvtts_stats* out);
+
+/* Per-kernel HIP-event timing over the last generate call (enabled by
+ * rwkvtts_set_profiling(e, 1)): name, launches, total ms. */
+int rwkvtts_set_profiling(rwkvtts_engine* e, int on);
+int rwkvtts_profile_entry(rwkvtts_engine* e, int idx, char* name, int name_cap, int64_t* launches,
+                          double* total_ms);
+
+/* ---- codec: BiCodecDetokenize via ORT (lightweight_tts_pipeline.rs:606-622,706-730) ----- */
+typedef struct rwkvtts_codec rwkvtts_codec;
+typedef struct {
+  int32_t codebook_size;  /* 8192 semantic codes */
+  int32_t codebook_dim;   /* 8 */
+  int32_t latent_dim;     /* 1024 */
+  int32_t n_global;       /* 32 speaker tokens */
+  int32_t fsq_levels;     /* 4 (per dim) */
+  int32_t fsq_dims;       /* 6 -> 4^6 = 4096 codes */
+  int32_t spk_dim;        /* d-vector 1024 */
+  int32_t prenet_dim;     /* ConvNeXt dim 384 */
+  int32_t prenet_inter;   /* 2048 */
+  int32_t prenet_layers;  /* 12 */
+  int32_t dec_channels;   /* 1536 */
+  int32_t n_up;           /* 4 */
+  int32_t up_rates[4];    /* 8,5,4,2 */
+  int32_t up_kernels[4];  /* 16,11,8,4 */
+} rwkvtts_codec_dims;
+int64_t rwkvtts_codec_blob_bytes(const rwkvtts_codec_dims* d);
+int rwkvtts_codec_synth_weights(const rwkvtts_codec_dims* d, uint64_t seed, float* out);
+int rwkvtts_codec_create(int device, const rwkvtts_codec_dims* d, const float* weights,
+                         rwkvtts_codec** out);
+int rwkvtts_codec_destroy(rwkvtts_codec* c);
+/* semantic [T] i64, global [n_global] i64 -> pcm [T * 320] f32 (output "wav_rec"). */
+int rwkvtts_codec_decode(rwkvtts_codec* c, const int64_t* semantic, int T, const int64_t* global,
+                         float* pcm);
+/* decode_audio_batch (lightweight_tts_pipeline.rs:625-703): n utterances in one pass. */
+int rwkvtts_codec_decode_batch(rwkvtts_codec* c, const int64_t* const* semantic, const int* T,
+                               const int64_t* const* global, int n, float* const* pcm);
+
+/* ---- zero-shot reference mel (src/tts_pipeline_fixes.rs:12-159) ------------------------- */
+/* wav [n] f32 @16 kHz -> mel [128][n_frames] (n_frames = (n + 1024 - 1024) / 320 + 1). */
+int rwkvtts_mel(int device, const float* wav, int n, float* mel, int* n_frames);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RWKVTTS_H */

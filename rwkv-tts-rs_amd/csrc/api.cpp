@@ -1,0 +1,130 @@
+// api.cpp -- the extern "C" boundary (include/rwkvtts.h). Each entry point wraps one engine
+// method; errors become status codes + a thread-local message, never C++ exceptions.
+#include <string.h>
+
+#include <new>
+
+#include "engine.h"
+
+namespace rwkvtts {
+static thread_local std::string g_last_error;
+void set_error(const std::string& msg) { g_last_error = msg; }
+}  // namespace rwkvtts
+
+using namespace rwkvtts;
+
+struct rwkvtts_engine {
+  Engine eng;
+};
+
+#define GUARD(body)                                      \
+  try {                                                  \
+    body                                                 \
+  } catch (const std::bad_alloc&) {                      \
+    set_error("out of host memory");                     \
+    return RWKVTTS_ENOMEM;                               \
+  } catch (const std::exception& ex) {                   \
+    set_error(ex.what());                                \
+    return RWKVTTS_EINVAL;                               \
+  }
+
+extern "C" {
+
+const char* rwkvtts_last_error(void) { return g_last_error.c_str(); }
+
+int rwkvtts_engine_create(const rwkvtts_engine_desc* desc, const void* weights, size_t bytes,
+                          int blob_on_device, rwkvtts_engine** out) {
+  GUARD({
+    RT_CHECK(desc && weights && out, RWKVTTS_EINVAL, "engine_create: null argument");
+    *out = nullptr;
+    rwkvtts_engine* e = new rwkvtts_engine();
+    const int rc = e->eng.init(*desc, weights, bytes, blob_on_device);
+    if (rc != RWKVTTS_OK) {
+      delete e;
+      return rc;
+    }
+    *out = e;
+    return RWKVTTS_OK;
+  })
+}
+
+int rwkvtts_engine_destroy(rwkvtts_engine* e) {
+  delete e;
+  return RWKVTTS_OK;
+}
+
+int rwkvtts_engine_dims(const rwkvtts_engine* e, rwkvtts_dims* out) {
+  RT_CHECK(e && out, RWKVTTS_EINVAL, "null argument");
+  *out = e->eng.dims;
+  return RWKVTTS_OK;
+}
+
+int64_t rwkvtts_state_floats(const rwkvtts_engine* e) { return e ? e->eng.state_floats() : -1; }
+
+int rwkvtts_slot_reset(rwkvtts_engine* e, int slot) {
+  RT_CHECK(e, RWKVTTS_EINVAL, "null engine");
+  GUARD({ return e->eng.slot_reset(slot); })
+}
+int rwkvtts_slot_read(rwkvtts_engine* e, int slot, float* out) {
+  RT_CHECK(e && out, RWKVTTS_EINVAL, "null argument");
+  GUARD({ return e->eng.slot_read(slot, out); })
+}
+int rwkvtts_slot_write(rwkvtts_engine* e, int slot, const float* in) {
+  RT_CHECK(e && in, RWKVTTS_EINVAL, "null argument");
+  GUARD({ return e->eng.slot_write(slot, in); })
+}
+
+int rwkvtts_infer(rwkvtts_engine* e, const rwkvtts_input* inputs, int n_inputs, int head_rows,
+                  float* logits, int32_t* consumed, int32_t* has_logits) {
+  RT_CHECK(e && inputs && consumed && has_logits && n_inputs > 0, RWKVTTS_EINVAL, "infer: bad arguments");
+  GUARD({ return e->eng.infer(inputs, n_inputs, head_rows, logits, consumed, has_logits); })
+}
+
+int rwkvtts_sample(rwkvtts_engine* e, const float* logits, int n_rows, int row_len,
+                   const rwkvtts_sample_args* args, rwkvtts_rng* const* rngs, int32_t* out_tokens) {
+  RT_CHECK(e && logits && args && out_tokens, RWKVTTS_EINVAL, "sample: bad arguments");
+  GUARD({ return e->eng.sample(logits, n_rows, row_len, args, rngs, out_tokens); })
+}
+
+int rwkvtts_generate_batch(rwkvtts_engine* e, const rwkvtts_request* reqs, int n,
+                           rwkvtts_result* results) {
+  RT_CHECK(e && reqs && results && n >= 0, RWKVTTS_EINVAL, "generate_batch: bad arguments");
+  GUARD({
+    const int rc = e->eng.generate(reqs, n, results);
+    if (rc != RWKVTTS_OK)
+      for (int i = 0; i < n; ++i) {  // dynamic_batch_manager.rs:387-392: errors -> empty results
+        results[i].status = rc;
+        results[i].n_global = results[i].n_semantic = 0;
+      }
+    return rc;
+  })
+}
+
+int rwkvtts_get_stats(rwkvtts_engine* e, rwkvtts_stats* out) {
+  RT_CHECK(e && out, RWKVTTS_EINVAL, "null argument");
+  *out = e->eng.stats;
+  out->profile_kernel_count = (int32_t)e->eng.prof.size();
+  return RWKVTTS_OK;
+}
+
+int rwkvtts_set_profiling(rwkvtts_engine* e, int on) {
+  RT_CHECK(e, RWKVTTS_EINVAL, "null engine");
+  e->eng.profiling = on != 0;
+  e->eng.prof.clear();
+  return RWKVTTS_OK;
+}
+
+int rwkvtts_profile_entry(rwkvtts_engine* e, int idx, char* name, int name_cap, int64_t* launches,
+                          double* total_ms) {
+  RT_CHECK(e && idx >= 0 && idx < (int)e->eng.prof.size(), RWKVTTS_EINVAL, "profile index out of range");
+  const ProfEntry& p = e->eng.prof[idx];
+  if (name && name_cap > 0) {
+    strncpy(name, p.name.c_str(), name_cap - 1);
+    name[name_cap - 1] = 0;
+  }
+  if (launches) *launches = p.launches;
+  if (total_ms) *total_ms = p.ms;
+  return RWKVTTS_OK;
+}
+
+}  // extern "C"

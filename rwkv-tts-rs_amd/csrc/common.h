@@ -1,0 +1,65 @@
+// common.h -- shared host/device helpers for the MI355X (gfx950) RWKV-TTS hot path.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#include "../../include/rwkvtts.h"
+
+namespace rwkvtts {
+
+// ---- error handling across the C ABI -------------------------------------------------
+void set_error(const std::string& msg);
+#define RT_HIP(expr)                                                                  \
+  do {                                                                               \
+    hipError_t _e = (expr);                                                          \
+    if (_e != hipSuccess) {                                                          \
+      ::rwkvtts::set_error(std::string(#expr) + ": " + hipGetErrorString(_e) + " @" + \
+                           __FILE__ + ":" + std::to_string(__LINE__));               \
+      return RWKVTTS_EHIP;                                                           \
+    }                                                                                \
+  } while (0)
+#define RT_CHECK(cond, code, msg)     \
+  do {                                \
+    if (!(cond)) {                    \
+      ::rwkvtts::set_error(msg);      \
+      return code;                    \
+    }                                 \
+  } while (0)
+
+// ---- numeric helpers -------------------------------------------------------------------
+typedef uint16_t bf16_t;
+typedef short short8 __attribute__((ext_vector_type(8)));
+typedef float float4_ __attribute__((ext_vector_type(4)));
+
+__host__ __device__ inline float as_f32(uint32_t u) { return __builtin_bit_cast(float, u); }
+__host__ __device__ inline uint32_t as_u32(float f) { return __builtin_bit_cast(uint32_t, f); }
+__host__ __device__ inline float bf16_to_f32(uint16_t h) { return as_f32((uint32_t)h << 16); }
+// round-to-nearest-even f32 -> bf16 (finite inputs)
+__host__ __device__ inline uint16_t f32_to_bf16(float f) {
+  uint32_t u = as_u32(f);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+__host__ __device__ inline float f16_to_f32(uint16_t h) {
+  uint32_t s = (uint32_t)(h >> 15) << 31, e = (h >> 10) & 31, m = h & 1023, u;
+  if (e == 0) {
+    if (m == 0) {
+      u = s;
+    } else {
+      int sh = 0;
+      while (!(m & 1024)) { m <<= 1; ++sh; }
+      m &= 1023;
+      u = s | ((uint32_t)(127 - 15 - sh + 1) << 23) | (m << 13);
+    }
+  } else if (e == 31) {
+    u = s | 0x7f800000u | (m << 13);
+  } else {
+    u = s | ((e + 112) << 23) | (m << 13);
+  }
+  return as_f32(u);
+}
+
+inline int64_t align_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
+
+}  // namespace rwkvtts

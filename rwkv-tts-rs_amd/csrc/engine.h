@@ -1,0 +1,115 @@
+// engine.h -- MI355X engine: SharedRwkvRuntime + v7::Bundle + TokioRuntime<Rnn> of the
+// reference (src/shared_runtime.rs:23-284) re-designed as one owner thread per GPU with
+// device-resident state slots, ragged-batch forward steps and hipGraph-replayed decode steps.
+#pragma once
+#include <map>
+#include <string>
+#include <vector>
+
+#include "lm_kernels.h"
+#include "sampler.h"
+
+namespace rwkvtts {
+
+struct LayerW {
+  const float *ln1_w, *ln1_b, *ln2_w, *ln2_b;
+  const float* mu[6];  // x_r x_w x_k x_v x_a x_g
+  const float *w0, *a0, *v0, *k_k, *k_a, *r_k, *lnx_w, *lnx_b, *ffn_xk;
+  const bf16_t *wr, *wk, *wv, *wo, *w1t, *a1t, *v1t, *g1t, *w2t, *a2t, *v2t, *g2t, *ffn_k, *ffn_v;
+};
+
+// One forward step description (host side).
+struct StepPlan {
+  std::vector<uint32_t> tok;   // per row
+  std::vector<int4> rows;      // slot, flags, prev_row, 0
+  std::vector<int4> segs;      // slot, row_begin, n_rows, 0
+  std::vector<int> lg_rows;    // rows whose logits are produced
+  std::vector<int> lg_slot;    // slot of each logits row (advance)
+  int head_rows = 0;
+  bool tok_from_ctrl = false;  // decode: token = ctrl[slot].next_token
+  bool advance = false;        // run the phase controller on the logits rows
+};
+
+struct ProfEntry {
+  std::string name;
+  int64_t launches = 0;
+  double ms = 0.0;
+};
+
+class Engine {
+ public:
+  Engine() = default;
+  ~Engine();
+  int init(const rwkvtts_engine_desc& desc, const void* weights, size_t bytes, int on_device);
+
+  int slot_reset(int slot);
+  int slot_read(int slot, float* out);
+  int slot_write(int slot, const float* in);
+  int64_t state_floats() const;
+
+  int infer(const rwkvtts_input* in, int n, int head_rows, float* logits, int32_t* consumed,
+            int32_t* has_logits);
+  int sample(const float* logits, int n_rows, int row_len, const rwkvtts_sample_args* args,
+             rwkvtts_rng* const* rngs, int32_t* out);
+  int generate(const rwkvtts_request* reqs, int n, rwkvtts_result* res);
+
+  rwkvtts_dims dims{};
+  rwkvtts_stats stats{};
+  bool profiling = false;
+  std::vector<ProfEntry> prof;
+
+ private:
+  int run_step(const StepPlan& p, bool upload);
+  int launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_from_ctrl, bool advance);
+  int upload_plan(const StepPlan& p);
+  void prof_begin(hipEvent_t* ev);
+  void prof_end(const char* name, hipEvent_t ev);
+  int flush_prof();
+
+  int device_ = 0;
+  hipStream_t stream_ = nullptr;
+  int S_ = 0, Rmax_ = 0, chunk_ = 0, H_ = 0, Vpad_ = 0, Dtot_ = 0, ldA_ = 0;
+  int splitA_ = 1, splitO_ = 1, splitF_ = 1;
+  bool use_graphs_ = true;
+  uint8_t* wblob_ = nullptr;
+  const bf16_t* emb_ = nullptr;
+  const bf16_t* head_ = nullptr;
+  const float *ln0_w_ = nullptr, *ln0_b_ = nullptr, *lnout_w_ = nullptr, *lnout_b_ = nullptr;
+  std::vector<LayerW> L_;
+  // state
+  float* wkv_ = nullptr;     // [S][L][H][N][N]
+  float* att_sh_ = nullptr;  // [2][S][L][C]
+  float* ffn_sh_ = nullptr;  // [2][S][L][C]
+  int* slot_par_ = nullptr;  // [S]
+  std::vector<int> par_host_;
+  // per-step tables
+  uint32_t* d_tok_ = nullptr;
+  int4* d_rows_ = nullptr;
+  int4* d_segs_ = nullptr;
+  int* d_lg_rows_ = nullptr;
+  int* d_lg_slot_ = nullptr;
+  // scratch
+  float *h0_ = nullptr, *h1_ = nullptr, *partA_ = nullptr, *partO_ = nullptr, *partF_ = nullptr,
+        *vfirst_ = nullptr, *logits_ = nullptr;
+  bf16_t *xm_hi_ = nullptr, *xm_lo_ = nullptr, *z_hi_ = nullptr, *z_lo_ = nullptr,
+         *xf_hi_ = nullptr, *xf_lo_ = nullptr, *kf_hi_ = nullptr, *kf_lo_ = nullptr,
+         *xo_hi_ = nullptr, *xo_lo_ = nullptr;
+  // controller
+  SlotCtrl* d_ctrl_ = nullptr;
+  int32_t* d_sem_ = nullptr;
+  SlotCtrl* h_ctrl_ = nullptr;  // pinned mirror
+  // sampler API scratch
+  float* d_samp_logits_ = nullptr;
+  int samp_cap_ = 0;
+  uint32_t* d_keys_ = nullptr;
+  uint64_t* d_draws_ = nullptr;
+  int32_t* d_out_ = nullptr;
+  // graphs keyed by (R, head_rows)
+  std::map<std::pair<int, int>, hipGraphExec_t> graphs_;
+  std::vector<std::pair<std::string, hipEvent_t>> pending_prof_;
+  std::vector<void*> allocs_;
+  template <typename T>
+  int alloc(T** p, size_t count);
+};
+
+}  // namespace rwkvtts

@@ -1,0 +1,763 @@
+// engine.cpp -- device memory layout, forward-step launcher, hipGraph cache, LM runtime API
+// (Runtime<Rnn>::infer semantics) and the continuous-batching scheduler that replaces
+// DynamicBatchManager's sequential slot-0 loop (src/dynamic_batch_manager.rs:409-551).
+#include "engine.h"
+
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+#include <deque>
+#include <random>
+
+namespace rwkvtts {
+
+template <typename T>
+int Engine::alloc(T** p, size_t count) {
+  void* q = nullptr;
+  RT_HIP(hipMalloc(&q, std::max<size_t>(count * sizeof(T), 256)));
+  RT_HIP(hipMemset(q, 0, std::max<size_t>(count * sizeof(T), 256)));
+  allocs_.push_back(q);
+  *p = (T*)q;
+  return RWKVTTS_OK;
+}
+
+Engine::~Engine() {
+  hipSetDevice(device_);
+  if (stream_) hipStreamSynchronize(stream_);
+  for (auto& g : graphs_) hipGraphExecDestroy(g.second);
+  for (auto& e : pending_prof_) hipEventDestroy(e.second);
+  for (void* p : allocs_) hipFree(p);
+  if (h_ctrl_) hipHostFree(h_ctrl_);
+  if (stream_) hipStreamDestroy(stream_);
+}
+
+#define RT_OK(x)                      \
+  do {                                \
+    int _r = (x);                     \
+    if (_r != RWKVTTS_OK) return _r;  \
+  } while (0)
+
+int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t bytes, int on_device) {
+  device_ = desc.device;
+  RT_HIP(hipSetDevice(device_));
+  RT_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  rwkvtts_blob_header hdr;
+  if (on_device) {
+    RT_HIP(hipMemcpy(&hdr, weights, sizeof(hdr), hipMemcpyDeviceToHost));
+  } else {
+    memcpy(&hdr, weights, sizeof(hdr));
+  }
+  RT_CHECK(hdr.magic == RWKVTTS_BLOB_MAGIC, RWKVTTS_EINVAL, "weight blob: bad magic");
+  RT_CHECK(hdr.dtype == RWKVTTS_DTYPE_BF16, RWKVTTS_EUNSUPPORTED,
+           "GPU path supports bf16 matrices (f16 blobs: convert with rwkvtts.weights)");
+  dims = hdr.dims;
+  const int C = dims.n_embd, F = dims.n_ffn;
+  RT_CHECK(dims.head_size == 64, RWKVTTS_EUNSUPPORTED, "head_size must be 64");
+  RT_CHECK(C % 128 == 0 && C <= 256 * kMaxPerThread, RWKVTTS_EUNSUPPORTED, "n_embd must be a multiple of 128, <= 2048");
+  RT_CHECK(F % 128 == 0, RWKVTTS_EUNSUPPORTED, "n_ffn must be a multiple of 128");
+  Dtot_ = dims.d_decay + dims.d_aaa + dims.d_mv + dims.d_gate;
+  RT_CHECK(Dtot_ <= kMaxLoraTotal && dims.d_decay % 16 == 0 && dims.d_aaa % 16 == 0 &&
+               dims.d_mv % 16 == 0 && dims.d_gate % 16 == 0,
+           RWKVTTS_EUNSUPPORTED, "LoRA ranks must be multiples of 16, total <= 512");
+  RT_CHECK((size_t)rwkvtts_blob_bytes(&dims) <= bytes, RWKVTTS_EINVAL, "weight blob too small");
+  H_ = C / 64;
+  Vpad_ = (int)align_up(dims.n_vocab, 16);
+  ldA_ = 3 * C + Dtot_;
+  S_ = std::max(1, desc.max_slots);
+  chunk_ = desc.token_chunk_size > 0 ? desc.token_chunk_size : 512;
+  Rmax_ = (int)align_up(std::max(chunk_, S_), 64);
+  use_graphs_ = desc.use_graphs != 0;
+  splitA_ = C >= 512 ? 2 : 1;
+  splitO_ = C >= 1024 ? 4 : (C >= 512 ? 2 : 1);
+  splitF_ = F >= 2048 ? 4 : (F >= 1024 ? 2 : 1);
+
+  // weights
+  const size_t wbytes = (size_t)rwkvtts_blob_bytes(&dims);
+  RT_OK(alloc(&wblob_, wbytes));
+  RT_HIP(hipMemcpy(wblob_, weights, wbytes, on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice));
+  auto T = [&](int l, int t) { return (const void*)(wblob_ + rwkvtts_tensor_offset(&dims, l, t)); };
+  emb_ = (const bf16_t*)T(-1, RWKVTTS_T_EMB);
+  head_ = (const bf16_t*)T(-1, RWKVTTS_T_HEAD);
+  ln0_w_ = (const float*)T(-1, RWKVTTS_T_LN0_W);
+  ln0_b_ = (const float*)T(-1, RWKVTTS_T_LN0_B);
+  lnout_w_ = (const float*)T(-1, RWKVTTS_T_LNOUT_W);
+  lnout_b_ = (const float*)T(-1, RWKVTTS_T_LNOUT_B);
+  L_.resize(dims.n_layer);
+  for (int l = 0; l < dims.n_layer; ++l) {
+    LayerW& w = L_[l];
+    auto Fv = [&](int t) { return (const float*)T(l, t); };
+    auto Mv = [&](int t) { return (const bf16_t*)T(l, t); };
+    w.ln1_w = Fv(RWKVTTS_L_LN1_W); w.ln1_b = Fv(RWKVTTS_L_LN1_B);
+    w.ln2_w = Fv(RWKVTTS_L_LN2_W); w.ln2_b = Fv(RWKVTTS_L_LN2_B);
+    w.mu[0] = Fv(RWKVTTS_L_XR); w.mu[1] = Fv(RWKVTTS_L_XW); w.mu[2] = Fv(RWKVTTS_L_XK);
+    w.mu[3] = Fv(RWKVTTS_L_XV); w.mu[4] = Fv(RWKVTTS_L_XA); w.mu[5] = Fv(RWKVTTS_L_XG);
+    w.w0 = Fv(RWKVTTS_L_W0); w.a0 = Fv(RWKVTTS_L_A0); w.v0 = Fv(RWKVTTS_L_V0);
+    w.k_k = Fv(RWKVTTS_L_KK); w.k_a = Fv(RWKVTTS_L_KA); w.r_k = Fv(RWKVTTS_L_RK);
+    w.lnx_w = Fv(RWKVTTS_L_LNX_W); w.lnx_b = Fv(RWKVTTS_L_LNX_B); w.ffn_xk = Fv(RWKVTTS_L_FFN_XK);
+    w.wr = Mv(RWKVTTS_L_WR); w.wk = Mv(RWKVTTS_L_WK); w.wv = Mv(RWKVTTS_L_WV); w.wo = Mv(RWKVTTS_L_WO);
+    w.w1t = Mv(RWKVTTS_L_W1T); w.a1t = Mv(RWKVTTS_L_A1T); w.v1t = Mv(RWKVTTS_L_V1T); w.g1t = Mv(RWKVTTS_L_G1T);
+    w.w2t = Mv(RWKVTTS_L_W2T); w.a2t = Mv(RWKVTTS_L_A2T); w.v2t = Mv(RWKVTTS_L_V2T); w.g2t = Mv(RWKVTTS_L_G2T);
+    w.ffn_k = Mv(RWKVTTS_L_FFN_K); w.ffn_v = Mv(RWKVTTS_L_FFN_V);
+  }
+  // state
+  const int64_t Lc = dims.n_layer;
+  RT_OK(alloc(&wkv_, (size_t)S_ * Lc * H_ * 64 * 64));
+  RT_OK(alloc(&att_sh_, (size_t)2 * S_ * Lc * C));
+  RT_OK(alloc(&ffn_sh_, (size_t)2 * S_ * Lc * C));
+  RT_OK(alloc(&slot_par_, (size_t)S_));
+  par_host_.assign(S_, 0);
+  // tables
+  RT_OK(alloc(&d_tok_, (size_t)Rmax_));
+  RT_OK(alloc(&d_rows_, (size_t)Rmax_));
+  RT_OK(alloc(&d_segs_, (size_t)std::max(Rmax_, S_)));
+  RT_OK(alloc(&d_lg_rows_, (size_t)Rmax_));
+  RT_OK(alloc(&d_lg_slot_, (size_t)Rmax_));
+  // scratch
+  const size_t RC = (size_t)Rmax_ * C;
+  RT_OK(alloc(&h0_, RC));
+  RT_OK(alloc(&h1_, RC));
+  RT_OK(alloc(&xm_hi_, 6 * RC));
+  RT_OK(alloc(&xm_lo_, 6 * RC));
+  RT_OK(alloc(&partA_, (size_t)splitA_ * Rmax_ * ldA_));
+  RT_OK(alloc(&z_hi_, RC));
+  RT_OK(alloc(&z_lo_, RC));
+  RT_OK(alloc(&partO_, (size_t)splitO_ * RC));
+  RT_OK(alloc(&xf_hi_, RC));
+  RT_OK(alloc(&xf_lo_, RC));
+  RT_OK(alloc(&kf_hi_, (size_t)Rmax_ * F));
+  RT_OK(alloc(&kf_lo_, (size_t)Rmax_ * F));
+  RT_OK(alloc(&partF_, (size_t)splitF_ * RC));
+  RT_OK(alloc(&vfirst_, RC));
+  RT_OK(alloc(&xo_hi_, RC));
+  RT_OK(alloc(&xo_lo_, RC));
+  RT_OK(alloc(&logits_, (size_t)Rmax_ * Vpad_));
+  RT_OK(alloc(&d_ctrl_, (size_t)S_));
+  RT_OK(alloc(&d_sem_, (size_t)S_ * RWKVTTS_SEMANTIC_LIMIT));
+  RT_HIP(hipHostMalloc((void**)&h_ctrl_, sizeof(SlotCtrl) * S_, hipHostMallocDefault));
+  RT_HIP(hipDeviceSynchronize());
+  return RWKVTTS_OK;
+}
+
+int64_t Engine::state_floats() const {
+  const int64_t C = dims.n_embd;
+  return (int64_t)dims.n_layer * (2 * C + (int64_t)H_ * 64 * 64);
+}
+
+int Engine::slot_reset(int slot) {
+  RT_CHECK(slot >= 0 && slot < S_, RWKVTTS_EINVAL, "slot out of range");
+  RT_HIP(hipSetDevice(device_));
+  const int64_t C = dims.n_embd, Lc = dims.n_layer, per = Lc * H_ * 64 * 64;
+  RT_HIP(hipMemsetAsync(wkv_ + slot * per, 0, per * 4, stream_));
+  for (int p = 0; p < 2; ++p) {
+    RT_HIP(hipMemsetAsync(att_sh_ + ((int64_t)p * S_ + slot) * Lc * C, 0, Lc * C * 4, stream_));
+    RT_HIP(hipMemsetAsync(ffn_sh_ + ((int64_t)p * S_ + slot) * Lc * C, 0, Lc * C * 4, stream_));
+  }
+  par_host_[slot] = 0;
+  RT_HIP(hipMemcpyAsync(slot_par_ + slot, &par_host_[slot], 4, hipMemcpyHostToDevice, stream_));
+  RT_HIP(hipStreamSynchronize(stream_));
+  return RWKVTTS_OK;
+}
+
+int Engine::slot_read(int slot, float* out) {
+  RT_CHECK(slot >= 0 && slot < S_, RWKVTTS_EINVAL, "slot out of range");
+  RT_HIP(hipSetDevice(device_));
+  RT_HIP(hipStreamSynchronize(stream_));
+  const int64_t C = dims.n_embd, Lc = dims.n_layer, HNN = (int64_t)H_ * 64 * 64;
+  int par = 0;
+  RT_HIP(hipMemcpy(&par, slot_par_ + slot, 4, hipMemcpyDeviceToHost));
+  for (int64_t l = 0; l < Lc; ++l) {
+    float* o = out + l * (2 * C + HNN);
+    RT_HIP(hipMemcpy(o, att_sh_ + (((int64_t)par * S_ + slot) * Lc + l) * C, C * 4, hipMemcpyDeviceToHost));
+    RT_HIP(hipMemcpy(o + C, wkv_ + ((int64_t)slot * Lc + l) * HNN, HNN * 4, hipMemcpyDeviceToHost));
+    RT_HIP(hipMemcpy(o + C + HNN, ffn_sh_ + (((int64_t)par * S_ + slot) * Lc + l) * C, C * 4, hipMemcpyDeviceToHost));
+  }
+  return RWKVTTS_OK;
+}
+
+int Engine::slot_write(int slot, const float* in) {
+  RT_CHECK(slot >= 0 && slot < S_, RWKVTTS_EINVAL, "slot out of range");
+  RT_HIP(hipSetDevice(device_));
+  RT_HIP(hipStreamSynchronize(stream_));
+  const int64_t C = dims.n_embd, Lc = dims.n_layer, HNN = (int64_t)H_ * 64 * 64;
+  par_host_[slot] = 0;
+  RT_HIP(hipMemcpy(slot_par_ + slot, &par_host_[slot], 4, hipMemcpyHostToDevice));
+  for (int64_t l = 0; l < Lc; ++l) {
+    const float* o = in + l * (2 * C + HNN);
+    RT_HIP(hipMemcpy(att_sh_ + (((int64_t)0 * S_ + slot) * Lc + l) * C, o, C * 4, hipMemcpyHostToDevice));
+    RT_HIP(hipMemcpy(wkv_ + ((int64_t)slot * Lc + l) * HNN, o + C, HNN * 4, hipMemcpyHostToDevice));
+    RT_HIP(hipMemcpy(ffn_sh_ + (((int64_t)0 * S_ + slot) * Lc + l) * C, o + C + HNN, C * 4, hipMemcpyHostToDevice));
+  }
+  return RWKVTTS_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// forward step
+// ------------------------------------------------------------------------------------------
+__global__ void k_prepare_tokens(const int4* rows, const SlotCtrl* ctrl, uint32_t* tok, int R) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < R) tok[r] = (uint32_t)ctrl[rows[r].x].next_token;
+}
+__global__ void k_rows_parity(int4* rows, const int* slot_par, int R) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < R) rows[r].w = slot_par[rows[r].x];
+}
+__global__ void k_flip_parity(const int4* segs, int* slot_par, int n_seg) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s < n_seg) slot_par[segs[s].x] ^= 1;
+}
+
+void Engine::prof_begin(hipEvent_t* ev) {
+  *ev = nullptr;
+  if (!profiling) return;
+  hipEventCreate(ev);
+  hipEventRecord(*ev, stream_);
+}
+void Engine::prof_end(const char* name, hipEvent_t ev) {
+  if (!profiling || !ev) return;
+  hipEvent_t e2;
+  hipEventCreate(&e2);
+  hipEventRecord(e2, stream_);
+  pending_prof_.push_back({std::string(name) + "#begin", ev});
+  pending_prof_.push_back({name, e2});
+}
+int Engine::flush_prof() {
+  if (pending_prof_.empty()) return RWKVTTS_OK;
+  RT_HIP(hipStreamSynchronize(stream_));
+  for (size_t i = 0; i + 1 < pending_prof_.size(); i += 2) {
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, pending_prof_[i].second, pending_prof_[i + 1].second);
+    const std::string& nm = pending_prof_[i + 1].first;
+    auto it = std::find_if(prof.begin(), prof.end(), [&](const ProfEntry& e) { return e.name == nm; });
+    if (it == prof.end()) {
+      prof.push_back({nm, 0, 0.0});
+      it = prof.end() - 1;
+    }
+    it->launches++;
+    it->ms += ms;
+    hipEventDestroy(pending_prof_[i].second);
+    hipEventDestroy(pending_prof_[i + 1].second);
+  }
+  pending_prof_.clear();
+  return RWKVTTS_OK;
+}
+
+int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_from_ctrl, bool advance) {
+  const int C = dims.n_embd, F = dims.n_ffn, Lc = dims.n_layer;
+  hipEvent_t ev;
+  const int nb = (R + 255) / 256;
+  hipLaunchKernelGGL(k_rows_parity, dim3(nb), dim3(256), 0, stream_, d_rows_, slot_par_, R);
+  if (tok_from_ctrl)
+    hipLaunchKernelGGL(k_prepare_tokens, dim3(nb), dim3(256), 0, stream_, d_rows_, d_ctrl_, d_tok_, R);
+  prof_begin(&ev);
+  launch_embed(d_tok_, emb_, ln0_w_, ln0_b_, h0_, R, C, stream_);
+  prof_end("embed", ev);
+  const int64_t RC = (int64_t)Rmax_ * C;
+  for (int l = 0; l < Lc; ++l) {
+    const LayerW& w = L_[l];
+    // ---- att: residual (+ previous layer's ffn partials) -> LN1 -> 6 mixes
+    LnMixArgs m{};
+    m.h_in = h0_;
+    m.h_out = h1_;
+    m.part = partF_;
+    m.n_part = l == 0 ? 0 : splitF_;
+    m.ldp = C;
+    m.part_stride = RC;
+    m.ln_w = w.ln1_w;
+    m.ln_b = w.ln1_b;
+    m.n_mix = 6;
+    for (int i = 0; i < 6; ++i) m.mu[i] = w.mu[i];
+    m.x_hi = xm_hi_;
+    m.x_lo = xm_lo_;
+    m.mix_stride = RC;
+    m.ldx = C;
+    m.shift = att_sh_;
+    m.S = S_;
+    m.L = Lc;
+    m.layer = l;
+    m.C = C;
+    m.rows = d_rows_;
+    m.row_map = nullptr;
+    prof_begin(&ev);
+    launch_ln_mix(m, R, stream_);
+    prof_end("ln_mix_att", ev);
+    // ---- r, k, v, LoRA-down (w, a, v, g) in one launch
+    GemmArgs g{};
+    const bf16_t* Xh[6];
+    const bf16_t* Xl[6];
+    for (int i = 0; i < 6; ++i) { Xh[i] = xm_hi_ + i * RC; Xl[i] = xm_lo_ + i * RC; }
+    // order: r(0) k(2) v(3) then lora: w(1) a(4) v(3) g(5) -- lora packed as one segment per matrix
+    int tiles = 0;
+    auto seg = [&](int idx, const bf16_t* W, int mix, int N, int col_off) {
+      g.seg[idx] = {W, Xh[mix], Xl[mix], C, N, col_off, tiles};
+      tiles += (N + 15) / 16;
+    };
+    g.nseg = 3;
+    seg(0, w.wr, 0, C, 0);
+    seg(1, w.wk, 2, C, C);
+    seg(2, w.wv, 3, C, 2 * C);
+    g.K = C; g.M = R; g.k_split = splitA_; g.kslice = C / splitA_;
+    g.epilogue = kEpiStore; g.out = partA_; g.split_stride = (int64_t)Rmax_ * ldA_; g.ldo = ldA_;
+    prof_begin(&ev);
+    launch_gemm(g, stream_);
+    prof_end("gemm_rkv", ev);
+    GemmArgs gl = g;
+    tiles = 0;
+    gl.nseg = 4;
+    g = gl;
+    seg(0, w.w1t, 1, dims.d_decay, 3 * C);
+    seg(1, w.a1t, 4, dims.d_aaa, 3 * C + dims.d_decay);
+    seg(2, w.v1t, 3, dims.d_mv, 3 * C + dims.d_decay + dims.d_aaa);
+    seg(3, w.g1t, 5, dims.d_gate, 3 * C + dims.d_decay + dims.d_aaa + dims.d_mv);
+    prof_begin(&ev);
+    launch_gemm(g, stream_);
+    prof_end("gemm_lora", ev);
+    // ---- WKV + LoRA-up + GroupNorm + bonus + gate
+    WkvArgs k{};
+    k.part = partA_; k.n_part = splitA_; k.ldp = ldA_; k.part_stride = (int64_t)Rmax_ * ldA_;
+    k.w2t = w.w2t; k.a2t = w.a2t; k.v2t = w.v2t; k.g2t = w.g2t;
+    k.w0 = w.w0; k.a0 = w.a0; k.v0 = w.v0; k.k_k = w.k_k; k.k_a = w.k_a; k.r_k = w.r_k;
+    k.lnx_w = w.lnx_w; k.lnx_b = w.lnx_b;
+    k.state = wkv_; k.slot_stride = (int64_t)Lc * H_ * 64 * 64; k.layer_off = (int64_t)l * H_ * 64 * 64;
+    k.v_first = vfirst_; k.ldv = C; k.z_hi = z_hi_; k.z_lo = z_lo_; k.ldz = C;
+    k.segs = d_segs_; k.layer = l; k.C = C;
+    k.Dw = dims.d_decay; k.Da = dims.d_aaa; k.Dv = dims.d_mv; k.Dg = dims.d_gate;
+    prof_begin(&ev);
+    launch_wkv(k, n_seg, H_, stream_);
+    prof_end("wkv", ev);
+    // ---- output projection (split-K partials)
+    GemmArgs go{};
+    go.nseg = 1;
+    go.seg[0] = {w.wo, z_hi_, z_lo_, C, C, 0, 0};
+    go.K = C; go.M = R; go.k_split = splitO_; go.kslice = C / splitO_;
+    go.epilogue = kEpiStore; go.out = partO_; go.split_stride = RC; go.ldo = C;
+    prof_begin(&ev);
+    launch_gemm(go, stream_);
+    prof_end("gemm_wo", ev);
+    // ---- ffn: residual + Wo partials -> LN2 -> mix
+    LnMixArgs f = m;
+    f.h_in = h1_;
+    f.h_out = h0_;
+    f.part = partO_;
+    f.n_part = splitO_;
+    f.ln_w = w.ln2_w;
+    f.ln_b = w.ln2_b;
+    f.n_mix = 1;
+    f.mu[0] = w.ffn_xk;
+    f.x_hi = xf_hi_;
+    f.x_lo = xf_lo_;
+    f.shift = ffn_sh_;
+    prof_begin(&ev);
+    launch_ln_mix(f, R, stream_);
+    prof_end("ln_mix_ffn", ev);
+    GemmArgs gk{};
+    gk.nseg = 1;
+    gk.seg[0] = {w.ffn_k, xf_hi_, xf_lo_, C, F, 0, 0};
+    gk.K = C; gk.M = R; gk.k_split = 1; gk.kslice = C;
+    gk.epilogue = kEpiRelu2Split; gk.out_hi = kf_hi_; gk.out_lo = kf_lo_; gk.ldo = F;
+    prof_begin(&ev);
+    launch_gemm(gk, stream_);
+    prof_end("gemm_ffn_key", ev);
+    GemmArgs gv{};
+    gv.nseg = 1;
+    gv.seg[0] = {w.ffn_v, kf_hi_, kf_lo_, F, C, 0, 0};
+    gv.K = F; gv.M = R; gv.k_split = splitF_; gv.kslice = F / splitF_;
+    gv.epilogue = kEpiStore; gv.out = partF_; gv.split_stride = RC; gv.ldo = C;
+    prof_begin(&ev);
+    launch_gemm(gv, stream_);
+    prof_end("gemm_ffn_value", ev);
+  }
+  if (n_lg > 0) {
+    LnMixArgs o{};
+    o.h_in = h0_;
+    o.h_out = nullptr;
+    o.part = partF_;
+    o.n_part = splitF_;
+    o.ldp = C;
+    o.part_stride = RC;
+    o.ln_w = lnout_w_;
+    o.ln_b = lnout_b_;
+    o.n_mix = 1;
+    o.x_hi = xo_hi_;
+    o.x_lo = xo_lo_;
+    o.mix_stride = RC;
+    o.ldx = C;
+    o.shift = nullptr;
+    o.C = C;
+    o.row_map = d_lg_rows_;
+    prof_begin(&ev);
+    launch_ln_mix(o, n_lg, stream_);
+    prof_end("ln_out", ev);
+    GemmArgs gh{};
+    gh.nseg = 1;
+    gh.seg[0] = {head_, xo_hi_, xo_lo_, C, head_rows, 0, 0};
+    gh.K = C; gh.M = n_lg; gh.k_split = 1; gh.kslice = C;
+    gh.epilogue = kEpiStore; gh.out = logits_; gh.split_stride = 0; gh.ldo = Vpad_;
+    prof_begin(&ev);
+    launch_gemm(gh, stream_);
+    prof_end("gemm_head", ev);
+    if (advance) {
+      AdvanceArgs a{};
+      a.logits = logits_;
+      a.ld = Vpad_;
+      a.row_slot = d_lg_slot_;
+      a.ctrl = d_ctrl_;
+      a.sem_out = d_sem_;
+      a.n_rows = n_lg;
+      prof_begin(&ev);
+      launch_advance(a, stream_);
+      prof_end("sample_advance", ev);
+    }
+  }
+  hipLaunchKernelGGL(k_flip_parity, dim3((n_seg + 255) / 256), dim3(256), 0, stream_, d_segs_, slot_par_, n_seg);
+  RT_HIP(hipGetLastError());
+  return RWKVTTS_OK;
+}
+
+int Engine::upload_plan(const StepPlan& p) {
+  const int R = (int)p.rows.size();
+  if (!p.tok_from_ctrl) RT_HIP(hipMemcpyAsync(d_tok_, p.tok.data(), R * 4, hipMemcpyHostToDevice, stream_));
+  RT_HIP(hipMemcpyAsync(d_rows_, p.rows.data(), R * sizeof(int4), hipMemcpyHostToDevice, stream_));
+  RT_HIP(hipMemcpyAsync(d_segs_, p.segs.data(), p.segs.size() * sizeof(int4), hipMemcpyHostToDevice, stream_));
+  if (!p.lg_rows.empty()) {
+    RT_HIP(hipMemcpyAsync(d_lg_rows_, p.lg_rows.data(), p.lg_rows.size() * 4, hipMemcpyHostToDevice, stream_));
+    RT_HIP(hipMemcpyAsync(d_lg_slot_, p.lg_slot.data(), p.lg_slot.size() * 4, hipMemcpyHostToDevice, stream_));
+  }
+  return RWKVTTS_OK;
+}
+
+// Runs one forward step. Decode steps (tok_from_ctrl) replay a cached hipGraph.
+int Engine::run_step(const StepPlan& p, bool upload) {
+  const int R = (int)p.rows.size();
+  RT_CHECK(R > 0 && R <= Rmax_, RWKVTTS_EINVAL, "step rows out of range");
+  RT_CHECK(p.head_rows <= Vpad_, RWKVTTS_EINVAL, "head_rows > n_vocab");
+  if (upload) RT_OK(upload_plan(p));
+  const int n_seg = (int)p.segs.size(), n_lg = (int)p.lg_rows.size();
+  if (p.tok_from_ctrl && use_graphs_ && !profiling) {
+    auto key = std::make_pair(R, p.head_rows * 2 + (p.advance ? 1 : 0));
+    auto it = graphs_.find(key);
+    if (it == graphs_.end()) {
+      hipGraph_t graph;
+      RT_HIP(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
+      int rc = launch_forward(R, n_seg, n_lg, p.head_rows, true, p.advance);
+      hipError_t ce = hipStreamEndCapture(stream_, &graph);
+      RT_OK(rc);
+      RT_HIP(ce);
+      hipGraphExec_t exec;
+      RT_HIP(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+      RT_HIP(hipGraphDestroy(graph));
+      it = graphs_.emplace(key, exec).first;
+    }
+    RT_HIP(hipGraphLaunch(it->second, stream_));
+    return RWKVTTS_OK;
+  }
+  RT_OK(launch_forward(R, n_seg, n_lg, p.head_rows, p.tok_from_ctrl, p.advance));
+  return RWKVTTS_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// Runtime<Rnn>::infer
+// ------------------------------------------------------------------------------------------
+int Engine::infer(const rwkvtts_input* in, int n, int head_rows, float* logits, int32_t* consumed,
+                  int32_t* has_logits) {
+  RT_HIP(hipSetDevice(device_));
+  RT_CHECK(head_rows > 0 && head_rows <= dims.n_vocab, RWKVTTS_EINVAL, "head_rows out of range");
+  StepPlan p;
+  p.head_rows = head_rows;
+  int budget = chunk_;
+  std::vector<std::pair<int, int>> out_map;  // (input index, logits row index)
+  for (int i = 0; i < n; ++i) {
+    consumed[i] = 0;
+    has_logits[i] = 0;
+    const rwkvtts_input& b = in[i];
+    RT_CHECK(b.slot >= 0 && b.slot < S_, RWKVTTS_EINVAL, "input slot out of range");
+    for (int j = 0; j < i; ++j)
+      RT_CHECK(in[j].slot != b.slot, RWKVTTS_EINVAL, "two inputs share a slot");
+    const int take = std::min(b.n_tokens, budget);
+    if (take <= 0) continue;
+    const int r0 = (int)p.rows.size();
+    for (int t = 0; t < take; ++t) {
+      RT_CHECK(b.tokens[t] < (uint32_t)dims.n_vocab, RWKVTTS_EINVAL, "token id >= n_vocab");
+      int flags = (t == 0 ? kRowFirst : 0) | (t == take - 1 ? kRowLast : 0);
+      p.rows.push_back(make_int4(b.slot, flags, t == 0 ? -1 : r0 + t - 1, 0));
+      p.tok.push_back(b.tokens[t]);
+      if (b.option == RWKVTTS_OPT_FULL) {
+        p.lg_rows.push_back(r0 + t);
+        p.lg_slot.push_back(b.slot);
+      }
+    }
+    p.segs.push_back(make_int4(b.slot, r0, take, 0));
+    consumed[i] = take;
+    budget -= take;
+    if (b.option == RWKVTTS_OPT_LAST && take == b.n_tokens) {
+      p.lg_rows.push_back(r0 + take - 1);
+      p.lg_slot.push_back(b.slot);
+      out_map.push_back({i, (int)p.lg_rows.size() - 1});
+    } else if (b.option == RWKVTTS_OPT_FULL) {
+      has_logits[i] = 1;
+    }
+  }
+  if (p.rows.empty()) return RWKVTTS_OK;
+  RT_OK(run_step(p, true));
+  const int n_lg = (int)p.lg_rows.size();
+  if (n_lg > 0 && logits) {
+    RT_HIP(hipMemcpy2DAsync(logits, (size_t)head_rows * 4, logits_, (size_t)Vpad_ * 4,
+                            (size_t)head_rows * 4, n_lg, hipMemcpyDeviceToHost, stream_));
+  }
+  RT_HIP(hipStreamSynchronize(stream_));
+  for (auto& om : out_map) has_logits[om.first] = 1;
+  RT_OK(flush_prof());
+  return RWKVTTS_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// sample_logits_with_top_p_k on the device
+// ------------------------------------------------------------------------------------------
+int Engine::sample(const float* logits, int n_rows, int row_len, const rwkvtts_sample_args* args,
+                   rwkvtts_rng* const* rngs, int32_t* out) {
+  RT_HIP(hipSetDevice(device_));
+  RT_CHECK(n_rows > 0 && row_len >= 0 && row_len <= kSampleMaxN, RWKVTTS_EINVAL,
+           "sample: row_len must be <= 16384");
+  const size_t need = (size_t)n_rows * std::max(row_len, 1);
+  if ((int)need > samp_cap_) {
+    if (d_samp_logits_) hipFree(d_samp_logits_);
+    if (d_keys_) hipFree(d_keys_);
+    if (d_draws_) hipFree(d_draws_);
+    if (d_out_) hipFree(d_out_);
+    RT_HIP(hipMalloc(&d_samp_logits_, need * 4));
+    RT_HIP(hipMalloc(&d_keys_, (size_t)n_rows * 32 + 256));
+    RT_HIP(hipMalloc(&d_draws_, (size_t)n_rows * 8 + 256));
+    RT_HIP(hipMalloc(&d_out_, (size_t)n_rows * 4 + 256));
+    samp_cap_ = (int)need;
+  }
+  std::vector<uint32_t> keys((size_t)n_rows * 8, 0);
+  std::vector<uint64_t> draws(n_rows, 0);
+  bool any_null = false, all_null = true;
+  for (int i = 0; i < n_rows; ++i) {
+    if (rngs && rngs[i]) {
+      memcpy(&keys[(size_t)i * 8], rngs[i]->key, 32);
+      draws[i] = rngs[i]->draw_index;
+      all_null = false;
+    } else {
+      any_null = true;
+    }
+  }
+  RT_CHECK(all_null || !any_null, RWKVTTS_EINVAL, "sample: mix of NULL and non-NULL rngs");
+  RT_HIP(hipMemcpyAsync(d_samp_logits_, logits, need * 4, hipMemcpyHostToDevice, stream_));
+  RT_HIP(hipMemcpyAsync(d_keys_, keys.data(), keys.size() * 4, hipMemcpyHostToDevice, stream_));
+  RT_HIP(hipMemcpyAsync(d_draws_, draws.data(), draws.size() * 8, hipMemcpyHostToDevice, stream_));
+  SampleRowArgs a{};
+  a.logits = d_samp_logits_;
+  a.ld = row_len;
+  a.n = row_len;
+  a.temperature = args->temperature;
+  a.top_p = args->top_p;
+  a.top_k = args->top_k;
+  a.forbid = args->forbid_token;
+  a.keys = all_null ? nullptr : d_keys_;
+  a.draws = all_null ? nullptr : d_draws_;
+  a.out = d_out_;
+  a.dbg = nullptr;
+  launch_sample_rows(a, n_rows, stream_);
+  RT_HIP(hipGetLastError());
+  RT_HIP(hipMemcpyAsync(out, d_out_, (size_t)n_rows * 4, hipMemcpyDeviceToHost, stream_));
+  RT_HIP(hipStreamSynchronize(stream_));
+  for (int i = 0; i < n_rows; ++i) {
+    RT_CHECK(out[i] >= 0, out[i], "sample: top-p over more than 4096 candidates is unsupported");
+    if (rngs && rngs[i]) rngs[i]->draw_index++;
+  }
+  return RWKVTTS_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// Continuous-batching scheduler (DynamicBatchManager::generate_tts_batch semantics)
+// ------------------------------------------------------------------------------------------
+namespace {
+struct Active {
+  int req;
+  int slot;
+  std::vector<uint32_t> prompt;
+  int prefilled = 0;
+  int advances = 0;  // phase-controller invocations so far
+  bool zero_shot = false;
+  bool done = false;
+};
+}  // namespace
+
+int Engine::generate(const rwkvtts_request* reqs, int n, rwkvtts_result* res) {
+  RT_HIP(hipSetDevice(device_));
+  auto t_start = std::chrono::steady_clock::now();
+  stats = rwkvtts_stats{};
+  std::deque<int> pending;
+  for (int i = 0; i < n; ++i) {
+    pending.push_back(i);
+    res[i].status = 0;
+    res[i].n_global = res[i].n_semantic = 0;
+  }
+  std::vector<int> free_slots;
+  for (int s = S_ - 1; s >= 0; --s) free_slots.push_back(s);
+  std::vector<Active> act;
+  std::random_device rd;
+  hipEvent_t e0, e1;
+  RT_HIP(hipEventCreate(&e0));
+  RT_HIP(hipEventCreate(&e1));
+  double decode_ms = 0, prefill_ms = 0;
+
+  while (!pending.empty() || !act.empty()) {
+    // ---- admit new requests into free slots
+    while (!pending.empty() && !free_slots.empty()) {
+      const int ri = pending.front();
+      pending.pop_front();
+      const rwkvtts_request& q = reqs[ri];
+      const int slot = free_slots.back();
+      free_slots.pop_back();
+      Active a;
+      a.req = ri;
+      a.slot = slot;
+      a.zero_shot = q.ref_global != nullptr && q.ref_semantic != nullptr;
+      for (int i = 0; i < q.n_property; ++i) a.prompt.push_back((uint32_t)q.property_tokens[i]);
+      a.prompt.push_back(RWKVTTS_TAG_2);
+      for (int i = 0; i < q.n_text; ++i) a.prompt.push_back((uint32_t)q.text_tokens[i]);
+      a.prompt.push_back(RWKVTTS_TAG_0);
+      SlotCtrl c;
+      memset(&c, 0, sizeof(c));
+      const uint64_t seed = q.has_seed ? q.seed : (((uint64_t)rd() << 32) ^ rd());
+      rwkvtts_rng rg, rs;
+      rwkvtts_rng_seed_from_u64(seed + 1000, &rg);
+      rwkvtts_rng_seed_from_u64(seed + 2000, &rs);
+      memcpy(c.gkey, rg.key, 32);
+      memcpy(c.skey, rs.key, 32);
+      c.top_k_g = q.greedy ? 1 : 20;
+      c.top_k_s = q.greedy ? 1 : 80;
+      int limit = q.max_tokens > 0 ? std::min(q.max_tokens, RWKVTTS_SEMANTIC_LIMIT) : RWKVTTS_SEMANTIC_LIMIT;
+      if (q.fixed_semantic > 0) limit = std::min(q.fixed_semantic, RWKVTTS_SEMANTIC_LIMIT);
+      c.fixed = q.fixed_semantic > 0;
+      if (a.zero_shot) {
+        c.mode = 1;
+        c.phase = kPhSemantic;
+        for (int i = 0; i < q.n_ref_global; ++i) {
+          const int g = std::min(std::max(q.ref_global[i], 0), 4095);
+          a.prompt.push_back((uint32_t)(g + RWKVTTS_GLOBAL_TOKEN_OFFSET));
+          if (i < RWKVTTS_N_GLOBAL) c.global_out[c.n_global++] = g;
+        }
+        a.prompt.push_back(RWKVTTS_TAG_1);
+        const int tlen = q.n_text;
+        const int min_sem = std::min(std::max(tlen / 4, 8), 64);
+        const int est = (int)ceilf((float)tlen * 1.8f);
+        const int upper = (int)floorf((float)RWKVTTS_SEMANTIC_LIMIT * 0.9f);
+        c.hard_min = std::min(upper, std::max(min_sem, est));
+        c.sem_limit = q.fixed_semantic > 0 ? limit : RWKVTTS_SEMANTIC_LIMIT;
+      } else {
+        c.mode = 0;
+        c.phase = kPhGlobal;
+        c.sem_limit = limit;
+      }
+      for (uint32_t t : a.prompt)
+        RT_CHECK(t < (uint32_t)dims.n_vocab, RWKVTTS_EINVAL, "prompt token id >= n_vocab");
+      RT_OK(slot_reset(slot));
+      RT_HIP(hipMemcpyAsync(d_ctrl_ + slot, &c, sizeof(c), hipMemcpyHostToDevice, stream_));
+      act.push_back(std::move(a));
+    }
+    // ---- prefill steps for slots with pending prompt tokens
+    bool any_prefill = false;
+    for (auto& a : act) any_prefill |= a.prefilled < (int)a.prompt.size();
+    if (any_prefill) {
+      StepPlan p;
+      p.advance = true;
+      p.head_rows = 8193;
+      int budget = chunk_;
+      bool all_global = true;
+      for (auto& a : act) {
+        const int left = (int)a.prompt.size() - a.prefilled;
+        if (left <= 0 || budget <= 0) continue;
+        const int take = std::min(left, budget);
+        const int r0 = (int)p.rows.size();
+        for (int t = 0; t < take; ++t) {
+          const int flags = (t == 0 ? kRowFirst : 0) | (t == take - 1 ? kRowLast : 0);
+          p.rows.push_back(make_int4(a.slot, flags, t == 0 ? -1 : r0 + t - 1, 0));
+          p.tok.push_back(a.prompt[a.prefilled + t]);
+        }
+        p.segs.push_back(make_int4(a.slot, r0, take, 0));
+        a.prefilled += take;
+        budget -= take;
+        if (a.prefilled == (int)a.prompt.size()) {
+          p.lg_rows.push_back(r0 + take - 1);
+          p.lg_slot.push_back(a.slot);
+          a.advances++;
+          all_global &= !a.zero_shot;
+        }
+      }
+      if (all_global) p.head_rows = std::min(4096, dims.n_vocab);
+      p.head_rows = std::min(p.head_rows, dims.n_vocab);
+      RT_HIP(hipEventRecord(e0, stream_));
+      RT_OK(run_step(p, true));
+      RT_HIP(hipEventRecord(e1, stream_));
+      RT_HIP(hipEventSynchronize(e1));
+      float ms = 0;
+      hipEventElapsedTime(&ms, e0, e1);
+      prefill_ms += ms;
+      stats.prefill_steps++;
+      RT_OK(flush_prof());
+      continue;
+    }
+    // ---- decode steps over all active slots until one finishes
+    StepPlan p;
+    p.tok_from_ctrl = true;
+    p.advance = true;
+    for (auto& a : act) {
+      const int r = (int)p.rows.size();
+      p.rows.push_back(make_int4(a.slot, kRowFirst | kRowLast, -1, 0));
+      p.segs.push_back(make_int4(a.slot, r, 1, 0));
+      p.lg_rows.push_back(r);
+      p.lg_slot.push_back(a.slot);
+    }
+    RT_OK(upload_plan(p));
+    const int R = (int)p.rows.size();
+    bool finished = false;
+    while (!finished) {
+      // head rows: 4096 while every slot samples global tokens (or feeds g31), else 8193
+      bool all_global = true;
+      for (auto& a : act) all_global &= !a.zero_shot && a.advances <= RWKVTTS_N_GLOBAL;
+      p.head_rows = std::min(all_global ? 4096 : 8193, dims.n_vocab);
+      RT_HIP(hipEventRecord(e0, stream_));
+      RT_OK(run_step(p, false));
+      for (auto& a : act) a.advances++;
+      RT_HIP(hipMemcpyAsync(h_ctrl_, d_ctrl_, sizeof(SlotCtrl) * S_, hipMemcpyDeviceToHost, stream_));
+      RT_HIP(hipEventRecord(e1, stream_));
+      RT_HIP(hipEventSynchronize(e1));
+      float ms = 0;
+      hipEventElapsedTime(&ms, e0, e1);
+      decode_ms += ms;
+      stats.steps++;
+      stats.decode_rows += R;
+      RT_OK(flush_prof());
+      for (auto& a : act) {
+        if (h_ctrl_[a.slot].phase == kPhDone) finished = true;
+      }
+    }
+    // ---- retire finished slots
+    for (size_t i = 0; i < act.size();) {
+      Active& a = act[i];
+      const SlotCtrl& c = h_ctrl_[a.slot];
+      if (c.phase != kPhDone) { ++i; continue; }
+      rwkvtts_result& r = res[a.req];
+      r.status = 0;
+      r.n_global = c.n_global;
+      memcpy(r.global_tokens, c.global_out, sizeof(int32_t) * RWKVTTS_N_GLOBAL);
+      r.n_semantic = c.n_sem;
+      if (r.semantic_tokens && c.n_sem > 0)
+        RT_HIP(hipMemcpy(r.semantic_tokens, d_sem_ + (int64_t)a.slot * RWKVTTS_SEMANTIC_LIMIT,
+                         sizeof(int32_t) * c.n_sem, hipMemcpyDeviceToHost));
+      free_slots.push_back(a.slot);
+      act.erase(act.begin() + i);
+    }
+  }
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  stats.decode_ms = decode_ms;
+  stats.prefill_ms = prefill_ms;
+  (void)t_start;
+  return RWKVTTS_OK;
+}
+
+}  // namespace rwkvtts

@@ -1,0 +1,85 @@
+// lm_kernels.h -- argument blocks and launchers of the RWKV-7 forward kernels.
+#pragma once
+#include "common.h"
+
+namespace rwkvtts {
+
+constexpr int kMaxPerThread = 8;     // C <= 2048 with 256-thread rows
+constexpr int kMaxLoraTotal = 512;   // Dw + Da + Dv + Dg
+constexpr int kRowFirst = 1;         // row flags
+constexpr int kRowLast = 2;
+constexpr int kEpiStore = 0;
+constexpr int kEpiRelu2Split = 1;
+
+struct LnMixArgs {
+  const float* h_in;   // [R][C]
+  float* h_out;        // nullable
+  const float* part;   // [n_part][R][ldp]
+  int n_part;
+  int ldp;
+  int64_t part_stride;
+  const float* ln_w;
+  const float* ln_b;
+  int n_mix;
+  const float* mu[6];
+  bf16_t* x_hi;        // [n_mix][rows][ldx]
+  bf16_t* x_lo;
+  int64_t mix_stride;
+  int ldx;
+  float* shift;        // [2][S][L][C] or null (ln_out)
+  int S, L, layer, C;
+  const int4* rows;    // per row: slot, flags, prev_row, parity
+  const int* row_map;  // output row -> source row (ln_out) or null
+};
+
+struct GemmSeg {
+  const bf16_t* W;     // [N][K]
+  const bf16_t* Xhi;   // [rows][ldx]
+  const bf16_t* Xlo;
+  int ldx;
+  int N;
+  int col_off;         // output column offset
+  int tile_start;      // first 16-column tile index of this segment
+};
+
+struct GemmArgs {
+  GemmSeg seg[4];
+  int nseg;
+  int K;
+  int M;               // valid rows
+  int k_split;
+  int kslice;          // K / k_split, multiple of 128
+  int epilogue;
+  float* out;          // kEpiStore: [k_split][rows][ldo]
+  int64_t split_stride;
+  int ldo;
+  bf16_t* out_hi;      // kEpiRelu2Split
+  bf16_t* out_lo;
+};
+
+struct WkvArgs {
+  const float* part;   // [n_part][R][ldp]
+  int n_part;
+  int ldp;
+  int64_t part_stride;
+  const bf16_t *w2t, *a2t, *v2t, *g2t;
+  const float *w0, *a0, *v0, *k_k, *k_a, *r_k, *lnx_w, *lnx_b;
+  float* state;
+  int64_t slot_stride;
+  int64_t layer_off;
+  float* v_first;
+  int ldv;
+  bf16_t* z_hi;
+  bf16_t* z_lo;
+  int ldz;
+  const int4* segs;    // slot, row_begin, n_rows, _
+  int layer, C, Dw, Da, Dv, Dg;
+};
+
+void launch_embed(const uint32_t* tokens, const bf16_t* emb, const float* w, const float* b,
+                  float* h, int R, int C, hipStream_t st);
+void launch_ln_mix(const LnMixArgs& a, int n_out_rows, hipStream_t st);
+void launch_gemm(const GemmArgs& a, hipStream_t st);
+void launch_wkv(const WkvArgs& a, int n_seg, int H, hipStream_t st);
+
+}  // namespace rwkvtts

@@ -1,0 +1,146 @@
+"""ctypes binding of include/rwkvtts.h (the C-ABI drop-in boundary).
+
+This is the Python twin of the Rust `extern "C"` block in INTEGRATION.md: same structs, same
+entry points. The product library is loaded from this directory (built in-tree by
+`make -C rwkv-tts-rs_amd/csrc`); there is no fallback -- a missing library is an error.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "librwkvtts.so")
+
+EOS_TOKEN = 8192
+TAG_0, TAG_1, TAG_2 = 8193, 8194, 8195
+GLOBAL_TOKEN_OFFSET = 8196
+SPECIAL_TOKEN_OFFSET = 77823
+N_GLOBAL = 32
+SEMANTIC_LIMIT = 2048
+HOP = 320
+SAMPLE_RATE = 16000
+
+OK, EINVAL, EHIP, ENOMEM, EUNSUPPORTED, EBUSY = 0, -1, -2, -3, -4, -5
+DTYPE_BF16, DTYPE_F16 = 0, 1
+OPT_LAST, OPT_FULL = 0, 1
+
+
+class Dims(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        "n_layer", "n_embd", "head_size", "n_ffn", "n_vocab", "d_decay", "d_aaa", "d_mv", "d_gate")]
+
+
+class EngineDesc(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("max_slots", ctypes.c_int32),
+                ("token_chunk_size", ctypes.c_int32), ("use_graphs", ctypes.c_int32)]
+
+
+class Input(ctypes.Structure):
+    _fields_ = [("slot", ctypes.c_int32), ("tokens", ctypes.POINTER(ctypes.c_uint32)),
+                ("n_tokens", ctypes.c_int32), ("option", ctypes.c_int32)]
+
+
+class Rng(ctypes.Structure):
+    _fields_ = [("key", ctypes.c_uint32 * 8), ("draw_index", ctypes.c_uint64)]
+
+
+class SampleArgs(ctypes.Structure):
+    _fields_ = [("temperature", ctypes.c_float), ("top_p", ctypes.c_float),
+                ("top_k", ctypes.c_int32), ("forbid_token", ctypes.c_int32)]
+
+
+class Request(ctypes.Structure):
+    _fields_ = [("text_tokens", ctypes.POINTER(ctypes.c_int32)), ("n_text", ctypes.c_int32),
+                ("property_tokens", ctypes.POINTER(ctypes.c_int32)), ("n_property", ctypes.c_int32),
+                ("ref_global", ctypes.POINTER(ctypes.c_int32)), ("n_ref_global", ctypes.c_int32),
+                ("ref_semantic", ctypes.POINTER(ctypes.c_int32)), ("n_ref_semantic", ctypes.c_int32),
+                ("has_seed", ctypes.c_int32), ("seed", ctypes.c_uint64),
+                ("max_tokens", ctypes.c_int32), ("fixed_semantic", ctypes.c_int32),
+                ("greedy", ctypes.c_int32)]
+
+
+class Result(ctypes.Structure):
+    _fields_ = [("status", ctypes.c_int32), ("n_global", ctypes.c_int32),
+                ("n_semantic", ctypes.c_int32), ("global_tokens", ctypes.c_int32 * N_GLOBAL),
+                ("semantic_tokens", ctypes.POINTER(ctypes.c_int32))]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("steps", ctypes.c_int64), ("prefill_steps", ctypes.c_int64),
+                ("decode_ms", ctypes.c_double), ("prefill_ms", ctypes.c_double),
+                ("sample_ms", ctypes.c_double), ("decode_rows", ctypes.c_int64),
+                ("profile_kernel_count", ctypes.c_int32)]
+
+
+class CodecDims(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        "codebook_size", "codebook_dim", "latent_dim", "n_global", "fsq_levels", "fsq_dims",
+        "spk_dim", "prenet_dim", "prenet_inter", "prenet_layers", "dec_channels", "n_up")] + [
+        ("up_rates", ctypes.c_int32 * 4), ("up_kernels", ctypes.c_int32 * 4)]
+
+
+# Every symbol include/rwkvtts.h declares (checked by tests/test_abi.py against the header).
+EXPORTS = {
+    "rwkvtts_synth_weights": (ctypes.c_int, [ctypes.POINTER(Dims), ctypes.c_int, ctypes.c_uint64, ctypes.c_void_p]),
+    "rwkvtts_engine_create": (ctypes.c_int, [ctypes.POINTER(EngineDesc), ctypes.c_void_p, ctypes.c_size_t,
+                                             ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    "rwkvtts_engine_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "rwkvtts_last_error": (ctypes.c_char_p, []),
+    "rwkvtts_engine_dims": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Dims)]),
+    "rwkvtts_state_floats": (ctypes.c_int64, [ctypes.c_void_p]),
+    "rwkvtts_slot_reset": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "rwkvtts_slot_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
+    "rwkvtts_slot_write": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
+    "rwkvtts_infer": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Input), ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "rwkvtts_rng_seed_from_u64": (None, [ctypes.c_uint64, ctypes.POINTER(Rng)]),
+    "rwkvtts_sample": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                      ctypes.POINTER(SampleArgs), ctypes.c_void_p, ctypes.c_void_p]),
+    "rwkvtts_generate_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Request), ctypes.c_int,
+                                              ctypes.POINTER(Result)]),
+    "rwkvtts_get_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Stats)]),
+    "rwkvtts_set_profiling": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "rwkvtts_profile_entry": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
+                                             ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)]),
+    "rwkvtts_codec_blob_bytes": (ctypes.c_int64, [ctypes.POINTER(CodecDims)]),
+    "rwkvtts_codec_synth_weights": (ctypes.c_int, [ctypes.POINTER(CodecDims), ctypes.c_uint64, ctypes.c_void_p]),
+    "rwkvtts_codec_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(CodecDims), ctypes.c_void_p,
+                                            ctypes.POINTER(ctypes.c_void_p)]),
+    "rwkvtts_codec_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "rwkvtts_codec_decode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                            ctypes.c_void_p]),
+    "rwkvtts_codec_decode_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                  ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
+    "rwkvtts_mel": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                   ctypes.POINTER(ctypes.c_int)]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load librwkvtts.so (raises if it was not built: the product has no CPU fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is missing: build it with `make -C rwkv-tts-rs_amd/csrc` "
+                               "(the HIP extension is required; there is no CPU fallback)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in EXPORTS.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+class RwkvTtsError(RuntimeError):
+    def __init__(self, rc, where):
+        msg = lib().rwkvtts_last_error()
+        super().__init__(f"{where} failed ({rc}): {msg.decode() if msg else ''}")
+        self.rc = rc
+
+
+def check(rc, where):
+    if rc != OK:
+        raise RwkvTtsError(rc, where)
+    return rc
