@@ -1,0 +1,228 @@
+#!/usr/bin/env python3
+"""bench.py -- audio samples/s for the RWKV-TTS hot path on MI355X (BASELINE.json metric).
+
+One "step" = one full batch of B=32 synthetic requests through the hot path on each GPU
+(config 3 of BASELINE.json): 32-token prompt -> RWKV-7 0.4B prefill -> 32 global tokens ->
+TAG_1 -> 512 semantic tokens (fixed-length benchmark mode, EOS masked) with the exact
+device sampler, continuous batching in 32 GPU slots. Weights are random-init bf16 of the assumed
+0.4B architecture (no checkpoints offline), broadcast from rank 0 over RCCL. value = all ranks'
+audio samples (320 per semantic token @16 kHz) / max-over-ranks wall time.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]; N>1 under torch.distributed.run.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "rwkv-tts-rs_amd"))
+
+import numpy as np  # noqa: E402
+
+B_PER_GPU = 32
+PROMPT_TEXT = 24
+SEMANTIC = 512
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+
+def algorithmic_bytes(d, R, head_rows):
+    """Per-kernel algorithmic HBM bytes of one decode step with R rows."""
+    C, F, L = d["n_embd"], d["n_ffn"], d["n_layer"]
+    H, N = C // 64, 64
+    Dt = d["d_decay"] + d["d_aaa"] + d["d_mv"] + d["d_gate"]
+    act2 = 2 * 2  # bf16 hi + lo planes
+    per = {
+        "gemm_rkv": 3 * C * C * 2 + 3 * R * C * act2 + 3 * R * C * 4,
+        "gemm_lora": Dt * C * 2 + 4 * R * C * act2 + R * Dt * 4,
+        "wkv": R * H * N * N * 4 * 2 + C * Dt * 2 + R * (3 * C + Dt) * 4 + R * C * act2,
+        "gemm_wo": C * C * 2 + R * C * act2 + R * C * 4,
+        "gemm_ffn_key": F * C * 2 + R * C * act2 + R * F * act2,
+        "gemm_ffn_value": C * F * 2 + R * F * act2 + R * C * 4,
+        "ln_mix_att": R * C * 4 * 2 + 6 * R * C * act2 + 2 * R * C * 4,
+        "ln_mix_ffn": R * C * 4 * 2 + R * C * act2 + 2 * R * C * 4,
+    }
+    per_step = {k: v * L for k, v in per.items()}
+    per_step["gemm_head"] = head_rows * C * 2 + R * C * act2 + R * head_rows * 4
+    return per, per_step
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--profile", action="store_true", help="per-kernel HIP-event pass (default on)")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import rwkvtts
+    from rwkvtts import weights as W
+
+    dims = W.DIMS_04B
+    nbytes = W.blob_bytes(dims)
+    # ---- weights: synthesised once on rank 0, broadcast over RCCL (xGMI) to every rank
+    wdev = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    if rank == 0:
+        blob = W.synth_blob(dims, seed=20251205)
+        wdev.copy_(torch.from_numpy(blob))
+        del blob
+    if world > 1:
+        dist.broadcast(wdev, src=0)
+    torch.cuda.synchronize()
+    rt = rwkvtts.SharedRwkvRuntime(nbytes, device=local, max_slots=B_PER_GPU, token_chunk_size=512,
+                                   use_graphs=True, device_ptr=wdev.data_ptr())
+    del wdev
+    torch.cuda.empty_cache()
+
+    def requests(step):
+        reqs = []
+        for i in range(B_PER_GPU):
+            rid = (rank * 1000003 + step * 9176 + i)
+            rs = np.random.RandomState(rid % (2**31))
+            text = rs.randint(12293, 77822, size=PROMPT_TEXT).tolist()
+            props = [77823, 77838, 77869, 77845, 77830, 77826]
+            reqs.append(rwkvtts.TtsBatchRequest(text_tokens=text, property_tokens=props,
+                                                args=rwkvtts.SamplerArgs(seed=rid, max_tokens=2048),
+                                                fixed_semantic=SEMANTIC))
+        return reqs
+
+    def run(step):
+        out = rt.generate_batch(requests(step))
+        return sum(len(s) for _, s in out)
+
+    for w in range(args.warmup):
+        run(-1 - w)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    sem_tokens = 0
+    decode_ms = 0.0
+    dec_steps = 0
+    for s in range(args.steps):
+        sem_tokens += run(s)
+        st = rt.stats()
+        decode_ms += st["decode_ms"]
+        dec_steps += st["steps"]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        n = torch.tensor([sem_tokens], dtype=torch.int64, device="cuda")
+        dist.all_reduce(n, op=dist.ReduceOp.SUM)
+        total_tokens = int(n.item())
+    else:
+        total_tokens = sem_tokens
+    samples = total_tokens * 320
+    value = samples / elapsed
+    audio_s = samples / 16000.0
+    rtf = elapsed / audio_s
+
+    # ---- per-kernel HIP-event pass (same workload, eager launches on the engine's stream)
+    roofline = None
+    kernels = {}
+    step_roof = None
+    if rank == 0:
+        rt.set_profiling(True)
+        run(10**6)
+        prof = rt.profile()
+        rt.set_profiling(False)
+        st = rt.stats()
+        R = B_PER_GPU
+        per_launch, per_step = algorithmic_bytes(dims, R, 8193)
+        for name, (launches, ms) in prof.items():
+            kernels[name] = {"launches": launches, "avg_us": 1000.0 * ms / max(launches, 1), "total_ms": ms}
+        # dominant kernel by total time among the decode-step kernels with a byte model
+        cand = [(v["total_ms"], k) for k, v in kernels.items() if k in per_launch]
+        if cand:
+            _, dom = max(cand)
+            avg_s = kernels[dom]["avg_us"] * 1e-6
+            ach = per_launch[dom] / avg_s / 1e9
+            roofline = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                        "bytes_per_launch": per_launch[dom], "avg_us": round(kernels[dom]["avg_us"], 2)}
+        # whole decode step (graph-replayed timing from the timed region)
+        if dec_steps:
+            step_ms = decode_ms / dec_steps
+            step_bytes = sum(per_step.values())
+            step_roof = {"bytes_per_step": step_bytes, "ms_per_decode_step": round(step_ms, 4),
+                         "achieved": round(step_bytes / (step_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                         "frac": round(step_bytes / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(dims, args.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": "audio samples/sec (16 kHz) for RWKV-TTS 0.4B, batch=32 per GPU",
+            "value": round(value, 1), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(1000.0 * elapsed / args.steps, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic (random-init bf16 weights of the assumed 0.4B RWKV-7 arch, synthetic prompts)",
+            "rtf": round(rtf, 6),
+            "config": {"workload": "config3: 32 requests/GPU, P=32 prompt, 32 global + 512 semantic tokens, "
+                                   "exact sampler, LM only (HIP vocoder not yet in the timed path)",
+                       "global_batch": B_PER_GPU * world, "seq_len": 32 + 33 + SEMANTIC,
+                       "parallelism": f"dp{world} (request sharding)"},
+            "roofline": roofline,
+            "decode_step_roofline": step_roof,
+            "kernels": kernels,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line))
+    rt.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(dims, seconds):
+    """The oracle (C restatement of the reference path, f32 math on bf16 weights, 1 request,
+    OpenMP over the host cores) timed on a bounded sample of the same request, extrapolated to
+    the full request (P + 33 + S - 1 forwards -> 320*S samples)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    from rwkvtts import weights as W
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
+    cores = min(cores, 16)
+    oracle.lib().oracle_set_threads(cores)
+    blob = W.synth_blob(dims, seed=20251205)
+    om = oracle.Model(blob)
+    del blob
+    st = om.new_state()
+    toks = [77823, 77838, 77869, 77845, 77830, 77826, 8195] + list(range(20000, 20024)) + [8193]
+    t0 = time.perf_counter()
+    n = 0
+    while True:
+        tok = toks[n] if n < len(toks) else 8196 + (n % 4096)
+        om.forward(st, tok, 4096 if n >= len(toks) - 1 else 0)
+        n += 1
+        if time.perf_counter() - t0 > seconds or n >= 2000:
+            break
+    per_fwd = (time.perf_counter() - t0) / n
+    fwd_per_req = 32 + 33 + SEMANTIC - 1
+    val = 320 * SEMANTIC / (fwd_per_req * per_fwd)
+    return {"value": round(val, 1), "unit": "samples/s", "cores": cores, "kind": "port",
+            "sample": f"oracle f32 RWKV-7 forward, 1 request, {n} forwards timed ({per_fwd*1e3:.1f} ms each), "
+                      f"extrapolated to {fwd_per_req} forwards / {320*SEMANTIC} samples; LM only"}
+
+
+if __name__ == "__main__":
+    main()
