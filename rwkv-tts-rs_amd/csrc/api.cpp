@@ -86,6 +86,16 @@ int rwkvtts_sample(rwkvtts_engine* e, const float* logits, int n_rows, int row_l
   GUARD({ return e->eng.sample(logits, n_rows, row_len, args, rngs, out_tokens); })
 }
 
+// Test hook (not part of the drop-in surface): same as rwkvtts_sample, also returns the softmax
+// denominator and the uniform draw of every row in dbg[2*i], dbg[2*i+1], followed by
+// n_rows x 16 uint64 phase stamps (dbg must hold n_rows * 34 floats).
+int rwkvtts_debug_sample(rwkvtts_engine* e, const float* logits, int n_rows, int row_len,
+                         const rwkvtts_sample_args* args, rwkvtts_rng* const* rngs, int32_t* out_tokens,
+                         float* dbg) {
+  RT_CHECK(e && logits && args && out_tokens && dbg, RWKVTTS_EINVAL, "debug_sample: bad arguments");
+  GUARD({ return e->eng.sample(logits, n_rows, row_len, args, rngs, out_tokens, dbg); })
+}
+
 int rwkvtts_generate_batch(rwkvtts_engine* e, const rwkvtts_request* reqs, int n,
                            rwkvtts_result* results) {
   RT_CHECK(e && reqs && results && n >= 0, RWKVTTS_EINVAL, "generate_batch: bad arguments");

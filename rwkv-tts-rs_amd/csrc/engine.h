@@ -50,7 +50,7 @@ class Engine {
   int infer(const rwkvtts_input* in, int n, int head_rows, float* logits, int32_t* consumed,
             int32_t* has_logits);
   int sample(const float* logits, int n_rows, int row_len, const rwkvtts_sample_args* args,
-             rwkvtts_rng* const* rngs, int32_t* out);
+             rwkvtts_rng* const* rngs, int32_t* out, float* dbg_host = nullptr);
   int generate(const rwkvtts_request* reqs, int n, rwkvtts_result* res);
 
   rwkvtts_dims dims{};
@@ -69,7 +69,7 @@ class Engine {
   int device_ = 0;
   hipStream_t stream_ = nullptr;
   int S_ = 0, Rmax_ = 0, chunk_ = 0, H_ = 0, Vpad_ = 0, Dtot_ = 0, ldA_ = 0;
-  int splitA_ = 1, splitO_ = 1, splitF_ = 1;
+  int splitA_ = 1, splitO_ = 1, splitK_ = 1, splitF_ = 1, splitH_ = 1;
   bool use_graphs_ = true;
   uint8_t* wblob_ = nullptr;
   const bf16_t* emb_ = nullptr;
@@ -90,9 +90,10 @@ class Engine {
   int* d_lg_slot_ = nullptr;
   // scratch
   float *h0_ = nullptr, *h1_ = nullptr, *partA_ = nullptr, *partO_ = nullptr, *partF_ = nullptr,
+        *partK_ = nullptr,
         *vfirst_ = nullptr, *logits_ = nullptr;
   bf16_t *xm_hi_ = nullptr, *xm_lo_ = nullptr, *z_hi_ = nullptr, *z_lo_ = nullptr,
-         *xf_hi_ = nullptr, *xf_lo_ = nullptr, *kf_hi_ = nullptr, *kf_lo_ = nullptr,
+         *xf_hi_ = nullptr, *xf_lo_ = nullptr,
          *xo_hi_ = nullptr, *xo_lo_ = nullptr;
   // controller
   SlotCtrl* d_ctrl_ = nullptr;

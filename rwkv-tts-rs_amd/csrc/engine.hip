@@ -68,9 +68,18 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
   chunk_ = desc.token_chunk_size > 0 ? desc.token_chunk_size : 512;
   Rmax_ = (int)align_up(std::max(chunk_, S_), 64);
   use_graphs_ = desc.use_graphs != 0;
-  splitA_ = C >= 512 ? 2 : 1;
-  splitO_ = C >= 1024 ? 4 : (C >= 512 ? 2 : 1);
-  splitF_ = F >= 2048 ? 4 : (F >= 1024 ? 2 : 1);
+  // split-K so that every GEMM slice is 128/256/512 deep and the grids fill the 256 CUs
+  auto pick = [](int K, int want) {
+    int ks = std::min(want, K);
+    while (ks > 128 && K % ks) ks >>= 1;
+    return K / ks;
+  };
+  splitA_ = pick(C, 256);   // r,k,v,LoRA-down: 53 col tiles x 4
+  splitO_ = pick(C, 128);   // Wo: 16 col tiles x 8
+  splitK_ = pick(C, 256);   // ffn key: 64 col tiles x 4 (relu^2 applied by the consumer)
+  splitF_ = pick(F, 256);   // ffn value: 16 col tiles x 16
+  splitH_ = pick(C, 512);   // head: 129 col tiles x 2
+  RT_CHECK(C % 128 == 0 && F % 128 == 0, RWKVTTS_EUNSUPPORTED, "K dims must be multiples of 128");
 
   // weights
   const size_t wbytes = (size_t)rwkvtts_blob_bytes(&dims);
@@ -125,13 +134,12 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
   RT_OK(alloc(&partO_, (size_t)splitO_ * RC));
   RT_OK(alloc(&xf_hi_, RC));
   RT_OK(alloc(&xf_lo_, RC));
-  RT_OK(alloc(&kf_hi_, (size_t)Rmax_ * F));
-  RT_OK(alloc(&kf_lo_, (size_t)Rmax_ * F));
+  RT_OK(alloc(&partK_, (size_t)splitK_ * Rmax_ * F));
   RT_OK(alloc(&partF_, (size_t)splitF_ * RC));
   RT_OK(alloc(&vfirst_, RC));
   RT_OK(alloc(&xo_hi_, RC));
   RT_OK(alloc(&xo_lo_, RC));
-  RT_OK(alloc(&logits_, (size_t)Rmax_ * Vpad_));
+  RT_OK(alloc(&logits_, (size_t)splitH_ * Rmax_ * Vpad_));
   RT_OK(alloc(&d_ctrl_, (size_t)S_));
   RT_OK(alloc(&d_sem_, (size_t)S_ * RWKVTTS_SEMANTIC_LIMIT));
   RT_HIP(hipHostMalloc((void**)&h_ctrl_, sizeof(SlotCtrl) * S_, hipHostMallocDefault));
@@ -201,6 +209,14 @@ __global__ void k_prepare_tokens(const int4* rows, const SlotCtrl* ctrl, uint32_
 __global__ void k_rows_parity(int4* rows, const int* slot_par, int R) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r < R) rows[r].w = slot_par[rows[r].x];
+}
+__global__ void k_sum_partials(float* p, int64_t part_stride, int n_part, int ld, int rows, int cols) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)rows * cols) return;
+  const int64_t o = (i / cols) * ld + (i % cols);
+  float v = p[o];
+  for (int q = 1; q < n_part; ++q) v += p[q * part_stride + o];
+  p[o] = v;
 }
 __global__ void k_flip_parity(const int4* segs, int* slot_par, int n_seg) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
@@ -281,37 +297,26 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     prof_begin(&ev);
     launch_ln_mix(m, R, stream_);
     prof_end("ln_mix_att", ev);
-    // ---- r, k, v, LoRA-down (w, a, v, g) in one launch
+    // ---- r, k, v and the LoRA-down projections (w, a, v, g) in one launch (7 segments)
     GemmArgs g{};
-    const bf16_t* Xh[6];
-    const bf16_t* Xl[6];
-    for (int i = 0; i < 6; ++i) { Xh[i] = xm_hi_ + i * RC; Xl[i] = xm_lo_ + i * RC; }
-    // order: r(0) k(2) v(3) then lora: w(1) a(4) v(3) g(5) -- lora packed as one segment per matrix
     int tiles = 0;
     auto seg = [&](int idx, const bf16_t* W, int mix, int N, int col_off) {
-      g.seg[idx] = {W, Xh[mix], Xl[mix], C, N, col_off, tiles};
-      tiles += (N + 15) / 16;
+      g.seg[idx] = {W, xm_hi_ + mix * RC, xm_lo_ + mix * RC, C, N, col_off, tiles};
+      tiles += (N + 63) / 64;
     };
-    g.nseg = 3;
+    g.nseg = 7;
     seg(0, w.wr, 0, C, 0);
     seg(1, w.wk, 2, C, C);
     seg(2, w.wv, 3, C, 2 * C);
+    seg(3, w.w1t, 1, dims.d_decay, 3 * C);
+    seg(4, w.a1t, 4, dims.d_aaa, 3 * C + dims.d_decay);
+    seg(5, w.v1t, 3, dims.d_mv, 3 * C + dims.d_decay + dims.d_aaa);
+    seg(6, w.g1t, 5, dims.d_gate, 3 * C + dims.d_decay + dims.d_aaa + dims.d_mv);
     g.K = C; g.M = R; g.k_split = splitA_; g.kslice = C / splitA_;
-    g.epilogue = kEpiStore; g.out = partA_; g.split_stride = (int64_t)Rmax_ * ldA_; g.ldo = ldA_;
+    g.xmode = kXPlanes; g.out = partA_; g.split_stride = (int64_t)Rmax_ * ldA_; g.ldo = ldA_;
     prof_begin(&ev);
     launch_gemm(g, stream_);
-    prof_end("gemm_rkv", ev);
-    GemmArgs gl = g;
-    tiles = 0;
-    gl.nseg = 4;
-    g = gl;
-    seg(0, w.w1t, 1, dims.d_decay, 3 * C);
-    seg(1, w.a1t, 4, dims.d_aaa, 3 * C + dims.d_decay);
-    seg(2, w.v1t, 3, dims.d_mv, 3 * C + dims.d_decay + dims.d_aaa);
-    seg(3, w.g1t, 5, dims.d_gate, 3 * C + dims.d_decay + dims.d_aaa + dims.d_mv);
-    prof_begin(&ev);
-    launch_gemm(g, stream_);
-    prof_end("gemm_lora", ev);
+    prof_end("gemm_rkv_lora", ev);
     // ---- WKV + LoRA-up + GroupNorm + bonus + gate
     WkvArgs k{};
     k.part = partA_; k.n_part = splitA_; k.ldp = ldA_; k.part_stride = (int64_t)Rmax_ * ldA_;
@@ -330,7 +335,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     go.nseg = 1;
     go.seg[0] = {w.wo, z_hi_, z_lo_, C, C, 0, 0};
     go.K = C; go.M = R; go.k_split = splitO_; go.kslice = C / splitO_;
-    go.epilogue = kEpiStore; go.out = partO_; go.split_stride = RC; go.ldo = C;
+    go.xmode = kXPlanes; go.out = partO_; go.split_stride = RC; go.ldo = C;
     prof_begin(&ev);
     launch_gemm(go, stream_);
     prof_end("gemm_wo", ev);
@@ -353,16 +358,18 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     GemmArgs gk{};
     gk.nseg = 1;
     gk.seg[0] = {w.ffn_k, xf_hi_, xf_lo_, C, F, 0, 0};
-    gk.K = C; gk.M = R; gk.k_split = 1; gk.kslice = C;
-    gk.epilogue = kEpiRelu2Split; gk.out_hi = kf_hi_; gk.out_lo = kf_lo_; gk.ldo = F;
+    gk.K = C; gk.M = R; gk.k_split = splitK_; gk.kslice = C / splitK_;
+    gk.xmode = kXPlanes; gk.out = partK_; gk.split_stride = (int64_t)Rmax_ * F; gk.ldo = F;
     prof_begin(&ev);
     launch_gemm(gk, stream_);
     prof_end("gemm_ffn_key", ev);
     GemmArgs gv{};
     gv.nseg = 1;
-    gv.seg[0] = {w.ffn_v, kf_hi_, kf_lo_, F, C, 0, 0};
+    gv.seg[0] = {w.ffn_v, nullptr, nullptr, F, C, 0, 0};
     gv.K = F; gv.M = R; gv.k_split = splitF_; gv.kslice = F / splitF_;
-    gv.epilogue = kEpiStore; gv.out = partF_; gv.split_stride = RC; gv.ldo = C;
+    gv.xmode = kXRelu2; gv.x_part = partK_; gv.x_nsplit = splitK_; gv.x_ld = F;
+    gv.x_part_stride = (int64_t)Rmax_ * F;
+    gv.out = partF_; gv.split_stride = RC; gv.ldo = C;
     prof_begin(&ev);
     launch_gemm(gv, stream_);
     prof_end("gemm_ffn_value", ev);
@@ -391,8 +398,8 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     GemmArgs gh{};
     gh.nseg = 1;
     gh.seg[0] = {head_, xo_hi_, xo_lo_, C, head_rows, 0, 0};
-    gh.K = C; gh.M = n_lg; gh.k_split = 1; gh.kslice = C;
-    gh.epilogue = kEpiStore; gh.out = logits_; gh.split_stride = 0; gh.ldo = Vpad_;
+    gh.K = C; gh.M = n_lg; gh.k_split = splitH_; gh.kslice = C / splitH_;
+    gh.xmode = kXPlanes; gh.out = logits_; gh.split_stride = (int64_t)Rmax_ * Vpad_; gh.ldo = Vpad_;
     prof_begin(&ev);
     launch_gemm(gh, stream_);
     prof_end("gemm_head", ev);
@@ -400,6 +407,8 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
       AdvanceArgs a{};
       a.logits = logits_;
       a.ld = Vpad_;
+      a.n_part = splitH_;
+      a.part_stride = (int64_t)Rmax_ * Vpad_;
       a.row_slot = d_lg_slot_;
       a.ctrl = d_ctrl_;
       a.sem_out = d_sem_;
@@ -501,6 +510,11 @@ int Engine::infer(const rwkvtts_input* in, int n, int head_rows, float* logits, 
   RT_OK(run_step(p, true));
   const int n_lg = (int)p.lg_rows.size();
   if (n_lg > 0 && logits) {
+    if (splitH_ > 1) {
+      const int64_t tot = (int64_t)n_lg * head_rows;
+      hipLaunchKernelGGL(k_sum_partials, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream_, logits_,
+                         (int64_t)Rmax_ * Vpad_, splitH_, Vpad_, n_lg, head_rows);
+    }
     RT_HIP(hipMemcpy2DAsync(logits, (size_t)head_rows * 4, logits_, (size_t)Vpad_ * 4,
                             (size_t)head_rows * 4, n_lg, hipMemcpyDeviceToHost, stream_));
   }
@@ -514,7 +528,7 @@ int Engine::infer(const rwkvtts_input* in, int n, int head_rows, float* logits, 
 // sample_logits_with_top_p_k on the device
 // ------------------------------------------------------------------------------------------
 int Engine::sample(const float* logits, int n_rows, int row_len, const rwkvtts_sample_args* args,
-                   rwkvtts_rng* const* rngs, int32_t* out) {
+                   rwkvtts_rng* const* rngs, int32_t* out, float* dbg_host) {
   RT_HIP(hipSetDevice(device_));
   RT_CHECK(n_rows > 0 && row_len >= 0 && row_len <= kSampleMaxN, RWKVTTS_EINVAL,
            "sample: row_len must be <= 16384");
@@ -558,8 +572,20 @@ int Engine::sample(const float* logits, int n_rows, int row_len, const rwkvtts_s
   a.draws = all_null ? nullptr : d_draws_;
   a.out = d_out_;
   a.dbg = nullptr;
+  float* d_dbg = nullptr;
+  if (dbg_host) {
+    RT_HIP(hipMalloc(&d_dbg, (size_t)n_rows * (8 + 128)));
+    RT_HIP(hipMemset(d_dbg, 0, (size_t)n_rows * (8 + 128)));
+    a.dbg = d_dbg;
+    a.stamps = (uint64_t*)(d_dbg + 2 * n_rows);
+  }
   launch_sample_rows(a, n_rows, stream_);
   RT_HIP(hipGetLastError());
+  if (dbg_host) {
+    RT_HIP(hipMemcpyAsync(dbg_host, d_dbg, (size_t)n_rows * (8 + 128), hipMemcpyDeviceToHost, stream_));
+    RT_HIP(hipStreamSynchronize(stream_));
+    hipFree(d_dbg);
+  }
   RT_HIP(hipMemcpyAsync(out, d_out_, (size_t)n_rows * 4, hipMemcpyDeviceToHost, stream_));
   RT_HIP(hipStreamSynchronize(stream_));
   for (int i = 0; i < n_rows; ++i) {

@@ -8,8 +8,8 @@ constexpr int kMaxPerThread = 8;     // C <= 2048 with 256-thread rows
 constexpr int kMaxLoraTotal = 512;   // Dw + Da + Dv + Dg
 constexpr int kRowFirst = 1;         // row flags
 constexpr int kRowLast = 2;
-constexpr int kEpiStore = 0;
-constexpr int kEpiRelu2Split = 1;
+constexpr int kXPlanes = 0;  // gemm X: bf16 hi/lo planes
+constexpr int kXRelu2 = 1;   // gemm X: relu(sum of f32 partial slabs)^2
 
 struct LnMixArgs {
   const float* h_in;   // [R][C]
@@ -30,6 +30,7 @@ struct LnMixArgs {
   int S, L, layer, C;
   const int4* rows;    // per row: slot, flags, prev_row, parity
   const int* row_map;  // output row -> source row (ln_out) or null
+  int n_rows;          // set by the launcher
 };
 
 struct GemmSeg {
@@ -39,22 +40,24 @@ struct GemmSeg {
   int ldx;
   int N;
   int col_off;         // output column offset
-  int tile_start;      // first 16-column tile index of this segment
+  int tile_start;      // first 64-column tile index of this segment
 };
 
 struct GemmArgs {
-  GemmSeg seg[4];
+  GemmSeg seg[8];
   int nseg;
   int K;
   int M;               // valid rows
   int k_split;
-  int kslice;          // K / k_split, multiple of 128
-  int epilogue;
-  float* out;          // kEpiStore: [k_split][rows][ldo]
+  int kslice;          // K / k_split in {128, 256, 512}
+  int xmode;           // kXPlanes / kXRelu2
+  const float* x_part; // kXRelu2: [x_nsplit][rows][x_ld] f32 partial slabs
+  int x_nsplit;
+  int x_ld;
+  int64_t x_part_stride;
+  float* out;          // [k_split][rows][ldo] f32
   int64_t split_stride;
   int ldo;
-  bf16_t* out_hi;      // kEpiRelu2Split
-  bf16_t* out_lo;
 };
 
 struct WkvArgs {

@@ -74,187 +74,286 @@ __global__ __launch_bounds__(256) void k_embed(const uint32_t* tokens, const bf1
 }
 
 // ------------------------------------------------------------------------------------
-// ln_mix: hn = h_in + sum(partials); optionally store hn; xx = LN(hn);
-// x_m = xx + (prev - xx) * mu_m (split to bf16 hi/lo); shift state update.
+// ln_mix: one workgroup per row, thread t owns the 4 columns [4t, 4t+4) (x kLnVec chunks of
+// 1024 columns). hn = h_in + sum(partials) (fixed order); optionally store hn; xx = LN(hn);
+// x_m = xx + (prev - xx) * mu_m (split to bf16 hi/lo); shift state update. Latency-bound:
+// every independent load (partials unrolled 4-wide) is issued before the first reduction.
 // ------------------------------------------------------------------------------------
-__device__ inline void load_residual(const LnMixArgs& a, int src, float* v) {
+__device__ inline float4_ ld4(const float* p) { return *(const float4_*)p; }
+
+template <int kLnVec>
+__device__ inline void ln_load_row(const LnMixArgs& a, int src, float4_* v) {
+  const int t4 = 4 * threadIdx.x;
 #pragma unroll
-  for (int i = 0; i < kMaxPerThread; ++i) {
-    const int c = threadIdx.x + i * 256;
-    float x = 0.f;
-    if (c < a.C) {
-      x = a.h_in[(int64_t)src * a.C + c];
-      for (int p = 0; p < a.n_part; ++p) x += a.part[p * a.part_stride + (int64_t)src * a.ldp + c];
+  for (int q = 0; q < kLnVec; ++q) {
+    const int c = t4 + 1024 * q;
+    v[q] = c < a.C ? ld4(a.h_in + (int64_t)src * a.C + c) : (float4_){0.f, 0.f, 0.f, 0.f};
+  }
+  int p = 0;
+  for (; p + 4 <= a.n_part; p += 4) {
+    const float* pp = a.part + p * a.part_stride + (int64_t)src * a.ldp;
+    float4_ t[4][kLnVec];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int q = 0; q < kLnVec; ++q) {
+        const int c = t4 + 1024 * q;
+        t[u][q] = c < a.C ? ld4(pp + u * a.part_stride + c) : (float4_){0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int q = 0; q < kLnVec; ++q) v[q] += t[u][q];
+  }
+  for (; p < a.n_part; ++p) {
+    const float* pp = a.part + p * a.part_stride + (int64_t)src * a.ldp;
+#pragma unroll
+    for (int q = 0; q < kLnVec; ++q) {
+      const int c = t4 + 1024 * q;
+      if (c < a.C) v[q] += ld4(pp + c);
     }
-    v[i] = x;
   }
 }
 
-__device__ inline void layer_norm_regs(const LnMixArgs& a, float* v, float* red) {
+// block (256) sum with one barrier: wave shuffles, then 4 partials through LDS slot `slot`
+__device__ inline float block_sum_1b(float v, float* red, int slot) {
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) red[slot * 4 + (threadIdx.x >> 6)] = v;
+  __syncthreads();
+  return (red[slot * 4 + 0] + red[slot * 4 + 1]) + (red[slot * 4 + 2] + red[slot * 4 + 3]);
+}
+
+template <int kLnVec>
+__device__ inline void ln_apply(const LnMixArgs& a, const float4_* w, const float4_* b, float4_* v,
+                                float* red, int slot) {
   float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < kMaxPerThread; ++i) s += v[i];
-  const float mean = block_sum256(s, red) / (float)a.C;
-  float q = 0.f;
+  for (int q = 0; q < kLnVec; ++q) s += (v[q][0] + v[q][1]) + (v[q][2] + v[q][3]);
+  const float mean = block_sum_1b(s, red, slot) / (float)a.C;
+  float qs = 0.f;
+  const int t4 = 4 * threadIdx.x;
 #pragma unroll
-  for (int i = 0; i < kMaxPerThread; ++i) {
-    const int c = threadIdx.x + i * 256;
-    const float d = c < a.C ? v[i] - mean : 0.f;
-    q += d * d;
-  }
-  const float rstd = 1.0f / sqrtf(block_sum256(q, red) / (float)a.C + 1e-5f);
+  for (int q = 0; q < kLnVec; ++q)
+    if (t4 + 1024 * q < a.C)
 #pragma unroll
-  for (int i = 0; i < kMaxPerThread; ++i) {
-    const int c = threadIdx.x + i * 256;
-    v[i] = c < a.C ? (v[i] - mean) * rstd * a.ln_w[c] + a.ln_b[c] : 0.f;
-  }
+      for (int e = 0; e < 4; ++e) {
+        const float d = v[q][e] - mean;
+        qs += d * d;
+      }
+  const float rstd = 1.0f / sqrtf(block_sum_1b(qs, red, slot + 1) / (float)a.C + 1e-5f);
+#pragma unroll
+  for (int q = 0; q < kLnVec; ++q)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[q][e] = (v[q][e] - mean) * rstd * w[q][e] + b[q][e];
 }
 
+__device__ inline void store_split4(const float4_& x, bf16_t* hi, bf16_t* lo, int64_t idx) {
+  uint16_t h[4], l[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    h[e] = f32_to_bf16(x[e]);
+    l[e] = f32_to_bf16(x[e] - bf16_to_f32(h[e]));
+  }
+  *(uint2*)(hi + idx) = make_uint2(h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16));
+  *(uint2*)(lo + idx) = make_uint2(l[0] | ((uint32_t)l[1] << 16), l[2] | ((uint32_t)l[3] << 16));
+}
+
+template <int kLnVec>  // C <= 1024 * kLnVec
 __global__ __launch_bounds__(256) void k_ln_mix(LnMixArgs a) {
-  __shared__ float red[4];
+  __shared__ float red[16];
   const int out_row = blockIdx.x;
   const int row = a.row_map ? a.row_map[out_row] : out_row;
-  float v[kMaxPerThread];
-  load_residual(a, row, v);
+  const int t4 = 4 * threadIdx.x;
+  const float4_ z = {0.f, 0.f, 0.f, 0.f};
+  float4_ v[kLnVec], w[kLnVec], b[kLnVec], pv[kLnVec], mu[6][kLnVec];
+  int slot = 0, flags = 0, prev_row = -1, par = 0;
+  if (a.shift) {
+    const int4 info = a.rows[row];
+    slot = info.x; flags = info.y; prev_row = info.z; par = info.w;
+  }
+  const float* sh = a.shift ? a.shift + (((int64_t)par * a.S + slot) * a.L + a.layer) * a.C : nullptr;
+#pragma unroll
+  for (int q = 0; q < kLnVec; ++q) {
+    const int c = t4 + 1024 * q;
+    const bool ok = c < a.C;
+    w[q] = ok ? ld4(a.ln_w + c) : z;
+    b[q] = ok ? ld4(a.ln_b + c) : z;
+    pv[q] = (ok && sh && prev_row < 0) ? ld4(sh + c) : z;
+#pragma unroll
+    for (int m = 0; m < 6; ++m) mu[m][q] = (ok && m < a.n_mix && a.mu[m]) ? ld4(a.mu[m] + c) : z;
+  }
+  ln_load_row<kLnVec>(a, row, v);
   if (a.h_out) {
 #pragma unroll
-    for (int i = 0; i < kMaxPerThread; ++i) {
-      const int c = threadIdx.x + i * 256;
-      if (c < a.C) a.h_out[(int64_t)row * a.C + c] = v[i];
+    for (int q = 0; q < kLnVec; ++q) {
+      const int c = t4 + 1024 * q;
+      if (c < a.C) *(float4_*)(a.h_out + (int64_t)row * a.C + c) = v[q];
     }
   }
-  layer_norm_regs(a, v, red);  // v = xx
-  if (!a.shift) {              // ln_out: x = xx
+  ln_apply<kLnVec>(a, w, b, v, red, 0);  // v = xx
+  if (!a.shift) {                        // ln_out: x = xx
 #pragma unroll
-    for (int i = 0; i < kMaxPerThread; ++i) {
-      const int c = threadIdx.x + i * 256;
-      if (c < a.C) split_store(v[i], a.x_hi, a.x_lo, (int64_t)out_row * a.ldx + c);
+    for (int q = 0; q < kLnVec; ++q) {
+      const int c = t4 + 1024 * q;
+      if (c < a.C) store_split4(v[q], a.x_hi, a.x_lo, (int64_t)out_row * a.ldx + c);
     }
     return;
   }
-  const int4 info = a.rows[row];  // slot, flags, prev_row, parity
-  const int slot = info.x, flags = info.y, prev_row = info.z, par = info.w;
-  float pv[kMaxPerThread];
-  if (prev_row >= 0) {
-    load_residual(a, prev_row, pv);
-    layer_norm_regs(a, pv, red);
-  } else {
-    const float* sh = a.shift + (((int64_t)par * a.S + slot) * a.L + a.layer) * a.C;
-#pragma unroll
-    for (int i = 0; i < kMaxPerThread; ++i) {
-      const int c = threadIdx.x + i * 256;
-      pv[i] = c < a.C ? sh[c] : 0.f;
-    }
+  if (prev_row >= 0) {  // prefill row: the previous token's LN output, recomputed identically
+    ln_load_row<kLnVec>(a, prev_row, pv);
+    ln_apply<kLnVec>(a, w, b, pv, red, 2);
   }
-  for (int m = 0; m < a.n_mix; ++m) {
-    const float* mu = a.mu[m];
-    bf16_t* hi = a.x_hi + m * a.mix_stride;
-    bf16_t* lo = a.x_lo + m * a.mix_stride;
 #pragma unroll
-    for (int i = 0; i < kMaxPerThread; ++i) {
-      const int c = threadIdx.x + i * 256;
-      if (c < a.C) split_store(v[i] + (pv[i] - v[i]) * mu[c], hi, lo, (int64_t)out_row * a.ldx + c);
+  for (int m = 0; m < 6; ++m) {
+    if (m >= a.n_mix) break;
+#pragma unroll
+    for (int q = 0; q < kLnVec; ++q) {
+      const int c = t4 + 1024 * q;
+      if (c < a.C) {
+        float4_ x;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[e] = v[q][e] + (pv[q][e] - v[q][e]) * mu[m][q][e];
+        store_split4(x, a.x_hi + m * a.mix_stride, a.x_lo + m * a.mix_stride, (int64_t)out_row * a.ldx + c);
+      }
     }
   }
   if (flags & kRowLast) {
-    float* sh = a.shift + (((int64_t)(par ^ 1) * a.S + slot) * a.L + a.layer) * a.C;
+    float* sn = a.shift + (((int64_t)(par ^ 1) * a.S + slot) * a.L + a.layer) * a.C;
 #pragma unroll
-    for (int i = 0; i < kMaxPerThread; ++i) {
-      const int c = threadIdx.x + i * 256;
-      if (c < a.C) sh[c] = v[i];
+    for (int q = 0; q < kLnVec; ++q) {
+      const int c = t4 + 1024 * q;
+      if (c < a.C) *(float4_*)(sn + c) = v[q];
     }
   }
 }
 
 // ------------------------------------------------------------------------------------
 // gemm: out[split][row][col_off + n] = sum_{k in split} X[row][k] * W[n][k]
-//   X given as bf16 hi/lo planes; W bf16 [N][K] row-major. MFMA 16x16x32 bf16.
-//   Workgroup = 4 waves = 16 output columns x (MT*16) rows x one K slice; the 4 waves split
-//   the slice and their accumulators are summed in LDS in fixed order.
-//   B fragment (lane l): W[col0 + (l&15)][k0 + 8(l>>4) .. +8]  -> one 16-byte load per lane.
-//   A fragment (lane l): X[row0 + (l&15)][k0 + 8(l>>4) .. +8].
+//   W bf16 [N][K] row-major; X as bf16 hi/lo planes (or, mode kXRelu2, relu(sum of f32
+//   partial slabs)^2 split on the fly). MFMA 16x16x32 bf16.
+//   Workgroup = 4 waves = 64 output columns (16 per wave) x MT*16 rows x one K slice.
+//   * every wave issues ALL of its weight loads for the slice first (HBM stream, one 16-byte
+//     load per lane per 32-deep K step: lane l reads W[col0 + (l&15)][k0 + 8(l>>4) .. +8]);
+//   * meanwhile the workgroup stages its X slice into LDS once (shared by the 4 waves);
+//   * A fragments come from LDS (ds_read_b128), B fragments from the registers.
+//   Each wave owns complete output columns: no cross-wave reduction; split-K partial slabs
+//   are summed (fixed order) by the consumer.
 // ------------------------------------------------------------------------------------
-template <int MT>
+template <int MT, int KSTEPS, int XMODE>
 __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
-  __shared__ float red[4 * MT * 4 * 64];
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int KS = KSTEPS * 32;      // K slice
+  constexpr int LD = KS + 8;           // LDS row stride (elements): +16 B breaks bank aliasing
+  constexpr int ROWS = MT * 16;
+  bf16_t* xh = (bf16_t*)smem;
+  bf16_t* xl = xh + ROWS * LD;
   const int tile = blockIdx.x;
   int s = 0;
   while (s + 1 < a.nseg && tile >= a.seg[s + 1].tile_start) ++s;
   const GemmSeg& sg = a.seg[s];
-  const int col0 = (tile - sg.tile_start) * 16;
-  const int split = blockIdx.y;
-  const int row0 = blockIdx.z * (MT * 16);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int g = lane >> 4, li = lane & 15;
-  const int wk = a.kslice >> 2;  // K per wave
-  const int kbeg = split * a.kslice + wave * wk;
+  const int col0 = (tile - sg.tile_start) * 64 + wave * 16;
+  const int split = blockIdx.y;
+  const int kbeg = split * KS;
+  const int row0 = blockIdx.z * ROWS;
+  // 1) weight stream for this wave's 16 columns
   int n = col0 + li;
-  if (n >= sg.N) n = sg.N - 1;  // clamp (result discarded)
+  if (n >= sg.N) n = sg.N - 1;
   const bf16_t* wrow = sg.W + (int64_t)n * a.K + kbeg + g * 8;
-  const bf16_t* xh[MT];
-  const bf16_t* xl[MT];
+  short8 b[KSTEPS];
 #pragma unroll
-  for (int m = 0; m < MT; ++m) {
-    const int64_t ro = (int64_t)(row0 + m * 16 + li) * sg.ldx + kbeg + g * 8;
-    xh[m] = sg.Xhi + ro;
-    xl[m] = sg.Xlo + ro;
+  for (int t = 0; t < KSTEPS; ++t) b[t] = __builtin_nontemporal_load((const short8*)(wrow + t * 32));
+  // 2) stage X slice
+  constexpr int CH = KS / 8;  // 16-byte chunks per row
+  if constexpr (XMODE == kXPlanes) {
+    constexpr int PER = ROWS * CH / 256;  // 16-byte chunks per thread per plane
+    short8 vh[PER], vl[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int c = threadIdx.x + u * 256;
+      const int r = c / CH, k8 = (c % CH) * 8;
+      const int src = row0 + r;
+      vh[u] = vl[u] = (short8){0, 0, 0, 0, 0, 0, 0, 0};
+      if (src < a.M) {
+        const int64_t o = (int64_t)src * sg.ldx + kbeg + k8;
+        vh[u] = *(const short8*)(sg.Xhi + o);
+        vl[u] = *(const short8*)(sg.Xlo + o);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int c = threadIdx.x + u * 256;
+      const int r = c / CH, k8 = (c % CH) * 8;
+      *(short8*)(xh + r * LD + k8) = vh[u];
+      *(short8*)(xl + r * LD + k8) = vl[u];
+    }
+  } else {  // kXRelu2: x = relu(sum_p P[p][row][k])^2, partials summed in order 0..n-1
+    constexpr int PER = ROWS * KS / 4 / 256;  // float4 chunks per thread
+    float4_ x[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) x[u] = (float4_){0.f, 0.f, 0.f, 0.f};
+    for (int p0 = 0; p0 < a.x_nsplit; p0 += 2) {
+      float4_ t[2][PER];
+#pragma unroll
+      for (int pp = 0; pp < 2; ++pp)
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+          const int c = threadIdx.x + u * 256;
+          const int r = c / (KS / 4), k4 = (c % (KS / 4)) * 4;
+          const int src = row0 + r;
+          t[pp][u] = (src < a.M && p0 + pp < a.x_nsplit)
+                         ? *(const float4_*)(a.x_part + (p0 + pp) * a.x_part_stride + (int64_t)src * a.x_ld + kbeg + k4)
+                         : (float4_){0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+      for (int pp = 0; pp < 2; ++pp)
+#pragma unroll
+        for (int u = 0; u < PER; ++u) x[u] += t[pp][u];
+    }
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int c = threadIdx.x + u * 256;
+      const int r = c / (KS / 4), k4 = (c % (KS / 4)) * 4;
+      uint16_t h[4], l[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float y = x[u][e] > 0.f ? x[u][e] * x[u][e] : 0.f;
+        h[e] = f32_to_bf16(y);
+        l[e] = f32_to_bf16(y - bf16_to_f32(h[e]));
+      }
+      *(uint2*)(xh + r * LD + k4) = make_uint2(h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16));
+      *(uint2*)(xl + r * LD + k4) = make_uint2(l[0] | ((uint32_t)l[1] << 16), l[2] | ((uint32_t)l[3] << 16));
+    }
   }
+  __syncthreads();
+  // 3) MFMA over the slice
   float4_ acc[MT];
 #pragma unroll
   for (int m = 0; m < MT; ++m) acc[m] = (float4_){0.f, 0.f, 0.f, 0.f};
-  const int steps = wk >> 5;
-  int t = 0;
-  for (; t + 4 <= steps; t += 4) {
-    short8 b[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) b[u] = *(const short8*)(wrow + (t + u) * 32);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-#pragma unroll
-      for (int m = 0; m < MT; ++m) {
-        const short8 ah = *(const short8*)(xh[m] + (t + u) * 32);
-        const short8 al = *(const short8*)(xl[m] + (t + u) * 32);
-        acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ah),
-                                                         __builtin_bit_cast(bf16x8, b[u]), acc[m], 0, 0, 0);
-        acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, al),
-                                                         __builtin_bit_cast(bf16x8, b[u]), acc[m], 0, 0, 0);
-      }
-    }
-  }
-  for (; t < steps; ++t) {
-    const short8 b = *(const short8*)(wrow + t * 32);
+  for (int t = 0; t < KSTEPS; ++t) {
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
-      const short8 ah = *(const short8*)(xh[m] + t * 32);
-      const short8 al = *(const short8*)(xl[m] + t * 32);
+      const int o = (m * 16 + li) * LD + t * 32 + g * 8;
+      const short8 ah = *(const short8*)(xh + o);
+      const short8 al = *(const short8*)(xl + o);
       acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ah),
-                                                       __builtin_bit_cast(bf16x8, b), acc[m], 0, 0, 0);
+                                                       __builtin_bit_cast(bf16x8, b[t]), acc[m], 0, 0, 0);
       acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, al),
-                                                       __builtin_bit_cast(bf16x8, b), acc[m], 0, 0, 0);
+                                                       __builtin_bit_cast(bf16x8, b[t]), acc[m], 0, 0, 0);
     }
   }
-  // cross-wave reduction: red[w][m][j][lane]
+  // 4) store (D layout: col = lane&15, row = 4*(lane>>4) + j)
+  const int col = col0 + li;
+  if (col < sg.N) {
 #pragma unroll
-  for (int m = 0; m < MT; ++m)
+    for (int m = 0; m < MT; ++m)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) red[((wave * MT + m) * 4 + j) * 64 + lane] = acc[m][j];
-  __syncthreads();
-  const int j = threadIdx.x >> 6;  // reuse: thread -> (j, lane)
-#pragma unroll
-  for (int m = 0; m < MT; ++m) {
-    float v = 0.f;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) v += red[((w * MT + m) * 4 + j) * 64 + lane];
-    const int row = row0 + m * 16 + 4 * g + j;
-    const int col = col0 + li;
-    if (row < a.M && col < sg.N) {
-      if (a.epilogue == kEpiStore) {
-        a.out[split * a.split_stride + (int64_t)row * a.ldo + sg.col_off + col] = v;
-      } else {  // kEpiRelu2Split
-        const float r = v > 0.f ? v : 0.f;
-        split_store(r * r, a.out_hi, a.out_lo, (int64_t)row * a.ldo + sg.col_off + col);
+      for (int j = 0; j < 4; ++j) {
+        const int row = row0 + m * 16 + 4 * g + j;
+        if (row < a.M) a.out[split * a.split_stride + (int64_t)row * a.ldo + sg.col_off + col] = acc[m][j];
       }
-    }
   }
 }
 
@@ -266,86 +365,124 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
 // ------------------------------------------------------------------------------------
 __device__ inline float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
 
-__device__ inline float dot_bf16_row(const bf16_t* w, const float* h, int D) {
-  float acc = 0.f;
-  for (int d = 0; d < D; d += 8) {
-    const short8 q = *(const short8*)(w + d);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) acc += bf16_to_f32((uint16_t)q[e]) * h[d + e];
-  }
-  return acc;
-}
 
 __global__ __launch_bounds__(256) void k_wkv(WkvArgs a) {
   constexpr int N = 64;
   __shared__ float s_hid[kMaxLoraTotal];
   __shared__ float s_r[N], s_k[N], s_v[N], s_w[N], s_kk[N], s_b[N], s_g[N], s_y[N];
   __shared__ float s_lora[4][N];
-  __shared__ float red[4];
+  __shared__ __attribute__((aligned(16))) bf16_t s_lw[N * (kMaxLoraTotal + 8)];
   const int4 sg = a.segs[blockIdx.x];
   const int slot = sg.x, r_begin = sg.y, n_rows = sg.z;
   const int h = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int C = a.C;
+  const int c = h * N + lane;  // this lane's channel (waves 0..3 all index the head's channels)
   const int i = tid >> 2, jq = (tid & 3) * 16;
   float* Sg = a.state + (int64_t)slot * a.slot_stride + a.layer_off + (int64_t)h * N * N + i * N + jq;
+  // ---- prologue: every load that does not depend on this step's activations
   float S[16];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const float4_ v4 = *(const float4_*)(Sg + q * 4);
     S[q * 4 + 0] = v4[0]; S[q * 4 + 1] = v4[1]; S[q * 4 + 2] = v4[2]; S[q * 4 + 3] = v4[3];
   }
+  // LoRA-up: 4 threads per channel (cc = tid >> 2, quarter pq = tid & 3 of each rank D)
+  const int cc = tid >> 2, pq = tid & 3;
+  const int Dv_eff = a.layer > 0 ? a.Dv : 0;
+  const int Dq[4] = {a.Dw / 4, a.Da / 4, Dv_eff / 4, a.Dg / 4};
+  // the head's LoRA-up rows (64 channels x Dtot bf16) staged once into LDS
+  const int Dall = a.Dw + a.Da + a.Dv + a.Dg, LDW = Dall + 8;
+  {
+    const int moff[4] = {0, a.Dw, a.Dw + a.Da, a.Dw + a.Da + a.Dv};
+    const int Dm[4] = {a.Dw, a.Da, a.Dv, a.Dg};
+    const bf16_t* Wb[4] = {a.w2t, a.a2t, a.v2t, a.g2t};
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int ch8 = Dm[m] / 8;  // 16-byte chunks per row
+      for (int q = tid; q < N * ch8; q += 256) {
+        const int ch = q / ch8, k8 = (q % ch8) * 8;
+        *(short8*)(s_lw + ch * LDW + moff[m] + k8) = *(const short8*)(Wb[m] + (int64_t)(h * N + ch) * Dm[m] + k8);
+      }
+    }
+  }
+  float w0 = 0.f, a0 = 0.f, v0 = 0.f, kkc = 0.f, kac = 0.f, rkc = 0.f, lnw = 0.f, lnb = 0.f;
+  if (wave == 0) {
+    w0 = a.w0[c]; a0 = a.a0[c]; v0 = a.v0[c]; kkc = a.k_k[c]; kac = a.k_a[c];
+    rkc = a.r_k[c]; lnw = a.lnx_w[c]; lnb = a.lnx_b[c];
+  }
   const int Dtot = a.Dw + a.Da + a.Dv + a.Dg;
   for (int rr = 0; rr < n_rows; ++rr) {
     const int row = r_begin + rr;
     const float* prow = a.part + (int64_t)row * a.ldp;
-    // LoRA hidden (whole vectors) with activations
-    for (int d = tid; d < Dtot; d += 256) {
-      float x = 0.f;
-      for (int p = 0; p < a.n_part; ++p) x += prow[p * a.part_stride + 3 * C + d];
-      if (d < a.Dw) x = tanhf(x);
-      else if (d >= a.Dw + a.Da + a.Dv) x = sigm(x);
-      s_hid[d] = x;
+    // ---- this row's activations: LoRA hidden (all), r/k/v (wave 0), v_first
+    float hx0 = 0.f, hx1 = 0.f;
+    for (int p = 0; p < a.n_part; ++p) {
+      if (tid < Dtot) hx0 += prow[p * a.part_stride + 3 * C + tid];
+      if (tid + 256 < Dtot) hx1 += prow[p * a.part_stride + 3 * C + tid + 256];
     }
-    __syncthreads();
-    // LoRA up for this head's channels: wave 0: w, 1: a, 2: v, 3: g
-    {
-      const int c = h * N + lane;
-      float acc = 0.f;
-      if (wave == 0) acc = dot_bf16_row(a.w2t + (int64_t)c * a.Dw, s_hid, a.Dw);
-      else if (wave == 1) acc = dot_bf16_row(a.a2t + (int64_t)c * a.Da, s_hid + a.Dw, a.Da);
-      else if (wave == 2) { if (a.layer > 0) acc = dot_bf16_row(a.v2t + (int64_t)c * a.Dv, s_hid + a.Dw + a.Da, a.Dv); }
-      else acc = dot_bf16_row(a.g2t + (int64_t)c * a.Dg, s_hid + a.Dw + a.Da + a.Dv, a.Dg);
-      s_lora[wave][lane] = acc;
-    }
-    __syncthreads();
+    float r = 0.f, k = 0.f, v = 0.f, vf = 0.f;
     if (wave == 0) {
-      const int c = h * N + lane;
-      float r = 0.f, k = 0.f, v = 0.f;
       for (int p = 0; p < a.n_part; ++p) {
         const float* pp = prow + p * a.part_stride;
         r += pp[c];
         k += pp[C + c];
         v += pp[2 * C + c];
       }
-      const float w = expf(-0.60653066f * sigm(a.w0[c] + s_lora[0][lane]));
-      const float av = sigm(a.a0[c] + s_lora[1][lane]);
-      float kk = k * a.k_k[c];
+      if (a.layer > 0) vf = a.v_first[(int64_t)row * a.ldv + c];
+    }
+    auto act = [&](int d, float x) {
+      if (d < a.Dw) return tanhf(x);
+      if (d >= a.Dw + a.Da + a.Dv) return sigm(x);
+      return x;
+    };
+    if (tid < Dtot) s_hid[tid] = act(tid, hx0);
+    if (tid + 256 < Dtot) s_hid[tid + 256] = act(tid + 256, hx1);
+    __syncthreads();
+    // ---- LoRA up for this head's channels from the prefetched rows
+    {
+      const int hoffs[4] = {0, a.Dw, a.Dw + a.Da, a.Dw + a.Da + a.Dv};
+      float accm[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        float acc = 0.f;
+        const bf16_t* wr = s_lw + cc * LDW + hoffs[m] + pq * Dq[m];
+        const float* hh = s_hid + hoffs[m] + pq * Dq[m];
+        for (int d = 0; d < Dq[m]; d += 4) {
+          const uint2 q = *(const uint2*)(wr + d);
+          acc += bf16_to_f32((uint16_t)(q.x & 0xFFFF)) * hh[d + 0];
+          acc += bf16_to_f32((uint16_t)(q.x >> 16)) * hh[d + 1];
+          acc += bf16_to_f32((uint16_t)(q.y & 0xFFFF)) * hh[d + 2];
+          acc += bf16_to_f32((uint16_t)(q.y >> 16)) * hh[d + 3];
+        }
+        acc += __shfl_xor(acc, 1);
+        acc += __shfl_xor(acc, 2);
+        accm[m] = acc;
+      }
+      if (pq == 0) {
+#pragma unroll
+        for (int m = 0; m < 4; ++m) s_lora[m][cc] = accm[m];
+      }
+    }
+    __syncthreads();
+    if (wave == 0) {
+      const float w = expf(-0.60653066f * sigm(w0 + s_lora[0][lane]));
+      const float av = sigm(a0 + s_lora[1][lane]);
+      float kk = k * kkc;
       const float nrm = sqrtf(wave_sum(kk * kk));
       kk = kk / fmaxf(nrm, 1e-12f);
-      k = k * (1.0f + (av - 1.0f) * a.k_a[c]);
-      float* vf = a.v_first + (int64_t)row * a.ldv + c;
+      k = k * (1.0f + (av - 1.0f) * kac);
       if (a.layer == 0) {
-        *vf = v;
+        a.v_first[(int64_t)row * a.ldv + c] = v;
       } else {
-        const float gate = sigm(a.v0[c] + s_lora[2][lane]);
-        v = v + (*vf - v) * gate;
+        const float gate = sigm(v0 + s_lora[2][lane]);
+        v = v + (vf - v) * gate;
       }
       s_r[lane] = r; s_k[lane] = k; s_v[lane] = v; s_w[lane] = w;
       s_kk[lane] = kk; s_b[lane] = kk * av; s_g[lane] = s_lora[3][lane];
     }
     __syncthreads();
-    // state update: S[i][j] = S[i][j]*w_j - sa_i*b_j + v_i*k_j ; y_i = sum_j S[i][j] r_j
+    // ---- state update: S[i][j] = S[i][j]*w_j - sa_i*b_j + v_i*k_j ; y_i = sum_j S[i][j] r_j
     float sa = 0.f;
 #pragma unroll
     for (int q = 0; q < 16; ++q) sa += S[q] * s_kk[jq + q];
@@ -364,17 +501,16 @@ __global__ __launch_bounds__(256) void k_wkv(WkvArgs a) {
     if ((tid & 3) == 0) s_y[i] = y;
     __syncthreads();
     if (wave == 0) {
-      const int c = h * N + lane;
       const float yv = s_y[lane];
       const float mean = wave_sum(yv) * (1.0f / N);
       const float dv = yv - mean;
       const float var = wave_sum(dv * dv) * (1.0f / N);
       const float rstd = 1.0f / sqrtf(var + 64e-5f);
-      const float bonus = wave_sum(s_r[lane] * s_k[lane] * a.r_k[c]);
-      const float gn = dv * rstd * a.lnx_w[c] + a.lnx_b[c];
+      const float bonus = wave_sum(s_r[lane] * s_k[lane] * rkc);
+      const float gn = dv * rstd * lnw + lnb;
       split_store((gn + bonus * s_v[lane]) * s_g[lane], a.z_hi, a.z_lo, (int64_t)row * a.ldz + c);
     }
-    __syncthreads();
+    if (rr + 1 < n_rows) __syncthreads();
   }
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -391,16 +527,40 @@ void launch_embed(const uint32_t* tokens, const bf16_t* emb, const float* w, con
   hipLaunchKernelGGL(k_embed, dim3(R), dim3(256), 0, st, tokens, emb, w, b, h, C);
 }
 void launch_ln_mix(const LnMixArgs& a, int n_out_rows, hipStream_t st) {
-  hipLaunchKernelGGL(k_ln_mix, dim3(n_out_rows), dim3(256), 0, st, a);
+  LnMixArgs b = a;
+  b.n_rows = n_out_rows;
+  const dim3 grid(n_out_rows);
+  if (a.C <= 1024) hipLaunchKernelGGL(k_ln_mix<1>, grid, dim3(256), 0, st, b);
+  else hipLaunchKernelGGL(k_ln_mix<2>, grid, dim3(256), 0, st, b);
 }
+
+template <int MT, int KSTEPS>
+static void launch_gemm_t(const GemmArgs& a, dim3 grid, hipStream_t st) {
+  const size_t lds = (size_t)MT * 16 * (KSTEPS * 32 + 8) * 2 * 2;
+  if (a.xmode == kXPlanes) hipLaunchKernelGGL((k_gemm<MT, KSTEPS, kXPlanes>), grid, dim3(256), lds, st, a);
+  else hipLaunchKernelGGL((k_gemm<MT, KSTEPS, kXRelu2>), grid, dim3(256), lds, st, a);
+}
+
+int gemm_ksteps(int kslice) { return kslice / 32; }
+
 void launch_gemm(const GemmArgs& a, hipStream_t st) {
-  int tiles = a.seg[a.nseg - 1].tile_start + (a.seg[a.nseg - 1].N + 15) / 16;
-  const int mt = a.M <= 16 ? 1 : (a.M <= 32 ? 2 : 4);
+  const int tiles = a.seg[a.nseg - 1].tile_start + (a.seg[a.nseg - 1].N + 63) / 64;
+  const int mt = a.M <= 16 ? 1 : 2;
   const int mg = (a.M + mt * 16 - 1) / (mt * 16);
   dim3 grid(tiles, a.k_split, mg);
-  if (mt == 1) hipLaunchKernelGGL(k_gemm<1>, grid, dim3(256), 0, st, a);
-  else if (mt == 2) hipLaunchKernelGGL(k_gemm<2>, grid, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL(k_gemm<4>, grid, dim3(256), 0, st, a);
+  const int ks = a.kslice / 32;
+#define GEMM_CASE(KS_)                                          \
+  case KS_:                                                     \
+    if (mt == 1) launch_gemm_t<1, KS_>(a, grid, st);            \
+    else launch_gemm_t<2, KS_>(a, grid, st);                    \
+    break;
+  switch (ks) {
+    GEMM_CASE(4)
+    GEMM_CASE(8)
+    GEMM_CASE(16)
+    default: break;  // rejected at engine init (kslice in {128, 256, 512})
+  }
+#undef GEMM_CASE
 }
 void launch_wkv(const WkvArgs& a, int n_seg, int H, hipStream_t st) {
   hipLaunchKernelGGL(k_wkv, dim3(n_seg, H), dim3(256), 0, st, a);

@@ -44,11 +44,14 @@ struct SampleRowArgs {
   const uint64_t* draws;    // [rows]
   int32_t* out;             // [rows]
   float* dbg;               // optional [rows][2]: softmax sum, r
+  uint64_t* stamps;         // optional [rows][16]: s_memtime at phase boundaries (diagnostics)
 };
 
 struct AdvanceArgs {
-  const float* logits;   // [rows][ld]
+  const float* logits;   // [n_part][rows][ld] split-K partial logits (summed in order)
   int ld;
+  int n_part;
+  int64_t part_stride;
   const int* row_slot;   // step row -> slot (rows of this decode/prefill step with logits)
   SlotCtrl* ctrl;
   int32_t* sem_out;      // [S][2048]

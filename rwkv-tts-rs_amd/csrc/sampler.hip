@@ -58,16 +58,63 @@ __device__ inline float draw_f32(const uint32_t* key, uint64_t index) {
   return (float)(chacha12_word(key, index) >> 8) * (1.0f / 16777216.0f);
 }
 
+// Optional phase stamps (debug builds of a call only: pointer is null in production).
+#define STAMP(k)                                                         \
+  do {                                                                   \
+    if (stamps && threadIdx.x == 0) stamps[k] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+
+__device__ inline float readlane_f(float v, int l) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+__device__ inline int readlane_i(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+
+// wave-uniform sequential f32 sum of p[b..e) (all 64 lanes of the calling wave participate):
+// 64 elements are staged into lanes per round and added in order from registers.
+__device__ inline float add64(float s, float v) {  // s + v[lane 0] + ... + v[lane 63], in order
+#pragma unroll
+  for (int i = 0; i < 64; ++i) s += readlane_f(v, i);
+  return s;
+}
+// Sequential adds of non-negative values: padding lanes hold +0.0, and s + 0 == s exactly.
+__device__ inline float wave_serial_add(float s, const float* p, int b, int e) {
+  const int lane = threadIdx.x & 63;
+  for (int q = b; q < e; q += 64) s = add64(s, (q + lane < e) ? p[q + lane] : 0.0f);
+  return s;
+}
+// In-order prefix sums of one 64-block: lane i receives s + v[0] + ... + v[i] (sequential).
+__device__ inline float prefix64(float s, float v, float* total) {
+  float out = 0.0f;
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int i = 0; i < 64; ++i) {
+    s += readlane_f(v, i);
+    out = lane == i ? s : out;
+  }
+  *total = s;
+  return out;
+}
+
 // Shared-memory layout of one sampling workgroup (256 threads).
 struct SampleSmem {
-  float* p;         // [n]
-  uint64_t* keys;   // [kSampleMaxSorted]
-  int* list;        // [kSampleMaxSorted] positive indices in index order
-  int* hist;        // [256]
-  int* scan;        // [257]
-  float* fred;      // [8]
-  int* ired;        // [8]
+  float* p;           // [n] logits -> e -> probabilities
+  uint64_t* keys;     // [kSampleMaxSorted] sort keys (p bits << 32 | ~index)
+  int* list;          // [kSampleMaxSorted] positive indices in index order
+  int* scan;          // [8] block-scan wave totals
+  double* dscan;      // [8]
+  uint32_t* sub_t;    // [256][2] sub-chunk parity maps of the exact-sum emulation
+  int* sub_ok;        // [256]
+  int* chunk_e;       // [64] predicted binade per chunk
+  uint32_t* chunk_t;  // [64][2]
+  int* chunk_ok;      // [64]
+  float* fred;        // [8]
+  int* ired;          // [16]
 };
+
+__device__ inline int wave_sum_i(int v) {
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
 
 __device__ inline float block_max(float v, float* fred) {
   for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
@@ -77,30 +124,31 @@ __device__ inline float block_max(float v, float* fred) {
   return fmaxf(fmaxf(fred[0], fred[1]), fmaxf(fred[2], fred[3]));
 }
 
-// exclusive scan of one int per thread (256 threads); returns this thread's offset, total in *tot
-__device__ inline int block_excl_scan(int v, int* scan, int* tot) {
-  __syncthreads();
-  scan[threadIdx.x] = v;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int acc = 0;
-    for (int i = 0; i < 256; ++i) {
-      const int c = scan[i];
-      scan[i] = acc;
-      acc += c;
-    }
-    scan[256] = acc;
+// block-wide exclusive scans (256 threads): wave shuffles + 4 wave totals
+template <typename T>
+__device__ inline T block_excl_scan_t(T v, T* scratch, T* tot) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  T x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const T y = __shfl_up(x, o);
+    if (lane >= o) x += y;
   }
   __syncthreads();
-  *tot = scan[256];
-  return scan[threadIdx.x];
+  if (lane == 63) scratch[w] = x;
+  __syncthreads();
+  T base = 0;
+  for (int k = 0; k < w; ++k) base += scratch[k];
+  *tot = (scratch[0] + scratch[1]) + (scratch[2] + scratch[3]);
+  return base + x - v;
 }
+__device__ inline int block_excl_scan(int v, int* scratch, int* tot) { return block_excl_scan_t<int>(v, scratch, tot); }
 
 // compact indices with p > 0 into list (index order); returns count (may exceed capacity:
 // then list is incomplete and callers fall back to a scan of p).
 __device__ int compact_positive(const SampleSmem& sm, int n) {
   const int chunk = (n + 255) / 256;
-  const int b = threadIdx.x * chunk, e = min(n, b + chunk);
+  const int b = min(n, (int)threadIdx.x * chunk), e = min(n, b + chunk);
   int cnt = 0;
   for (int i = b; i < e; ++i) cnt += sm.p[i] > 0.0f;
   int tot;
@@ -114,135 +162,309 @@ __device__ int compact_positive(const SampleSmem& sm, int n) {
   return tot;
 }
 
-// index-order sequential f32 sum of p (only positive entries contribute: +0 adds are exact)
-__device__ float serial_sum_positive(const SampleSmem& sm, int n, int npos) {
+// index-order sequential f32 sum of p by one wave (only positive entries contribute: +0 adds
+// are exact); positive values staged into lanes, added in order from registers.
+__device__ float wave_sum_positive(const SampleSmem& sm, int n, int npos) {
+  const int lane = threadIdx.x & 63;
   float s = 0.0f;
   if (npos <= kSampleMaxSorted) {
-    for (int q = 0; q < npos; ++q) s += sm.p[sm.list[q]];
+    for (int q0 = 0; q0 < npos; q0 += 64) {
+      const float v = (q0 + lane < npos) ? sm.p[sm.list[q0 + lane]] : 0.0f;
+      const int cnt = min(64, npos - q0);
+      for (int i = 0; i < cnt; ++i) s += readlane_f(v, i);
+    }
   } else {
-    for (int i = 0; i < n; ++i) s += sm.p[i];
+    for (int q0 = 0; q0 < n; q0 += 64) {
+      const float v = (q0 + lane < n) ? sm.p[q0 + lane] : 0.0f;
+      const int cnt = min(64, n - q0);
+      for (int i = 0; i < cnt; ++i) s += readlane_f(v, i);
+    }
   }
   return s;
+}
+
+// ---------------------------------------------------------------------------------------
+// Exact parallel emulation of the sequential f32 sum  s = (((0 + e0) + e1) + ...) + e_{n-1}
+// for e_i >= 0 (rwkv_sampler.rs:88, `probs.iter().sum()`).
+// While s stays inside one binade [2^E, 2^(E+1)), s = m * u with u = 2^(E-23) and
+//   RN(s + e) = u * (m + a + c),  a = floor(e/u),  c = 1 if frac(e/u) > 1/2,
+//   c = (m + a) & 1 if frac(e/u) == 1/2 (ties to even), else 0,
+// so a run of additions only depends on the parity of m: it is a map {0,1} -> (increment,
+// parity), and such maps compose. Each of 64 chunks is simulated for the binade predicted from
+// the exact (double) prefix sum at its start; one lane then walks the chunks, applying a
+// chunk's map when the running s really is in the predicted binade and stays in it (m + T <
+// 2^24), and otherwise adding that chunk's elements one by one. The result is bit-identical
+// to the sequential loop by construction.
+// ---------------------------------------------------------------------------------------
+__device__ inline void sum_sim_elem(uint32_t b, int E, uint32_t& T0, uint32_t& T1, int& q0, int& q1, bool& ok) {
+  const uint32_t ef = (b >> 23) & 0xFFu;
+  uint32_t M = b & 0x7FFFFFu;
+  int ex;
+  if (ef == 0) ex = -149;
+  else { M |= 0x800000u; ex = (int)ef - 150; }
+  uint32_t a = 0;
+  int cls = 0;  // 0 below half, 1 tie, 2 above
+  if (M != 0) {
+    const int sh = (E - 23) - ex;
+    if (sh <= 0) {
+      if (sh < -8) { ok = false; return; }
+      a = M << (-sh);
+      if (a >= 0x1000000u) { ok = false; return; }
+    } else if (sh <= 24) {
+      a = M >> sh;
+      const uint32_t r = M & ((1u << sh) - 1u), half = 1u << (sh - 1);
+      cls = r > half ? 2 : (r == half ? 1 : 0);
+    }
+  }
+  const uint32_t c0 = (cls == 2 || (cls == 1 && ((q0 + a) & 1u))) ? 1u : 0u;
+  const uint32_t c1 = (cls == 2 || (cls == 1 && ((q1 + a) & 1u))) ? 1u : 0u;
+  T0 += a + c0;
+  T1 += a + c1;
+  q0 = (int)((q0 + a + c0) & 1u);
+  q1 = (int)((q1 + a + c1) & 1u);
+  if (T0 >= 0x1000000u || T1 >= 0x1000000u) ok = false;
+}
+
+__device__ float exact_seq_sum(const SampleSmem& sm, int n, uint64_t* stamps = nullptr) {
+  const int tid = threadIdx.x;
+  const int CH = (n + 63) / 64, SUB = (CH + 3) / 4;
+  const int chunk = tid >> 2, sub = tid & 3;
+  const int cb = min(n, chunk * CH), ce = min(n, cb + CH);
+  const int sb = min(ce, cb + sub * SUB), se = min(ce, sb + SUB);
+  double ds = 0.0;
+  for (int i = sb; i < se; ++i) ds += (double)sm.p[i];
+  double dtot;
+  const double pre = block_excl_scan_t<double>(ds, sm.dscan, &dtot);
+  STAMP(10);
+  const double pchunk = __shfl(pre, (tid & 63) & ~3);  // prefix at the chunk start
+  const float pf = (float)pchunk;
+  const uint32_t pb = __builtin_bit_cast(uint32_t, pf);
+  const int E = (int)((pb >> 23) & 0xFFu) - 127;
+  bool ok = pf >= 0x1p-100f && pf < 0x1p+100f;
+  uint32_t T0 = 0, T1 = 0;
+  int q0 = 0, q1 = 1;
+  for (int i = sb; i < se && ok; ++i) sum_sim_elem(__builtin_bit_cast(uint32_t, sm.p[i]), E, T0, T1, q0, q1, ok);
+  sm.sub_t[2 * tid] = T0;
+  sm.sub_t[2 * tid + 1] = T1;
+  sm.sub_ok[tid] = ok;
+  if (sub == 0) sm.chunk_e[chunk] = E;
+  __syncthreads();
+  STAMP(11);
+  if (tid < 64) {  // compose the 4 sub-chunk maps of chunk `tid`
+    bool cok = true;
+    for (int s = 0; s < 4; ++s) cok &= sm.sub_ok[4 * tid + s] != 0;
+    for (int pin = 0; pin < 2; ++pin) {
+      int par = pin;
+      uint32_t T = 0;
+      for (int s = 0; s < 4; ++s) {
+        const uint32_t t = sm.sub_t[2 * (4 * tid + s) + par];
+        T += t;
+        par = (int)((par + t) & 1u);
+      }
+      if (T >= 0x1000000u) cok = false;
+      sm.chunk_t[2 * tid + pin] = T;
+    }
+    sm.chunk_ok[tid] = cok;
+  }
+  __syncthreads();
+  STAMP(12);
+  int nfast = 0;
+  if (tid < 64) {  // wave 0 walks the chunks; chunk c's map lives in lane c
+    const int okv = sm.chunk_ok[tid], ev = sm.chunk_e[tid];
+    const int t0v = (int)sm.chunk_t[2 * tid], t1v = (int)sm.chunk_t[2 * tid + 1];
+    float s = 0.0f;
+    const int nch = (n + CH - 1) / CH;
+    for (int c = 0; c < nch; ++c) {
+      const int b0 = c * CH, e0 = min(n, b0 + CH);
+      const uint32_t sb2 = __builtin_bit_cast(uint32_t, s);
+      const int ef = (int)((sb2 >> 23) & 0xFFu);
+      if (readlane_i(okv, c) && ef != 0 && ef - 127 == readlane_i(ev, c)) {
+        const uint32_t m = (sb2 & 0x7FFFFFu) | 0x800000u;
+        const uint32_t T = (uint32_t)((m & 1u) ? readlane_i(t1v, c) : readlane_i(t0v, c));
+        const uint32_t m2 = m + T;
+        if (m2 < 0x1000000u) {
+          s = __builtin_bit_cast(float, (sb2 & 0xFF800000u) | (m2 & 0x7FFFFFu));
+          ++nfast;
+          continue;
+        }
+      }
+      s = wave_serial_add(s, sm.p, b0, e0);  // binade crossing: add this chunk one by one
+    }
+    if (tid == 0) {
+      sm.fred[4] = s;
+      if (stamps) stamps[14] = nfast;
+    }
+  }
+  __syncthreads();
+  STAMP(13);
+  return sm.fred[4];
+}
+
+// bitonic sort (descending) of M (power of two) keys in LDS by the whole workgroup
+__device__ void bitonic_desc(uint64_t* keys, int M) {
+  for (int k = 2; k <= M; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int q = threadIdx.x; q < M; q += 256) {
+        const int ixj = q ^ j;
+        if (ixj > q) {
+          const uint64_t A = keys[q], B = keys[ixj];
+          const bool desc = (q & k) == 0;
+          if (desc ? (A < B) : (A > B)) { keys[q] = B; keys[ixj] = A; }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+__device__ inline uint64_t pkey(float p, int i) {
+  return ((uint64_t)__builtin_bit_cast(uint32_t, p) << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)i);
 }
 
 // The sampler. p holds the (masked) logits on entry. Returns the index in every thread.
 // status: 0 ok, RWKVTTS_EUNSUPPORTED for the documented limitation.
 __device__ int sample_block(const SampleSmem& sm, int n, float temperature, float top_p,
                             int top_k, const uint32_t* key, uint64_t draw, bool fixed42,
-                            float* dbg, int* status) {
+                            float* dbg, int* status, uint64_t* stamps = nullptr) {
   const int tid = threadIdx.x;
   *status = 0;
   if (n == 0) return 0;
-  // (2) softmax: max, exp, sequential sum, divide
+  STAMP(1);
+  // (2) softmax: max, exp, sequential sum (exact emulation), divide
   float mx = -__builtin_inff();
   for (int i = tid; i < n; i += 256) mx = fmaxf(mx, sm.p[i]);
   mx = block_max(mx, sm.fred);
   for (int i = tid; i < n; i += 256) sm.p[i] = glibc_expf(sm.p[i] - mx);
   __syncthreads();
-  if (tid == 0) {
-    float s = 0.0f;
-    int i = 0;
-    for (; i + 4 <= n; i += 4) {
-      const float4_ q = *(const float4_*)(sm.p + i);
-      s += q[0];
-      s += q[1];
-      s += q[2];
-      s += q[3];
-    }
-    for (; i < n; ++i) s += sm.p[i];
-    sm.fred[4] = s;
-  }
-  __syncthreads();
-  const float sum = sm.fred[4];
+  STAMP(2);
+  const float sum = exact_seq_sum(sm, n, stamps);
+  STAMP(3);
   if (sum > 0.0f)
     for (int i = tid; i < n; i += 256) sm.p[i] = sm.p[i] / sum;
   __syncthreads();
-  // (3) top-k: radix-select the k-th largest (p desc, index asc)
+  STAMP(4);
+  // sorted (p desc, index asc) candidate keys; valid for the first n_sorted entries
+  int n_sorted = -1;
+  // (3) top-k (:95-105): candidates above a lower bound of the k-th largest, sorted
   if (top_k > 0 && top_k < n) {
-    uint32_t prefix = 0, mask = 0;
-    int remaining = top_k;
-    for (int pass = 0; pass < 4; ++pass) {
-      const int shift = 24 - 8 * pass;
-      sm.hist[tid] = 0;
-      __syncthreads();
-      for (int i = tid; i < n; i += 256) {
-        const uint32_t u = __builtin_bit_cast(uint32_t, sm.p[i]);
-        if ((u & mask) == prefix) atomicAdd(&sm.hist[(u >> shift) & 255], 1);
-      }
-      __syncthreads();
-      if (tid == 0) {
-        int acc = 0, D = 0;
-        for (int d = 255; d >= 0; --d) {
-          if (acc + sm.hist[d] >= remaining) { D = d; break; }
-          acc += sm.hist[d];
+    bool done = false;
+    if (top_k <= 256) {
+      // lower bound L: min over waves of the ceil(k/4)-th largest thread-local maximum
+      const int chunk = (n + 255) / 256;
+      const int b = min(n, tid * chunk), e = min(n, b + chunk);
+      float lm = -1.0f;  // every p >= 0
+      for (int i = b; i < e; ++i) lm = fmaxf(lm, sm.p[i]);
+      // wave bitonic sort (descending) of the 64 local maxima
+      const int lane = tid & 63;
+      float v = lm;
+      for (int k = 2; k <= 64; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+          const float o = __shfl_xor(v, j);
+          const bool up = ((lane & k) == 0) == ((lane & j) == 0);
+          v = up ? fmaxf(v, o) : fminf(v, o);
         }
-        sm.ired[0] = D;
-        sm.ired[1] = remaining - acc;
-      }
+      const int kw = (top_k + 3) / 4;
+      const float vw = __shfl(v, kw - 1);
+      if (lane == 0) sm.fred[tid >> 6] = vw;
       __syncthreads();
-      prefix |= (uint32_t)sm.ired[0] << shift;
-      mask |= 0xFFu << shift;
-      remaining = sm.ired[1];
-      __syncthreads();
-    }
-    const float t = __builtin_bit_cast(float, prefix);
-    const int need_eq = remaining;
-    const int chunk = (n + 255) / 256;
-    const int b = tid * chunk, e = min(n, b + chunk);
-    int cnt = 0;
-    for (int i = b; i < e; ++i) cnt += (sm.p[i] == t);
-    int tot;
-    int rank = block_excl_scan(cnt, sm.scan, &tot);
-    for (int i = b; i < e; ++i) {
-      const float v = sm.p[i];
-      if (v < t) {
-        sm.p[i] = 0.0f;
-      } else if (v == t) {
-        if (rank >= need_eq) sm.p[i] = 0.0f;
-        ++rank;
-      }
-    }
-    __syncthreads();
-  }
-  int npos = compact_positive(sm, n);
-  // (4) top-p
-  if (top_p < 1.0f) {
-    if (npos > kSampleMaxSorted) {
-      *status = RWKVTTS_EUNSUPPORTED;
-      return 0;
-    }
-    int M = 1;
-    while (M < npos) M <<= 1;
-    for (int q = tid; q < M; q += 256)
-      sm.keys[q] = q < npos ? (((uint64_t)__builtin_bit_cast(uint32_t, sm.p[sm.list[q]]) << 32) |
-                               (uint64_t)(0xFFFFFFFFu - (uint32_t)sm.list[q]))
-                            : 0ull;
-    __syncthreads();
-    for (int k = 2; k <= M; k <<= 1) {  // bitonic sort, descending
-      for (int j = k >> 1; j > 0; j >>= 1) {
-        for (int q = tid; q < M; q += 256) {
-          const int ixj = q ^ j;
-          if (ixj > q) {
-            const uint64_t A = sm.keys[q], B = sm.keys[ixj];
-            const bool desc = (q & k) == 0;
-            if (desc ? (A < B) : (A > B)) { sm.keys[q] = B; sm.keys[ixj] = A; }
-          }
+      const float L = fmaxf(fminf(fminf(sm.fred[0], sm.fred[1]), fminf(sm.fred[2], sm.fred[3])), 0.0f);
+      int cnt = 0;
+      for (int i = b; i < e; ++i) cnt += sm.p[i] >= L;
+      int tot;
+      int off = block_excl_scan(cnt, sm.scan, &tot);
+      if (tot <= kSampleMaxSorted) {
+        for (int i = b; i < e; ++i)
+          if (sm.p[i] >= L) sm.keys[off++] = pkey(sm.p[i], i);
+        int M = 1;
+        while (M < tot) M <<= 1;
+        for (int q = tot + tid; q < M; q += 256) sm.keys[q] = 0ull;
+        __syncthreads();
+        bitonic_desc(sm.keys, M);
+        // zero everything, then restore the k survivors
+        for (int i = tid; i < n; i += 256) sm.p[i] = 0.0f;
+        __syncthreads();
+        for (int q = tid; q < top_k; q += 256) {
+          const uint64_t kk = sm.keys[q];
+          sm.p[0xFFFFFFFFu - (uint32_t)kk] = __builtin_bit_cast(float, (uint32_t)(kk >> 32));
         }
         __syncthreads();
+        n_sorted = top_k;
+        done = true;
       }
     }
-    if (tid == 0) {
+    if (!done) {  // general path: bisection on the bits of the k-th largest probability
+      uint32_t lo = 0, hi = 0x7F800000u;
+      int cnt_hi = 0, it = 0;
+      while (hi - lo > 1) {
+        const uint32_t mid = lo + ((hi - lo) >> 1);
+        int c = 0;
+        for (int i = tid; i < n; i += 256) c += __builtin_bit_cast(uint32_t, sm.p[i]) >= mid;
+        c = wave_sum_i(c);
+        if ((tid & 63) == 0) sm.ired[8 + (it & 1) * 4 + (tid >> 6)] = c;
+        __syncthreads();
+        const int* r4 = sm.ired + 8 + (it & 1) * 4;
+        const int t4 = (r4[0] + r4[1]) + (r4[2] + r4[3]);
+        if (t4 >= top_k) lo = mid;
+        else { hi = mid; cnt_hi = t4; }
+        ++it;
+      }
+      const float t = __builtin_bit_cast(float, lo);
+      const int need_eq = top_k - cnt_hi;
+      const int chunk = (n + 255) / 256;
+      const int b = min(n, tid * chunk), e = min(n, b + chunk);
+      int cnt = 0;
+      for (int i = b; i < e; ++i) cnt += (sm.p[i] == t);
+      int tot;
+      int rank = block_excl_scan(cnt, sm.scan, &tot);
+      for (int i = b; i < e; ++i) {
+        const float v = sm.p[i];
+        if (v < t) sm.p[i] = 0.0f;
+        else if (v == t) {
+          if (rank >= need_eq) sm.p[i] = 0.0f;
+          ++rank;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  STAMP(5);
+  int npos = compact_positive(sm, n);
+  STAMP(6);
+  // (4) top-p (:108-153)
+  if (top_p < 1.0f) {
+    if (n_sorted < 0 || n_sorted > npos) {
+      // survivors not yet sorted (or fewer positives than k): sort the positive ones
+      if (npos > kSampleMaxSorted) {
+        *status = RWKVTTS_EUNSUPPORTED;
+        return 0;
+      }
+      int M = 1;
+      while (M < npos) M <<= 1;
+      for (int q = tid; q < M; q += 256) sm.keys[q] = q < npos ? pkey(sm.p[sm.list[q]], sm.list[q]) : 0ull;
+      __syncthreads();
+      bitonic_desc(sm.keys, M);
+    }
+    if (tid < 64) {  // sequential cumulative in sorted order (wave-uniform, keys staged in lanes)
       float cum = 0.0f, cutoff = 0.0f;
       int found = 0;
-      for (int q = 0; q < npos; ++q) {
-        const float pv = __builtin_bit_cast(float, (uint32_t)(sm.keys[q] >> 32));
-        cum += pv;
-        if (cum >= top_p) { found = 1; cutoff = pv; break; }
+      for (int q0 = 0; q0 < npos && !found; q0 += 64) {
+        const bool in = q0 + tid < npos;
+        const float pv_l = in ? __builtin_bit_cast(float, (uint32_t)(sm.keys[q0 + tid] >> 32)) : 0.0f;
+        float tot;
+        const float pre = prefix64(cum, pv_l, &tot);
+        const uint64_t hit = __ballot(in && pre >= top_p);
+        if (hit) {
+          const int i = __builtin_ctzll(hit);
+          found = 1;
+          cutoff = readlane_f(pv_l, i);
+        }
+        cum = tot;
       }
-      if (!found && npos < n && cum >= top_p) { found = 1; cutoff = 0.0f; }  // (unreachable for top_p > 0)
-      if (!found && npos == 0 && 0.0f >= top_p) { found = 1; cutoff = 0.0f; }
-      sm.fred[5] = cutoff;
-      sm.ired[2] = found;
+      if (!found && 0.0f >= top_p && npos < n) { found = 1; cutoff = 0.0f; }  // top_p <= 0 with zeros
+      if (tid == 0) {
+        sm.fred[5] = cutoff;
+        sm.ired[2] = found;
+      }
     }
     __syncthreads();
     if (sm.ired[2]) {
@@ -252,18 +474,21 @@ __device__ int sample_block(const SampleSmem& sm, int n, float temperature, floa
       __syncthreads();
       if (top_p > 0.0f) {
         npos = compact_positive(sm, n);
-        sm.ired[3] = 0;
+        if (tid == 0) sm.ired[3] = 0;
         __syncthreads();
         int c = 0;
         for (int i = tid; i < n; i += 256) c += (sm.p[i] == cutoff);
-        if (c) atomicAdd(&sm.ired[3], c);
+        c = wave_sum_i(c);
+        if ((tid & 63) == 0) atomicAdd(&sm.ired[3], c);
         __syncthreads();
-        if (tid == 0) {
-          const float cur = serial_sum_positive(sm, n, npos);
-          sm.ired[4] = 0;
-          if (cur < top_p && sm.ired[3] > 0) {
-            sm.fred[6] = (top_p - cur) / (float)sm.ired[3];
-            sm.ired[4] = 1;
+        if (tid < 64) {
+          const float cur = wave_sum_positive(sm, n, npos);
+          if (tid == 0) {
+            sm.ired[4] = 0;
+            if (cur < top_p && sm.ired[3] > 0) {
+              sm.fred[6] = (top_p - cur) / (float)sm.ired[3];
+              sm.ired[4] = 1;
+            }
           }
         }
         __syncthreads();
@@ -275,9 +500,10 @@ __device__ int sample_block(const SampleSmem& sm, int n, float temperature, floa
         }
       }
     }
+    npos = compact_positive(sm, n);
   }
-  npos = compact_positive(sm, n);
-  // (5) temperature
+  STAMP(7);
+  // (5) temperature (:156-171)
   if (temperature != 1.0f && temperature > 0.0f) {
     const float tinv = 1.0f / temperature;
     for (int i = tid; i < n; i += 256) {
@@ -286,15 +512,19 @@ __device__ int sample_block(const SampleSmem& sm, int n, float temperature, floa
     }
     __syncthreads();
     npos = compact_positive(sm, n);
-    if (tid == 0) sm.fred[7] = serial_sum_positive(sm, n, npos);
+    if (tid < 64) {
+      const float s2 = wave_sum_positive(sm, n, npos);
+      if (tid == 0) sm.fred[7] = s2;
+    }
     __syncthreads();
     const float s2 = sm.fred[7];
     if (s2 > 0.0f)
       for (int i = tid; i < n; i += 256) sm.p[i] = sm.p[i] / s2;
     __syncthreads();
   }
-  // (6) multinomial
-  if (tid == 0) {
+  STAMP(8);
+  // (6) multinomial (:174-207): wave 0, cumulative in index order from lanes
+  if (tid < 64) {
     uint32_t k42[8];
     if (fixed42) {
       uint64_t st = 42;
@@ -310,52 +540,66 @@ __device__ int sample_block(const SampleSmem& sm, int n, float temperature, floa
     int ret = -1;
     if (r <= sm.p[0]) {
       ret = 0;
-    } else if (npos <= kSampleMaxSorted) {
-      float cum = 0.0f;
-      for (int q = 0; q < npos; ++q) {
-        cum += sm.p[sm.list[q]];
-        if (r <= cum) { ret = sm.list[q]; break; }
-      }
-      if (ret < 0 && npos > 0) ret = sm.list[npos - 1];
     } else {
+      const bool listed = npos <= kSampleMaxSorted;
+      const int cnt_all = listed ? npos : n;
       float cum = 0.0f;
-      for (int i = 0; i < n; ++i) {
-        cum += sm.p[i];
-        if (r <= cum) { ret = i; break; }
+      int last_pos = -1;
+      for (int q0 = 0; q0 < cnt_all && ret < 0; q0 += 64) {
+        const bool in = q0 + tid < cnt_all;
+        const int idx_l = in ? (listed ? sm.list[q0 + tid] : q0 + tid) : 0;
+        const float v = in ? sm.p[idx_l] : 0.0f;
+        float tot;
+        const float pre = prefix64(cum, v, &tot);
+        const uint64_t hit = __ballot(in && r <= pre);
+        const uint64_t posm = __ballot(in && v > 0.0f);
+        if (posm) last_pos = readlane_i(idx_l, 63 - __builtin_clzll(posm));
+        if (hit) ret = readlane_i(idx_l, __builtin_ctzll(hit));
+        cum = tot;
       }
-      if (ret < 0)
-        for (int i = n - 1; i >= 0; --i)
-          if (sm.p[i] > 0.0f) { ret = i; break; }
+      if (ret < 0) ret = last_pos;  // highest index with p > 0 (:183-189)
     }
     if (ret < 0) ret = 0;
-    sm.ired[5] = ret;
-    if (dbg) { dbg[0] = sum; dbg[1] = r; }
+    if (tid == 0) {
+      sm.ired[5] = ret;
+      if (dbg) { dbg[0] = sum; dbg[1] = r; }
+    }
   }
   __syncthreads();
+  STAMP(9);
   return sm.ired[5];
 }
 
 __device__ SampleSmem carve(char* base, int n) {
   SampleSmem sm;
   const int npad = (n + 3) & ~3;
-  sm.p = (float*)base;
-  sm.keys = (uint64_t*)(base + (int64_t)npad * 4);
-  sm.list = (int*)(sm.keys + kSampleMaxSorted);
-  sm.hist = sm.list + kSampleMaxSorted;
-  sm.scan = sm.hist + 256;
-  sm.fred = (float*)(sm.scan + 260);
-  sm.ired = (int*)(sm.fred + 8);
+  char* q = base;
+  sm.p = (float*)q; q += (size_t)npad * 4;
+  sm.keys = (uint64_t*)q; q += kSampleMaxSorted * 8;
+  sm.dscan = (double*)q; q += 8 * 8;
+  sm.list = (int*)q; q += kSampleMaxSorted * 4;
+  sm.scan = (int*)q; q += 8 * 4;
+  sm.sub_t = (uint32_t*)q; q += 512 * 4;
+  sm.sub_ok = (int*)q; q += 256 * 4;
+  sm.chunk_e = (int*)q; q += 64 * 4;
+  sm.chunk_t = (uint32_t*)q; q += 128 * 4;
+  sm.chunk_ok = (int*)q; q += 64 * 4;
+  sm.fred = (float*)q; q += 8 * 4;
+  sm.ired = (int*)q;
   return sm;
 }
 inline size_t smem_bytes(int n) {
   const int npad = (n + 3) & ~3;
-  return (size_t)npad * 4 + kSampleMaxSorted * 8 + kSampleMaxSorted * 4 + 256 * 4 + 260 * 4 + 8 * 4 + 8 * 4;
+  return (size_t)npad * 4 + kSampleMaxSorted * 8 + 64 + kSampleMaxSorted * 4 + 32 + 2048 + 1024 + 256 +
+         512 + 256 + 32 + 64;
 }
 
 __global__ __launch_bounds__(256) void k_sample_rows(SampleRowArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const SampleSmem sm = carve(smem, a.n);
   const int row = blockIdx.x;
+  uint64_t* stamps = a.stamps ? a.stamps + row * 16 : nullptr;
+  STAMP(0);
   const float* lg = a.logits + (int64_t)row * a.ld;
   for (int i = threadIdx.x; i < a.n; i += 256) sm.p[i] = lg[i];
   __syncthreads();
@@ -364,7 +608,7 @@ __global__ __launch_bounds__(256) void k_sample_rows(SampleRowArgs a) {
   int status;
   const int id = sample_block(sm, a.n, a.temperature, a.top_p, a.top_k,
                               a.keys ? a.keys + row * 8 : nullptr, a.draws ? a.draws[row] : 0,
-                              a.keys == nullptr, a.dbg ? a.dbg + row * 2 : nullptr, &status);
+                              a.keys == nullptr, a.dbg ? a.dbg + row * 2 : nullptr, &status, stamps);
   if (threadIdx.x == 0) a.out[row] = status ? status : id;
 }
 
@@ -375,6 +619,12 @@ void launch_sample_rows(const SampleRowArgs& a, int rows, hipStream_t st) {
 // ---------------------------------------------------------------------------------------
 // Phase controller: one workgroup per step row that carries logits.
 // ---------------------------------------------------------------------------------------
+__device__ inline float load_logit(const AdvanceArgs& a, const float* lg, int i) {
+  float v = lg[i];
+  for (int p = 1; p < a.n_part; ++p) v += lg[p * a.part_stride + i];
+  return v;
+}
+
 __global__ __launch_bounds__(256) void k_advance(AdvanceArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int row = blockIdx.x;
@@ -393,7 +643,7 @@ __global__ __launch_bounds__(256) void k_advance(AdvanceArgs a) {
   const float* lg = a.logits + (int64_t)row * a.ld;
   if (phase == kPhGlobal) {
     const SampleSmem sm = carve(smem, 4096);
-    for (int i = threadIdx.x; i < 4096; i += 256) sm.p[i] = lg[i];
+    for (int i = threadIdx.x; i < 4096; i += 256) sm.p[i] = load_logit(a, lg, i);
     __syncthreads();
     int status;
     const int id = sample_block(sm, 4096, 1.0f, 0.95f, c->top_k_g, c->gkey, c->gdraw, false,
@@ -410,7 +660,7 @@ __global__ __launch_bounds__(256) void k_advance(AdvanceArgs a) {
   constexpr int NS = RWKVTTS_EOS_TOKEN + 1;
   const SampleSmem sm = carve(smem, NS);
   const bool eos_masked = c->fixed || (c->mode == 1 && c->n_sem < c->hard_min);
-  for (int i = threadIdx.x; i < NS; i += 256) sm.p[i] = lg[i];
+  for (int i = threadIdx.x; i < NS; i += 256) sm.p[i] = load_logit(a, lg, i);
   __syncthreads();
   if (threadIdx.x == 0 && eos_masked) sm.p[RWKVTTS_EOS_TOKEN] = -__builtin_inff();
   __syncthreads();
@@ -428,7 +678,7 @@ __global__ __launch_bounds__(256) void k_advance(AdvanceArgs a) {
       if (wl >= 12 && ratio >= 0.7f) {
         stop = true;
       } else {  // re-draw with EOS masked from the same logits (zero_shot_inference.rs:287-297)
-        for (int i = threadIdx.x; i < NS; i += 256) sm.p[i] = lg[i];
+        for (int i = threadIdx.x; i < NS; i += 256) sm.p[i] = load_logit(a, lg, i);
         __syncthreads();
         if (threadIdx.x == 0) sm.p[RWKVTTS_EOS_TOKEN] = -__builtin_inff();
         __syncthreads();

@@ -96,3 +96,42 @@ def test_sampler_temperature(rt, oracle_mod):
     dev = rt.sample(rows, 0.7, 0.95, 50, None, [rwkvtts.StdRng.seed_from_u64(s) for s in seeds])
     ref = [oracle_mod.sample(rows[i], 0.7, 0.95, 50, None, oracle_mod.Rng(seeds[i])) for i in range(32)]
     assert sum(int(a != b) for a, b in zip(dev.tolist(), ref)) <= 1
+
+
+def _debug_sums(rt, rows, T=1.0, p=0.95, k=80):
+    import ctypes
+    from rwkvtts import _ffi
+    L = _ffi.lib()
+    f = L.rwkvtts_debug_sample
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_ffi.SampleArgs),
+                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    rows = np.ascontiguousarray(rows, dtype=np.float32)
+    out = np.zeros(len(rows), np.int32)
+    dbg = np.zeros(len(rows) * 34, np.float32)  # (sum, r) per row + 16 uint64 stamps per row
+    args = _ffi.SampleArgs(T, p, k, -1)
+    rc = f(rt.handle, rows.ctypes.data_as(ctypes.c_void_p), len(rows), rows.shape[1], ctypes.byref(args), None,
+           out.ctypes.data_as(ctypes.c_void_p), dbg.ctypes.data_as(ctypes.c_void_p))
+    assert rc == 0
+    return out, dbg[:2 * len(rows)].reshape(len(rows), 2)
+
+
+@pytest.mark.parametrize("n", [17, 64, 1000, 4096, 8193, 16384])
+def test_softmax_sum_bit_exact(rt, oracle_mod, n):
+    """The parallel emulation of the sequential f32 softmax denominator (sampler.hip
+    exact_seq_sum) equals the oracle's left-to-right sum bit for bit, including rows built to
+    stress ties at half-ulp, binade crossings, subnormal terms and wide dynamic range."""
+    rs = np.random.RandomState(n)
+    rows = [rs.randn(n) * s for s in (0.05, 0.6, 1.6, 4.0, 12.0, 40.0)]
+    rows.append(np.round(rs.randn(n) * 8) / 8)              # exact binary fractions -> many ties
+    rows.append(np.where(rs.rand(n) < 0.5, 0.0, -np.log(2.0) * rs.randint(1, 30, n)))  # powers of two
+    x = rs.randn(n) * 2
+    x[rs.rand(n) < 0.3] = -np.inf
+    rows.append(x)
+    rows.append(np.linspace(0, -110, n))                     # down to subnormal/zero exp
+    rows.append(np.zeros(n))                                 # all equal: sum == n exactly
+    rows = np.stack(rows).astype(np.float32)
+    tok, dbg = _debug_sums(rt, rows)
+    for i, row in enumerate(rows):
+        o_idx, o_sum, _ = oracle_mod.sample(row, 1.0, 0.95, 80, None, None, debug=True)
+        assert np.float32(dbg[i, 0]).view(np.uint32) == np.float32(o_sum).view(np.uint32), (i, dbg[i, 0], o_sum)
+        assert tok[i] == o_idx, i
