@@ -6,7 +6,9 @@ One "step" = one full batch of B=32 synthetic requests through the hot path on e
 TAG_1 -> 512 semantic tokens (fixed-length benchmark mode, EOS masked) with the exact
 device sampler, continuous batching in 32 GPU slots. Weights are random-init bf16 of the assumed
 0.4B architecture (no checkpoints offline), broadcast from rank 0 over RCCL. value = all ranks'
-audio samples (320 per semantic token @16 kHz) / max-over-ranks wall time.
+audio samples (320 per semantic token @16 kHz) / max-over-ranks wall time. Each step ends with the
+BiCodec decoder (HIP MFMA conv stack, assumed SparkTTS dims, random-init weights) turning every
+request's 32 global + 512 semantic tokens into PCM, so the timed region is tokens -> waveform.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]; N>1 under torch.distributed.run.
 """
@@ -25,6 +27,25 @@ B_PER_GPU = 32
 PROMPT_TEXT = 24
 SEMANTIC = 512
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA
+
+
+def codec_flops(cd, T):
+    """Algorithmic FLOPs (2 per multiply-add, f32-equivalent) of the BiCodec decoder for T
+    frames, by profiling class: the bf16 hi+lo split doubles MFMA work but not
+    this count."""
+    L, P, I, C = cd["latent_dim"], cd["prenet_dim"], cd["prenet_inter"], cd["dec_channels"]
+    f = {"codec_prenet_gemm": 2 * T * (L * P + 7 * P * P + cd["prenet_layers"] * 2 * P * I + P * L),
+         "codec_conv_in": 2 * T * 7 * L * C}
+    m = 1
+    for i in range(cd["n_up"]):
+        s, K, Co = cd["up_rates"][i], cd["up_kernels"][i], C // 2
+        f[f"codec_convT@{Co}"] = 2 * T * m * C * Co * K
+        m *= s
+        f[f"codec_res_conv7@{Co}"] = 3 * 2 * T * m * 7 * Co * Co
+        f[f"codec_res_conv1@{Co}"] = 3 * 2 * T * m * Co * Co
+        C = Co
+    return f
 
 
 def algorithmic_bytes(d, R, head_rows):
@@ -85,6 +106,16 @@ def main():
     rt = rwkvtts.SharedRwkvRuntime(nbytes, device=local, max_slots=B_PER_GPU, token_chunk_size=512,
                                    use_graphs=True, device_ptr=wdev.data_ptr())
     del wdev
+    # ---- vocoder weights: same scheme (rank 0 synthesises, RCCL broadcast)
+    from rwkvtts import codec as CC
+    cdims = CC.CODEC_DIMS_FULL
+    cw = torch.empty(CC.codec_blob_floats(cdims), dtype=torch.float32, device="cuda")
+    if rank == 0:
+        cw.copy_(torch.from_numpy(CC.synth_codec_blob(cdims)))
+    if world > 1:
+        dist.broadcast(cw, src=0)
+    voc = CC.BiCodecDetokenizer(cw.cpu().numpy(), cdims, device=local)
+    del cw
     torch.cuda.empty_cache()
 
     def requests(step):
@@ -101,7 +132,10 @@ def main():
 
     def run(step):
         out = rt.generate_batch(requests(step))
-        return sum(len(s) for _, s in out)
+        pcm = voc.decode_audio_batch([(g, s) for g, s in out])
+        n = sum(len(s) for _, s in out)
+        assert sum(p.size for p in pcm) == 320 * n, "vocoder output length mismatch"
+        return n
 
     for w in range(args.warmup):
         run(-1 - w)
@@ -139,11 +173,15 @@ def main():
     roofline = None
     kernels = {}
     step_roof = None
+    codec_roof = None
     if rank == 0:
         rt.set_profiling(True)
+        voc.set_profiling(True)
         run(10**6)
         prof = rt.profile()
+        vprof = voc.profile()
         rt.set_profiling(False)
+        voc.set_profiling(False)
         st = rt.stats()
         R = B_PER_GPU
         per_launch, per_step = algorithmic_bytes(dims, R, 8193)
@@ -158,6 +196,20 @@ def main():
             roofline = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
                         "bytes_per_launch": per_launch[dom], "avg_us": round(kernels[dom]["avg_us"], 2)}
+        # vocoder: MFMA-bound conv stack, achieved TFLOP/s per class and for the whole decoder
+        cfl = codec_flops(cdims, B_PER_GPU * SEMANTIC)
+        vk = {}
+        for name, (launches, ms) in vprof.items():
+            e = {"launches": launches, "avg_us": round(1000.0 * ms / max(launches, 1), 2), "total_ms": round(ms, 3)}
+            if name in cfl and ms > 0:
+                e["tflops"] = round(cfl[name] / (ms * 1e-3) / 1e12, 1)
+            vk[name] = e
+        vtot = sum(ms for _, ms in vprof.values())
+        codec_roof = {"bound": "mfma", "flops_per_batch": sum(cfl.values()), "ms_per_batch": round(vtot, 3),
+                      "achieved": round(sum(cfl.values()) / (vtot * 1e-3) / 1e12, 1),
+                      "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                      "frac": round(sum(cfl.values()) / (vtot * 1e-3) / 1e12 / MFMA_BF16_PEAK_TFLOPS, 4),
+                      "kernels": vk}
         # whole decode step (graph-replayed timing from the timed region)
         if dec_steps:
             step_ms = decode_ms / dec_steps
@@ -168,7 +220,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(dims, args.cpu_seconds)
+        cpu = cpu_baseline(dims, cdims, args.cpu_seconds)
 
     if rank == 0:
         line = {
@@ -179,24 +231,27 @@ def main():
             "data": "synthetic (random-init bf16 weights of the assumed 0.4B RWKV-7 arch, synthetic prompts)",
             "rtf": round(rtf, 6),
             "config": {"workload": "config3: 32 requests/GPU, P=32 prompt, 32 global + 512 semantic tokens, "
-                                   "exact sampler, LM only (HIP vocoder not yet in the timed path)",
+                                   "exact sampler, + BiCodec vocoder -> PCM",
                        "global_batch": B_PER_GPU * world, "seq_len": 32 + 33 + SEMANTIC,
                        "parallelism": f"dp{world} (request sharding)"},
             "roofline": roofline,
             "decode_step_roofline": step_roof,
+            "codec_roofline": codec_roof,
             "kernels": kernels,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line))
     rt.close()
+    voc.close()
     if world > 1:
         dist.destroy_process_group()
 
 
-def cpu_baseline(dims, seconds):
+def cpu_baseline(dims, cdims, seconds):
     """The oracle (C restatement of the reference path, f32 math on bf16 weights, 1 request,
     OpenMP over the host cores) timed on a bounded sample of the same request, extrapolated to
-    the full request (P + 33 + S - 1 forwards -> 320*S samples)."""
+    the full request (P + 33 + S - 1 forwards -> 320*S samples), plus the oracle vocoder timed
+    on a 16-frame utterance and scaled linearly to S frames (convolutions are linear in T)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     from rwkvtts import weights as W
@@ -218,10 +273,19 @@ def cpu_baseline(dims, seconds):
             break
     per_fwd = (time.perf_counter() - t0) / n
     fwd_per_req = 32 + 33 + SEMANTIC - 1
-    val = 320 * SEMANTIC / (fwd_per_req * per_fwd)
+    del om
+    from rwkvtts import codec as CC
+    cw = CC.synth_codec_blob(cdims)
+    Tc = 16
+    rs = np.random.default_rng(0)
+    t1 = time.perf_counter()
+    oracle.codec_decode(CC.make_codec_dims(cdims), cw, rs.integers(0, 8192, Tc), rs.integers(0, 4096, 32))
+    voc_s = (time.perf_counter() - t1) * SEMANTIC / Tc
+    val = 320 * SEMANTIC / (fwd_per_req * per_fwd + voc_s)
     return {"value": round(val, 1), "unit": "samples/s", "cores": cores, "kind": "port",
             "sample": f"oracle f32 RWKV-7 forward, 1 request, {n} forwards timed ({per_fwd*1e3:.1f} ms each), "
-                      f"extrapolated to {fwd_per_req} forwards / {320*SEMANTIC} samples; LM only"}
+                      f"extrapolated to {fwd_per_req} forwards; oracle vocoder on {Tc} frames scaled to "
+                      f"{SEMANTIC} ({voc_s:.2f} s); {320*SEMANTIC} samples per request"}
 
 
 if __name__ == "__main__":

@@ -289,6 +289,11 @@ int rwkvtts_codec_decode(rwkvtts_codec* c, const int64_t* semantic, int T, const
 /* decode_audio_batch (lightweight_tts_pipeline.rs:625-703): n utterances in one pass. */
 int rwkvtts_codec_decode_batch(rwkvtts_codec* c, const int64_t* const* semantic, const int* T,
                                const int64_t* const* global, int n, float* const* pcm);
+/* Per-stage HIP-event timing of later decode calls (profiling on): name, launches, total ms. */
+int rwkvtts_codec_set_profiling(rwkvtts_codec* c, int on);
+int rwkvtts_codec_profile_count(rwkvtts_codec* c);
+int rwkvtts_codec_profile_entry(rwkvtts_codec* c, int idx, char* name, int name_cap, int64_t* launches,
+                                double* total_ms);
 
 /* ---- zero-shot reference mel (src/tts_pipeline_fixes.rs:12-159) ------------------------- */
 /* wav [n] f32 @16 kHz -> mel [128][n_frames] (n_frames = (n + 1024 - 1024) / 320 + 1). */

@@ -143,3 +143,18 @@ class Model:
         lib().oracle_generate(self.h, ctypes.byref(request_struct), ctypes.byref(res))
         return (list(res.global_tokens[:res.n_global]), list(res.semantic_tokens[:res.n_semantic]),
                 res.n_forward)
+
+
+def codec_decode(dims_struct, weights: np.ndarray, semantic, global_tokens, threads: int = 0) -> np.ndarray:
+    """f32 CPU restatement of the BiCodec decoder (codec.c) -> PCM [T * 320]."""
+    if threads:
+        lib().oracle_set_threads(threads)
+    s = np.ascontiguousarray(semantic, dtype=np.int64)
+    g = np.ascontiguousarray(global_tokens, dtype=np.int64)
+    w = np.ascontiguousarray(weights, dtype=np.float32)
+    pcm = np.empty(s.size * 320, dtype=np.float32)
+    rc = lib().oracle_codec_decode(ctypes.byref(dims_struct), w.ctypes.data, s.ctypes.data, int(s.size),
+                                   g.ctypes.data, pcm.ctypes.data)
+    if rc != 0:
+        raise ValueError(f"oracle_codec_decode failed ({rc})")
+    return pcm

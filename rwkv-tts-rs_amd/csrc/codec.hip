@@ -1,0 +1,891 @@
+// codec.hip -- MI355X BiCodec decoder: replaces the ORT CPU session that runs
+// BiCodecDetokenize.onnx at src/lightweight_tts_pipeline.rs:706-730 (decode_audio :606-622,
+// decode_audio_batch :625-703).  Architecture: include/rwkvtts_codec_layout.h.
+//
+// Every conv / ConvTranspose / pointwise linear of the decoder runs through ONE implicit-GEMM
+// MFMA kernel (k_conv): D[t][co] = sum_{tap, ci} act(X[pos(t, tap)][ci]) * W[co][tap][ci], with
+//   * activations f32 channel-last [t][c] in HBM, staged into LDS as bf16 hi + lo planes
+//     (x = hi + lo to ~2^-17 relative) so two bf16 MFMAs give ~f32 products against the
+//     bf16 weights (the synthetic codec weights are bf16-exact);
+//   * the Snake1d of the producing block fused into the staging (x + sin^2(a x) / (a + 1e-9));
+//   * ConvTranspose1d(k, s, p=(k-s)/2) decomposed into s output phases, each a stride-1 conv
+//     with ceil((k - kr)/s) taps -- no zero-stuffed input, no wasted MACs;
+//   * bias, GELU, layer-scale gamma, residual add and a per-utterance bias (+ d_vector) fused
+//     into the epilogue.
+// Utterances of one batch run in the same launches (blockIdx.z), each with its own length.
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "common.h"
+#include "../../include/rwkvtts_codec_layout.h"
+
+namespace rwkvtts {
+
+typedef __bf16 cbf16x8 __attribute__((ext_vector_type(8)));
+
+struct ConvArgs {
+  const bf16_t* xh;  // input planes (already activated): x = hi + lo, channel-last [t][Ci]
+  const bf16_t* xl;
+  int64_t x_bs;      // per-utterance stride (elements)
+  int Ci, tin_mul;
+  const bf16_t* w;   // [Co][K][Ci]
+  int K, Co;
+  int mode;          // 0: conv (dil, pad), 1: ConvTranspose (stride s, pad (K - s) / 2)
+  int dil, pad, s;
+  const float* bias;   // [Co]
+  const float* rbias;  // per-utterance bias [n][Co] (nullable)
+  int64_t rb_bs;
+  const float* gamma;  // epilogue scale (nullable)
+  const float* res;    // f32 residual, layout of y (nullable; may alias y)
+  int act;             // 0 none, 1 exact GELU
+  float* y;            // f32 output (nullable)
+  bf16_t* yh;          // output planes (nullable): act_out(v) split hi + lo
+  bf16_t* yl;
+  const float* y_alpha;  // Snake1d alpha applied to the planes output (nullable)
+  int64_t y_bs;
+  const int* ntok;     // tokens per utterance; input length = ntok * tin_mul
+  const bf16_t* zeros; // >= 16 zero bytes (source of out-of-range window rows)
+};
+
+__device__ inline float snake(float v, float a) {
+  const float s = sinf(a * v);
+  return v + (1.0f / (a + 1e-9f)) * (s * s);
+}
+// Snake with the hardware sine (v_sin_f32; |error| ~1e-6 for the |a x| < ~100 seen here)
+__device__ inline float snake_fast(float v, float a) {
+  const float s = __sinf(a * v);
+  return v + (1.0f / (a + 1e-9f)) * (s * s);
+}
+__device__ inline void split_store(bf16_t* h, bf16_t* l, int64_t o, float v) {
+  const uint16_t hb = f32_to_bf16(v);
+  h[o] = hb;
+  l[o] = f32_to_bf16(v - bf16_to_f32(hb));
+}
+
+constexpr int kConvTM = 128;  // output rows (time) per workgroup
+
+// LDS image of a 32-channel chunk: 64-B rows of four 16-B pieces, piece p of row r stored at
+// slot p ^ ((r >> 1) & 3): the MFMA fragment reads (16 rows x 4 pieces per ds_read_b128 lane
+// group) are then bank-conflict free. The image is filled by global_load_lds_dwordx4 (one
+// 1-KiB, 16-row block per wave-instruction, LDS destination lane-linear), so the swizzle is
+// applied to each lane's SOURCE address and undone by the reads (the same involution).
+__device__ inline int swz(int row, int piece) { return row * 64 + ((piece ^ ((row >> 1) & 3)) << 4); }
+__device__ inline void glds16(const void* g, void* l) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+}
+
+// Workgroup = 4 waves along time, each 32 rows x TN channels (2 x TN/16 MFMA 16x16x32 tiles).
+// Per 32-channel chunk the workgroup stages (double-buffered, async global->LDS) the input
+// window that ALL taps read -- TM + (ntaps - 1) * |tap stride| rows of the hi and lo planes --
+// and the chunk of every tap's weights, then runs ntaps x 2 x NT x 2 MFMAs per wave while the
+// next chunk streams in.
+template <int TN, int KT>
+__global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
+  constexpr int TM = kConvTM, NT = TN / 16;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int req = blockIdx.z;
+  const int Tin = a.ntok[req] * a.tin_mul;
+  const int q0 = blockIdx.x * TM;
+  if (q0 >= Tin) return;
+  const int ncot = a.Co / TN;
+  const int phase = blockIdx.y / ncot, co0 = (blockIdx.y % ncot) * TN;
+  int ntaps, k0, kstep, pbase, pstep, ostr;
+  if (a.mode == 0) {
+    ntaps = a.K; k0 = 0; kstep = 1; pbase = -a.pad; pstep = a.dil; ostr = 1;
+  } else {
+    const int p = (a.K - a.s) / 2, kr = (phase + p) % a.s;
+    ntaps = (a.K - kr + a.s - 1) / a.s; k0 = kr; kstep = a.s; pbase = (phase + p - kr) / a.s;
+    pstep = -1; ostr = a.s;
+  }
+  const int span = (ntaps - 1) * (pstep < 0 ? -pstep : pstep);
+  const int WRp = (TM + span + 15) & ~15;  // window rows, whole 16-row blocks
+  const int wlo = pstep < 0 ? -span : 0;   // window row 0 <-> position q0 + pbase + wlo
+  const int wstart = q0 + pbase + wlo;
+  const int nAblk = 2 * WRp / 16, nblk = nAblk + ntaps * (TN / 16);
+  const int buf_bytes = nblk * 1024;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, g = lane >> 4;
+  const int64_t xoff = req * a.x_bs;
+  const int nck = a.Ci / 32;
+  const int lrow = lane >> 2, lslot = lane & 3;
+
+  // This wave's share of the chunk's 16-row blocks: per-lane source pointers at channel 0,
+  // computed once (a chunk adds c0); out-of-range window rows read the zero page.
+  constexpr int MAXB = 16;
+  const bf16_t* srcp[MAXB];
+#pragma unroll
+  for (int u = 0; u < MAXB; ++u) {
+    const int b = wave + 4 * u;
+    const bf16_t* src = a.zeros;
+    if (b < nAblk) {
+      const int plane = b >= WRp / 16, row = (b - plane * (WRp / 16)) * 16 + lrow;
+      const int piece = lslot ^ ((row >> 1) & 3), pos = wstart + row;
+      if (pos >= 0 && pos < Tin) src = (plane ? a.xl : a.xh) + xoff + (int64_t)pos * a.Ci + piece * 8;
+      else src = a.zeros + piece * 8;
+    } else if (b < nblk) {
+      const int wb = b - nAblk, tap = wb / (TN / 16), co = (wb % (TN / 16)) * 16 + lrow;
+      const int piece = lslot ^ ((co >> 1) & 3);
+      src = a.w + ((int64_t)(co0 + co) * a.K + k0 + tap * kstep) * a.Ci + piece * 8;
+    }
+    srcp[u] = src;
+  }
+  auto issue = [&](int ck, uint8_t* buf) {
+    const int c0 = ck * 32;
+#pragma unroll
+    for (int u = 0; u < MAXB; ++u) {
+      const int b = wave + 4 * u;
+      if (b < nblk) glds16(srcp[u] + c0, buf + b * 1024);
+    }
+  };
+
+  float4_ acc[2][NT];
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int n = 0; n < NT; ++n) acc[m][n] = (float4_){0.f, 0.f, 0.f, 0.f};
+
+  issue(0, lds);
+  for (int ck = 0; ck < nck; ++ck) {
+    __syncthreads();  // chunk ck has landed; every wave is done with the other buffer
+    uint8_t* cur = lds + (ck & 1) * buf_bytes;
+    if (ck + 1 < nck) issue(ck + 1, lds + ((ck + 1) & 1) * buf_bytes);
+    const uint8_t* sA = cur;
+    const uint8_t* sW = cur + nAblk * 1024;
+#pragma unroll
+    for (int j = 0; j < KT; ++j) {
+      if (j >= ntaps) break;
+      short8 bw[NT];
+#pragma unroll
+      for (int n = 0; n < NT; ++n) bw[n] = *(const short8*)(sW + j * TN * 64 + swz(n * 16 + li, g));
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        const int wr = wave * 32 + m * 16 + li + j * pstep - wlo;
+        const short8 ah = *(const short8*)(sA + swz(wr, g));
+        const short8 al = *(const short8*)(sA + WRp * 64 + swz(wr, g));
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(cbf16x8, ah),
+                                                              __builtin_bit_cast(cbf16x8, bw[n]), acc[m][n], 0, 0, 0);
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(cbf16x8, al),
+                                                              __builtin_bit_cast(cbf16x8, bw[n]), acc[m][n], 0, 0, 0);
+        }
+      }
+    }
+  }
+  // Epilogue. (1) bias / GELU / gamma in the MFMA layout (col = lane & 15 -> co,
+  // row = 4 * (lane >> 4) + j -> q), staged through this wave's LDS tile [32][TN + 4] f32;
+  // (2) read back row-contiguous so each lane moves 16 B of f32 (residual, y) and 8 B per
+  // plane, with the output Snake applied once per element.
+  __syncthreads();  // every wave is done with the chunk buffers
+  constexpr int LDE = TN + 4;
+  float* sE = (float*)lds + wave * 32 * LDE;
+#pragma unroll
+  for (int n = 0; n < NT; ++n) {
+    const int co = co0 + n * 16 + li;
+    const float b = a.bias[co] + (a.rbias ? a.rbias[req * a.rb_bs + co] : 0.0f);
+    const float gm = a.gamma ? a.gamma[co] : 1.0f;
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float v = acc[m][n][j] + b;
+        if (a.act == 1) v = 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
+        sE[(m * 16 + 4 * g + j) * LDE + n * 16 + li] = v * gm;
+      }
+  }
+  const int64_t yoff = req * a.y_bs;
+#pragma unroll
+  for (int it = 0; it < TN / 8; ++it) {
+    const int idx = lane + 64 * it, r = idx / (TN / 4), c4 = (idx % (TN / 4)) * 4;
+    const int q = q0 + wave * 32 + r;
+    if (q >= Tin) continue;
+    float4_ v = *(const float4_*)(sE + r * LDE + c4);
+    const int64_t o = yoff + (int64_t)(q * ostr + phase) * a.Co + co0 + c4;
+    if (a.res) v += *(const float4_*)(a.res + o);
+    if (a.y) *(float4_*)(a.y + o) = v;
+    if (a.yh) {
+      uint16_t h[4], l[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float pv = a.y_alpha ? snake_fast(v[e], a.y_alpha[co0 + c4 + e]) : v[e];
+        h[e] = f32_to_bf16(pv);
+        l[e] = f32_to_bf16(pv - bf16_to_f32(h[e]));
+      }
+      *(uint2*)(a.yh + o) = make_uint2(h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16));
+      *(uint2*)(a.yl + o) = make_uint2(l[0] | ((uint32_t)l[1] << 16), l[2] | ((uint32_t)l[3] << 16));
+    }
+  }
+}
+
+// semantic FVQ: z[t][c] = b[c] + sum_k W[c][k] * codebook[tok][k]   (-> planes)
+__global__ void k_fvq(const int* tok, int Tmax, const int* ntok, const float* cb, int cd,
+                      const float* w, const float* b, int L, bf16_t* zh, bf16_t* zl) {
+  const int t = blockIdx.x, req = blockIdx.y;
+  if (t >= ntok[req]) return;
+  const float* e = cb + (int64_t)tok[req * Tmax + t] * cd;
+  const int64_t base = ((int64_t)req * Tmax + t) * L;
+  for (int c = threadIdx.x; c < L; c += blockDim.x) {
+    float acc = 0.0f;
+    for (int k = 0; k < cd; ++k) acc += w[c * cd + k] * e[k];
+    split_store(zh, zl, base + c, acc + b[c]);
+  }
+}
+
+// speaker FSQ: h[c * G + t] = b[c] + sum_k W[c][k] * code_k(global[t])
+__global__ void k_fsq(const int* glob, int G, int levels, int dims, const float* w, const float* b,
+                      int Q, float* h) {
+  const int req = blockIdx.x;
+  for (int i = threadIdx.x; i < Q * G; i += blockDim.x) {
+    const int c = i / G, t = i % G;
+    int idx = glob[req * G + t];
+    const int half = levels / 2;
+    float acc = 0.0f;
+    for (int k = 0; k < dims; ++k) {
+      const float code = (float)((idx % levels) - half) / (float)half;
+      idx /= levels;
+      acc += w[c * dims + k] * code;
+    }
+    h[(int64_t)req * Q * G + i] = acc + b[c];
+  }
+}
+
+// out[req][r] = b[r] + W[r] . v[req]   (one wave per output row)
+__global__ __launch_bounds__(256) void k_gemv(const float* w, const float* b, int rows, int cols,
+                                              const float* v, int64_t v_bs, float* out, int64_t o_bs) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63, req = blockIdx.y;
+  if (r >= rows) return;
+  const float* wr = w + (int64_t)r * cols;
+  const float* vr = v + req * v_bs;
+  float acc = 0.0f;
+  for (int i = lane; i < cols; i += 64) acc += wr[i] * vr[i];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  if (lane == 0) out[req * o_bs + r] = acc + b[r];
+}
+
+// [optional depthwise conv k7 pad 3] -> LayerNorm (eps 1e-6) -> * scale + shift
+// scale/shift: [n][P] (AdaLN, stride P) or [P] (plain LN affine, stride 0).
+// Output: f32 y (nullable) and/or planes yh/yl (nullable).
+__global__ __launch_bounds__(128) void k_dw_ln(const float* x, float* y, bf16_t* yh, bf16_t* yl, int Tmax,
+                                               const int* ntok, int P, const float* dw_w, const float* dw_b,
+                                               const float* scale, const float* shift, int64_t ss_bs) {
+  constexpr int MAXV = 4;  // P <= 512
+  __shared__ float s_red[2][2];
+  const int t = blockIdx.x, req = blockIdx.y;
+  const int T = ntok[req];
+  if (t >= T) return;
+  const float* X = x + (int64_t)req * Tmax * P;
+  float v[MAXV];
+  float sum = 0.0f;
+#pragma unroll
+  for (int u = 0; u < MAXV; ++u) {
+    const int c = threadIdx.x + u * 128;
+    v[u] = 0.0f;
+    if (c < P) {
+      if (dw_w) {
+        float acc = 0.0f;
+        for (int k = 0; k < 7; ++k) {
+          const int p = t + k - 3;
+          if (p >= 0 && p < T) acc += dw_w[c * 7 + k] * X[(int64_t)p * P + c];
+        }
+        v[u] = acc + dw_b[c];
+      } else {
+        v[u] = X[(int64_t)t * P + c];
+      }
+      sum += v[u];
+    }
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+  if (lane == 0) s_red[0][wv] = sum;
+  __syncthreads();
+  const float mean = (s_red[0][0] + s_red[0][1]) / (float)P;
+  float sq = 0.0f;
+#pragma unroll
+  for (int u = 0; u < MAXV; ++u) {
+    const int c = threadIdx.x + u * 128;
+    if (c < P) sq += (v[u] - mean) * (v[u] - mean);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) sq += __shfl_xor(sq, o);
+  if (lane == 0) s_red[1][wv] = sq;
+  __syncthreads();
+  const float inv = 1.0f / sqrtf((s_red[1][0] + s_red[1][1]) / (float)P + 1e-6f);
+  const int64_t base = ((int64_t)req * Tmax + t) * P;
+#pragma unroll
+  for (int u = 0; u < MAXV; ++u) {
+    const int c = threadIdx.x + u * 128;
+    if (c < P) {
+      const float o = (v[u] - mean) * inv * scale[req * ss_bs + c] + shift[req * ss_bs + c];
+      if (y) y[base + c] = o;
+      if (yh) split_store(yh, yl, base + c, o);
+    }
+  }
+}
+
+// final conv7 (C -> 1) over the snake-activated planes -> tanh; 128 samples per workgroup,
+// the input window staged in LDS as f32 (hi + lo) with row stride C + 1 (conflict-free walks).
+__global__ __launch_bounds__(128) void k_conv_out(const bf16_t* xh, const bf16_t* xl, int64_t x_bs, int C,
+                                                  int tin_mul, const int* ntok, const float* w,
+                                                  const float* b, float* pcm, int64_t p_bs) {
+  extern __shared__ float s_x[];
+  const int req = blockIdx.y, T = ntok[req] * tin_mul, t0 = blockIdx.x * 128;
+  if (t0 >= T) return;
+  const int LDX = C + 1, rows = 128 + 6;
+  const int64_t xo = req * x_bs;
+  for (int i = threadIdx.x; i < rows * C; i += 128) {
+    const int r = i / C, c = i % C, p = t0 - 3 + r;
+    const int64_t o = xo + (int64_t)p * C + c;
+    s_x[r * LDX + c] = (p >= 0 && p < T) ? bf16_to_f32(xh[o]) + bf16_to_f32(xl[o]) : 0.0f;
+  }
+  __syncthreads();
+  const int t = t0 + threadIdx.x;
+  if (t >= T) return;
+  float acc = 0.0f;
+  for (int k = 0; k < 7; ++k) {
+    const float* xr = s_x + (threadIdx.x + k) * LDX;
+    const float* wr = w + k * C;
+    for (int c = 0; c < C; ++c) acc += wr[c] * xr[c];
+  }
+  pcm[req * p_bs + t] = tanhf(acc + b[0]);
+}
+
+__global__ void k_f32_to_bf16(const float* in, bf16_t* out, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = f32_to_bf16(in[i]);
+}
+
+// ------------------------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------------------------
+struct Planes {  // activated activations as bf16 hi + lo (x = hi + lo)
+  bf16_t* h = nullptr;
+  bf16_t* l = nullptr;
+};
+
+class Codec {
+ public:
+  rwkvtts_codec_dims d{};
+  int device = 0;
+  hipStream_t stream = nullptr;
+  float* wf = nullptr;   // f32 blob on device
+  bf16_t* zeros = nullptr;
+  bf16_t* wb = nullptr;  // bf16 mirror (same element offsets) for MFMA operands
+  int cap_n = 0, cap_T = 0;
+  int *d_tok = nullptr, *d_glob = nullptr, *d_ntok = nullptr;
+  // prenet: x f32 residual stream [n][T][P]; zp/up/hp planes [n][T][L|P|I]
+  float *xb = nullptr, *hs = nullptr, *dvec = nullptr, *cond = nullptr, *pcm = nullptr;
+  Planes zp, up, hp;
+  // WaveGenerator: xf f32 residual stream and two planes buffers, big_per_tok elements per frame
+  float* xf = nullptr;
+  Planes pp[2];
+  int64_t big_per_tok = 0;
+  std::vector<void*> bufs;
+  // profiling (HIP events around each launch class)
+  bool profiling = false;
+  std::vector<std::pair<std::string, std::pair<int64_t, double>>> prof;
+
+  ~Codec() {
+    release();
+    if (wf) (void)hipFree(wf);
+    if (wb) (void)hipFree(wb);
+    if (zeros) (void)hipFree(zeros);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+  void release() {
+    for (void* p : bufs) (void)hipFree(p);
+    bufs.clear();
+    cap_n = cap_T = 0;
+  }
+  template <typename T>
+  int dalloc(T** p, int64_t count) {
+    RT_HIP(hipMalloc((void**)p, count * sizeof(T)));
+    bufs.push_back(*p);
+    return RWKVTTS_OK;
+  }
+  int palloc(Planes* p, int64_t count) {
+    int rc = dalloc(&p->h, 2 * count);
+    p->l = p->h + count;
+    return rc;
+  }
+  const float* F(int g, int i, int t) const { return wf + rwkvtts_codec_offset(&d, g, i, t); }
+  const bf16_t* B(int g, int i, int t) const { return wb + rwkvtts_codec_offset(&d, g, i, t); }
+
+  int init(int dev, const rwkvtts_codec_dims& dims, const float* host_w) {
+    d = dims;
+    device = dev;
+    RT_CHECK(d.n_up >= 1 && d.n_up <= 4 && d.latent_dim == d.spk_dim && d.prenet_dim <= 512 &&
+                 d.fsq_dims <= 16 && d.codebook_dim <= 64 && d.fsq_levels >= 2,
+             RWKVTTS_EINVAL, "codec: unsupported dims");
+    RT_CHECK(d.latent_dim % 64 == 0 && d.prenet_dim % 64 == 0 && d.prenet_inter % 64 == 0 &&
+                 (d.dec_channels >> d.n_up) % 32 == 0 && (d.dec_channels >> d.n_up) <= 112,
+             RWKVTTS_EINVAL, "codec: channel counts must be multiples of 64 (last stage: of 32, <= 112)");
+    for (int i = 0; i < d.n_up; ++i)
+      RT_CHECK(d.up_rates[i] >= 1 && d.up_kernels[i] >= d.up_rates[i] && ((d.up_kernels[i] - d.up_rates[i]) % 2) == 0 &&
+                   (d.up_kernels[i] + d.up_rates[i] - 1) / d.up_rates[i] <= 8,
+               RWKVTTS_EINVAL, "codec: ConvTranspose needs k >= s, even k - s and <= 8 taps per phase");
+    RT_HIP(hipSetDevice(device));
+    RT_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+#define RT_CONV_ATTR(TN, KT) \
+    RT_HIP(hipFuncSetAttribute((const void*)k_conv<TN, KT>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    RT_CONV_ATTR(32, 1) RT_CONV_ATTR(32, 3) RT_CONV_ATTR(32, 7)
+    RT_CONV_ATTR(64, 1) RT_CONV_ATTR(64, 3) RT_CONV_ATTR(64, 7)
+    RT_CONV_ATTR(96, 1)
+#undef RT_CONV_ATTR
+    // zero page: out-of-range window rows read zeros at channel offsets up to the largest Ci
+    RT_HIP(hipMalloc(&zeros, 16384));
+    RT_HIP(hipMemset(zeros, 0, 16384));
+    const int64_t n = rwkvtts_codec_offset(&d, -1, 0, 0);
+    RT_HIP(hipMalloc(&wf, n * sizeof(float)));
+    RT_HIP(hipMalloc(&wb, n * sizeof(bf16_t)));
+    RT_HIP(hipMemcpy(wf, host_w, n * sizeof(float), hipMemcpyHostToDevice));
+    k_f32_to_bf16<<<2048, 256, 0, stream>>>(wf, wb, n);
+    RT_HIP(hipGetLastError());
+    RT_HIP(hipStreamSynchronize(stream));
+    // largest per-frame activation of the WaveGenerator (conv_in or any up stage)
+    big_per_tok = (int64_t)d.dec_channels;
+    int64_t mul = 1;
+    for (int i = 0; i < d.n_up; ++i) {
+      mul *= d.up_rates[i];
+      big_per_tok = std::max(big_per_tok, mul * (int64_t)(d.dec_channels >> (i + 1)));
+    }
+    return RWKVTTS_OK;
+  }
+
+  int ensure(int n, int T) {
+    if (n <= cap_n && T <= cap_T) return RWKVTTS_OK;
+    release();
+    const int64_t nt = (int64_t)n * T;
+    const int Q = RWKVTTS_CODEC_SPK_LATENT;
+    int rc = 0;
+    rc |= dalloc(&d_tok, nt);
+    rc |= dalloc(&d_glob, (int64_t)n * d.n_global);
+    rc |= dalloc(&d_ntok, n);
+    rc |= dalloc(&xb, nt * d.prenet_dim);
+    rc |= palloc(&zp, nt * d.latent_dim);
+    rc |= palloc(&up, nt * d.prenet_dim);
+    rc |= palloc(&hp, nt * d.prenet_inter);
+    rc |= dalloc(&hs, (int64_t)n * Q * d.n_global);
+    rc |= dalloc(&dvec, (int64_t)n * d.spk_dim);
+    rc |= dalloc(&cond, (int64_t)n * 2 * (d.prenet_layers + 1) * d.prenet_dim);
+    rc |= dalloc(&xf, nt * big_per_tok);
+    rc |= palloc(&pp[0], nt * big_per_tok);
+    rc |= palloc(&pp[1], nt * big_per_tok);
+    rc |= dalloc(&pcm, nt * RWKVTTS_HOP);
+    if (rc) return RWKVTTS_EHIP;
+    cap_n = n;
+    cap_T = T;
+    return RWKVTTS_OK;
+  }
+
+  hipEvent_t ev0 = nullptr;
+  void pbeg() {
+    if (!profiling) return;
+    (void)hipEventCreate(&ev0);
+    (void)hipEventRecord(ev0, stream);
+  }
+  void pend(const char* name) {
+    if (!profiling) return;
+    hipEvent_t e1;
+    (void)hipEventCreate(&e1);
+    (void)hipEventRecord(e1, stream);
+    (void)hipEventSynchronize(e1);
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, ev0, e1);
+    (void)hipEventDestroy(ev0);
+    (void)hipEventDestroy(e1);
+    for (auto& p : prof)
+      if (p.first == name) {
+        p.second.first++;
+        p.second.second += ms;
+        return;
+      }
+    prof.push_back({name, {1, (double)ms}});
+  }
+
+  // One implicit-GEMM conv launch. Output: f32 y and/or planes (snake(y_alpha) applied).
+  struct ConvOut {
+    float* y = nullptr;
+    Planes p{};
+    const float* alpha = nullptr;
+    const float* res = nullptr;
+    const float* gamma = nullptr;
+    const float* rbias = nullptr;
+    int64_t rb_bs = 0;
+    int act = 0;
+    int64_t y_bs = -1;  // per-utterance stride of y / planes / res (-1: same as the input's)
+  };
+  std::string stage_name(const char* base, int C) { return profiling ? std::string(base) + "@" + std::to_string(C) : std::string(); }
+  int conv(int n, int Tmax, const std::string& name, Planes x, int64_t bs, int Ci, int tin_mul, const bf16_t* w,
+           int K, int Co, int mode, int dil, int pad, int s, const float* bias, const ConvOut& o) {
+    RT_CHECK(Ci % 32 == 0 && Co % 32 == 0, RWKVTTS_EINVAL, "codec conv: channels must be multiples of 32");
+    const int TN = (Co % 64 == 0) ? 64 : ((Co % 96 == 0 && K == 1) ? 96 : 32);
+    const int ntaps_max = mode == 1 ? (K + s - 1) / s : K;
+    const int span = (ntaps_max - 1) * (mode == 1 ? 1 : dil);
+    const int WRp = (kConvTM + span + 15) & ~15;
+    const size_t shm = std::max(2 * (size_t)(2 * WRp + ntaps_max * TN) * 64,        // two chunk buffers
+                                (size_t)4 * 32 * (TN + 4) * sizeof(float));          // epilogue tiles
+    RT_CHECK(shm <= 160 * 1024 && (2 * WRp + ntaps_max * TN) / 16 <= 64 && ntaps_max <= 7 && Ci <= 4096,
+             RWKVTTS_EINVAL, "codec conv: tile window too large");
+    ConvArgs a;
+    a.xh = x.h; a.xl = x.l; a.x_bs = bs; a.Ci = Ci; a.tin_mul = tin_mul; a.w = w; a.K = K; a.Co = Co;
+    a.mode = mode; a.dil = dil; a.pad = pad; a.s = s; a.bias = bias; a.rbias = o.rbias; a.rb_bs = o.rb_bs;
+    a.gamma = o.gamma; a.res = o.res; a.act = o.act; a.y = o.y; a.yh = o.p.h; a.yl = o.p.l;
+    a.y_alpha = o.alpha; a.y_bs = o.y_bs >= 0 ? o.y_bs : bs; a.ntok = d_ntok; a.zeros = zeros;
+    const int phases = mode == 1 ? s : 1;
+    dim3 grid((unsigned)((Tmax * (int64_t)tin_mul + kConvTM - 1) / kConvTM), (unsigned)(phases * (Co / TN)), (unsigned)n);
+    pbeg();
+    const int KT = ntaps_max <= 1 ? 1 : (ntaps_max <= 3 ? 3 : 7);
+    if (TN == 96) k_conv<96, 1><<<grid, 256, shm, stream>>>(a);
+    else if (TN == 64) {
+      if (KT == 1) k_conv<64, 1><<<grid, 256, shm, stream>>>(a);
+      else if (KT == 3) k_conv<64, 3><<<grid, 256, shm, stream>>>(a);
+      else k_conv<64, 7><<<grid, 256, shm, stream>>>(a);
+    } else {
+      if (KT == 1) k_conv<32, 1><<<grid, 256, shm, stream>>>(a);
+      else if (KT == 3) k_conv<32, 3><<<grid, 256, shm, stream>>>(a);
+      else k_conv<32, 7><<<grid, 256, shm, stream>>>(a);
+    }
+    RT_HIP(hipGetLastError());
+    pend(name.c_str());
+    return RWKVTTS_OK;
+  }
+
+  // Decode n utterances; semantic[i] has T[i] codes, global[i] n_global codes; pcm[i] gets T[i]*320.
+  int decode(const int64_t* const* semantic, const int* T, const int64_t* const* global, int n,
+             float* const* out) {
+    RT_CHECK(n > 0, RWKVTTS_EINVAL, "codec decode: n must be > 0");
+    int Tmax = 0;
+    for (int i = 0; i < n; ++i) {
+      RT_CHECK(semantic[i] && global[i] && out[i] && T[i] > 0, RWKVTTS_EINVAL, "codec decode: bad utterance");
+      Tmax = std::max(Tmax, T[i]);
+    }
+    int n_codes = 1;
+    for (int i = 0; i < d.fsq_dims; ++i) n_codes *= d.fsq_levels;
+    std::vector<int> tok((size_t)n * Tmax, 0), glob((size_t)n * d.n_global), ntok(T, T + n);
+    for (int i = 0; i < n; ++i) {
+      for (int t = 0; t < T[i]; ++t) {
+        RT_CHECK(semantic[i][t] >= 0 && semantic[i][t] < d.codebook_size, RWKVTTS_EINVAL,
+                 "codec decode: semantic code out of range");
+        tok[(size_t)i * Tmax + t] = (int)semantic[i][t];
+      }
+      for (int t = 0; t < d.n_global; ++t) {
+        RT_CHECK(global[i][t] >= 0 && global[i][t] < n_codes, RWKVTTS_EINVAL,
+                 "codec decode: global code out of range");
+        glob[(size_t)i * d.n_global + t] = (int)global[i][t];
+      }
+    }
+    RT_HIP(hipSetDevice(device));
+    int rc = ensure(n, Tmax);
+    if (rc) return rc;
+    RT_HIP(hipMemcpyAsync(d_tok, tok.data(), tok.size() * sizeof(int), hipMemcpyHostToDevice, stream));
+    RT_HIP(hipMemcpyAsync(d_glob, glob.data(), glob.size() * sizeof(int), hipMemcpyHostToDevice, stream));
+    RT_HIP(hipMemcpyAsync(d_ntok, ntok.data(), n * sizeof(int), hipMemcpyHostToDevice, stream));
+    rc = forward(n, Tmax);
+    if (rc) return rc;
+    for (int i = 0; i < n; ++i)
+      RT_HIP(hipMemcpyAsync(out[i], pcm + (int64_t)i * Tmax * RWKVTTS_HOP, (size_t)T[i] * RWKVTTS_HOP * sizeof(float),
+                            hipMemcpyDeviceToHost, stream));
+    RT_HIP(hipStreamSynchronize(stream));
+    return RWKVTTS_OK;
+  }
+
+  int forward(int n, int Tmax) {
+    const int L = d.latent_dim, P = d.prenet_dim, I = d.prenet_inter, S = d.spk_dim, G = d.n_global;
+    const int Q = RWKVTTS_CODEC_SPK_LATENT;
+    const int64_t tL = (int64_t)Tmax * L, tP = (int64_t)Tmax * P, tI = (int64_t)Tmax * I;
+    const int64_t cstr = 2 * (int64_t)(d.prenet_layers + 1) * P;  // cond stride per utterance
+    int rc;
+    // speaker d-vector and every AdaLN scale/shift (cond[req][2 * (layer + 1) + {0, 1}][P])
+    pbeg();
+    k_fsq<<<n, 256, 0, stream>>>(d_glob, G, d.fsq_levels, d.fsq_dims, F(0, 0, CD_FSQ_W), F(0, 0, CD_FSQ_B), Q, hs);
+    k_gemv<<<dim3((S + 3) / 4, n), 256, 0, stream>>>(F(0, 0, CD_SPK_W), F(0, 0, CD_SPK_B), S, Q * G, hs,
+                                                     (int64_t)Q * G, dvec, S);
+    for (int l = -1; l < d.prenet_layers; ++l) {
+      const float* sw = l < 0 ? F(0, 0, CD_N0_SW) : F(1, l, CB_SW);
+      const float* sb = l < 0 ? F(0, 0, CD_N0_SB) : F(1, l, CB_SB);
+      const float* hw = l < 0 ? F(0, 0, CD_N0_HW) : F(1, l, CB_HW);
+      const float* hb = l < 0 ? F(0, 0, CD_N0_HB) : F(1, l, CB_HB);
+      k_gemv<<<dim3((P + 3) / 4, n), 256, 0, stream>>>(sw, sb, P, S, dvec, S, cond + 2 * (l + 1) * P, cstr);
+      k_gemv<<<dim3((P + 3) / 4, n), 256, 0, stream>>>(hw, hb, P, S, dvec, S, cond + (2 * (l + 1) + 1) * P, cstr);
+    }
+    k_fvq<<<dim3(Tmax, n), 256, 0, stream>>>(d_tok, Tmax, d_ntok, F(0, 0, CD_CODEBOOK), d.codebook_dim,
+                                            F(0, 0, CD_OUTP_W), F(0, 0, CD_OUTP_B), L, zp.h, zp.l);
+    RT_HIP(hipGetLastError());
+    pend("codec_cond");
+    // prenet: linear_pre -> embed conv7 -> AdaLN0 -> ConvNeXt blocks -> LN -> linear (+ d)
+    {
+      ConvOut o;
+      o.p = up;
+      o.y_bs = tP;
+      if ((rc = conv(n, Tmax, "codec_prenet_gemm", zp, tL, L, 1, B(0, 0, CD_PRE_W), 1, P, 0, 1, 0, 1,
+                     F(0, 0, CD_PRE_B), o))) return rc;
+      ConvOut e;
+      e.y = xb;
+      if ((rc = conv(n, Tmax, "codec_prenet_gemm", up, tP, P, 1, B(0, 0, CD_EMB_W), 7, P, 0, 1, 3, 1,
+                     F(0, 0, CD_EMB_B), e))) return rc;
+    }
+    pbeg();
+    k_dw_ln<<<dim3(Tmax, n), 128, 0, stream>>>(xb, xb, nullptr, nullptr, Tmax, d_ntok, P, nullptr, nullptr, cond,
+                                               cond + P, cstr);
+    RT_HIP(hipGetLastError());
+    pend("codec_ln");
+    for (int l = 0; l < d.prenet_layers; ++l) {
+      pbeg();
+      k_dw_ln<<<dim3(Tmax, n), 128, 0, stream>>>(xb, nullptr, up.h, up.l, Tmax, d_ntok, P, F(1, l, CB_DW_W),
+                                                 F(1, l, CB_DW_B), cond + 2 * (l + 1) * P,
+                                                 cond + (2 * (l + 1) + 1) * P, cstr);
+      RT_HIP(hipGetLastError());
+      pend("codec_ln");
+      ConvOut o1;
+      o1.p = hp;
+      o1.act = 1;
+      o1.y_bs = tI;
+      if ((rc = conv(n, Tmax, "codec_prenet_gemm", up, tP, P, 1, B(1, l, CB_PW1_W), 1, I, 0, 1, 0, 1,
+                     F(1, l, CB_PW1_B), o1))) return rc;
+      ConvOut o2;
+      o2.y = xb;
+      o2.res = xb;
+      o2.gamma = F(1, l, CB_GAMMA);
+      o2.y_bs = tP;
+      if ((rc = conv(n, Tmax, "codec_prenet_gemm", hp, tI, I, 1, B(1, l, CB_PW2_W), 1, P, 0, 1, 0, 1,
+                     F(1, l, CB_PW2_B), o2))) return rc;
+    }
+    pbeg();
+    k_dw_ln<<<dim3(Tmax, n), 128, 0, stream>>>(xb, nullptr, up.h, up.l, Tmax, d_ntok, P, nullptr, nullptr,
+                                               F(0, 0, CD_FLN_W), F(0, 0, CD_FLN_B), 0);
+    RT_HIP(hipGetLastError());
+    pend("codec_ln");
+    {
+      ConvOut o;
+      o.p = zp;
+      o.rbias = dvec;
+      o.rb_bs = S;
+      o.y_bs = tL;
+      if ((rc = conv(n, Tmax, "codec_prenet_gemm", up, tP, P, 1, B(0, 0, CD_LIN_W), 1, L, 0, 1, 0, 1,
+                     F(0, 0, CD_LIN_B), o))) return rc;
+    }
+    // WaveGenerator: conv_in -> [snake -> convT -> 3 x residual unit] x n_up -> snake -> conv_out
+    const int64_t bs = (int64_t)Tmax * big_per_tok;
+    int C = d.dec_channels, mul = 1, cur = 0;
+    {
+      ConvOut o;
+      o.p = pp[cur];
+      o.alpha = F(2, 0, CU_SNAKE);
+      // conv_in reads the prenet planes with the prenet's per-utterance stride
+      o.y_bs = bs;
+      if ((rc = conv(n, Tmax, "codec_conv_in", zp, tL, L, 1, B(0, 0, CD_CIN_W), 7, C, 0, 1, 3, 1,
+                     F(0, 0, CD_CIN_B), o))) return rc;
+    }
+    static const int dils[3] = {1, 3, 9};
+    for (int ub = 0; ub < d.n_up; ++ub) {
+      const int Co = C / 2, s = d.up_rates[ub], K = d.up_kernels[ub];
+      ConvOut ot;
+      ot.y = xf;
+      ot.p = pp[cur ^ 1];
+      ot.alpha = F(2, ub, CU_R0_A1);
+      if ((rc = conv(n, Tmax, stage_name("codec_convT", Co), pp[cur], bs, C, mul, B(2, ub, CU_T_W), K, Co, 1, 1, 0, s,
+                     F(2, ub, CU_T_B), ot))) return rc;
+      cur ^= 1;
+      mul *= s;
+      C = Co;
+      for (int r = 0; r < 3; ++r) {
+        const int o = r * (CU_R1_A1 - CU_R0_A1);
+        ConvOut o7;
+        o7.p = pp[cur ^ 1];
+        o7.alpha = F(2, ub, CU_R0_A2 + o);
+        if ((rc = conv(n, Tmax, stage_name("codec_res_conv7", C), pp[cur], bs, C, mul, B(2, ub, CU_R0_W7 + o), 7, C, 0, dils[r],
+                       3 * dils[r], 1, F(2, ub, CU_R0_B7 + o), o7))) return rc;
+        cur ^= 1;
+        ConvOut o1;
+        o1.y = xf;
+        o1.res = xf;
+        o1.p = pp[cur ^ 1];
+        o1.alpha = r < 2 ? F(2, ub, CU_R0_A1 + o + (CU_R1_A1 - CU_R0_A1))
+                         : (ub + 1 < d.n_up ? F(2, ub + 1, CU_SNAKE) : F(0, 0, CD_SOUT_A));
+        if ((rc = conv(n, Tmax, stage_name("codec_res_conv1", C), pp[cur], bs, C, mul, B(2, ub, CU_R0_W1 + o), 1, C, 0, 1, 0, 1,
+                       F(2, ub, CU_R0_B1 + o), o1))) return rc;
+        cur ^= 1;
+      }
+    }
+    pbeg();
+    const size_t shm = (size_t)(128 + 6) * (C + 1) * sizeof(float);
+    k_conv_out<<<dim3((unsigned)((Tmax * (int64_t)mul + 127) / 128), n), 128, shm, stream>>>(
+        pp[cur].h, pp[cur].l, bs, C, mul, d_ntok, F(0, 0, CD_COUT_W), F(0, 0, CD_COUT_B), pcm,
+        (int64_t)Tmax * RWKVTTS_HOP);
+    RT_HIP(hipGetLastError());
+    pend("codec_conv_out");
+    return RWKVTTS_OK;
+  }
+
+};
+
+// ---- synthetic weights (counter-based, deterministic) -----------------------------------
+static inline uint64_t cmix(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+static inline double cnormal(uint64_t h) {
+  const double s = (double)(h & 0xFFFF) + (double)((h >> 16) & 0xFFFF) + (double)((h >> 32) & 0xFFFF) +
+                   (double)((h >> 48) & 0xFFFF);
+  return (s / 65536.0 - 2.0) * 1.7320508075688772;
+}
+static inline double cuniform(uint64_t h) { return (double)(h >> 11) * (1.0 / 9007199254740992.0); }
+
+// (scale kind, std) of each tensor; bf16 = used as an MFMA operand (stored bf16-exact)
+static void codec_init_rule(const rwkvtts_codec_dims* d, int g, int idx, int t, int* kind, double* sd, int* bf16) {
+  const double L = d->latent_dim, P = d->prenet_dim, I = d->prenet_inter, S = d->spk_dim;
+  *kind = 0; *sd = 0.02; *bf16 = 0;  // kind 0: sd * normal, 1: 1 + sd * normal, 2: 0.5 + uniform, 3: const sd
+  if (g == 0) {
+    switch (t) {
+      case CD_CODEBOOK: *sd = 1.0; break;
+      case CD_OUTP_W: *sd = 1.0 / sqrt((double)d->codebook_dim); break;
+      case CD_FSQ_W: *sd = 1.0 / sqrt((double)d->fsq_dims); break;
+      case CD_SPK_W: *sd = 1.0 / sqrt((double)RWKVTTS_CODEC_SPK_LATENT * d->n_global); break;
+      case CD_PRE_W: *sd = 1.0 / sqrt(L); *bf16 = 1; break;
+      case CD_EMB_W: *sd = 1.0 / sqrt(7.0 * P); *bf16 = 1; break;
+      case CD_N0_SW: case CD_N0_HW: *sd = 0.1 / sqrt(S); break;
+      case CD_N0_SB: *kind = 1; break;
+      case CD_FLN_W: *kind = 1; *sd = 0.05; break;
+      case CD_LIN_W: *sd = 1.0 / sqrt(P); *bf16 = 1; break;
+      case CD_CIN_W: *sd = 1.0 / sqrt(7.0 * L); *bf16 = 1; break;
+      case CD_SOUT_A: *kind = 2; break;
+      case CD_COUT_W: *sd = 0.2 / sqrt(7.0 * (d->dec_channels >> d->n_up)); break;
+      default: break;
+    }
+    return;
+  }
+  if (g == 1) {
+    switch (t) {
+      case CB_DW_W: *sd = 1.0 / sqrt(7.0); break;
+      case CB_SW: case CB_HW: *sd = 0.1 / sqrt(S); break;
+      case CB_SB: *kind = 1; break;
+      case CB_PW1_W: *sd = 1.0 / sqrt(P); *bf16 = 1; break;
+      case CB_PW2_W: *sd = 1.0 / sqrt(I); *bf16 = 1; break;
+      case CB_GAMMA: *kind = 3; *sd = 1.0 / d->prenet_layers; break;
+      default: break;
+    }
+    return;
+  }
+  const double Ci = d->dec_channels >> idx, Co = d->dec_channels >> (idx + 1);
+  switch (t) {
+    case CU_SNAKE: case CU_R0_A1: case CU_R0_A2: case CU_R1_A1: case CU_R1_A2: case CU_R2_A1: case CU_R2_A2:
+      *kind = 2; break;
+    case CU_T_W: *sd = 1.0 / sqrt(Ci * d->up_kernels[idx] / d->up_rates[idx]); *bf16 = 1; break;
+    case CU_R0_W7: case CU_R1_W7: case CU_R2_W7: *sd = 0.5 / sqrt(7.0 * Co); *bf16 = 1; break;
+    case CU_R0_W1: case CU_R1_W1: case CU_R2_W1: *sd = 0.5 / sqrt(Co); *bf16 = 1; break;
+    default: break;
+  }
+}
+
+}  // namespace rwkvtts
+
+using namespace rwkvtts;
+
+struct rwkvtts_codec {
+  Codec c;
+};
+
+extern "C" {
+
+int64_t rwkvtts_codec_blob_bytes(const rwkvtts_codec_dims* d) {
+  if (!d) return -1;
+  return rwkvtts_codec_offset(d, -1, 0, 0) * (int64_t)sizeof(float);
+}
+
+int rwkvtts_codec_synth_weights(const rwkvtts_codec_dims* d, uint64_t seed, float* out) {
+  RT_CHECK(d && out, RWKVTTS_EINVAL, "codec_synth_weights: null argument");
+  const int64_t total = rwkvtts_codec_offset(d, -1, 0, 0);
+  memset(out, 0, total * sizeof(float));
+  memcpy(out, d, sizeof(*d));  // header: dims
+  for (int g = 0; g < 3; ++g) {
+    const int nidx = g == 0 ? 1 : (g == 1 ? d->prenet_layers : d->n_up);
+    const int nt = g == 0 ? CD_GLOBAL_COUNT : (g == 1 ? CB_COUNT : CU_COUNT);
+    for (int i = 0; i < nidx; ++i)
+      for (int t = 0; t < nt; ++t) {
+        int kind, bf;
+        double sd;
+        codec_init_rule(d, g, i, t, &kind, &sd, &bf);
+        const uint64_t key = cmix(seed ^ (0xA0761D6478BD642Full * (uint64_t)((g * 64 + i) * 64 + t + 1)));
+        float* p = out + rwkvtts_codec_offset(d, g, i, t);
+        const int64_t n = rwkvtts_codec_numel(d, g, i, t);
+        for (int64_t e = 0; e < n; ++e) {
+          const uint64_t h = cmix(key ^ (uint64_t)e);
+          double v = kind == 0 ? sd * cnormal(h) : kind == 1 ? 1.0 + sd * cnormal(h) : kind == 2 ? 0.5 + cuniform(h) : sd;
+          float f = (float)v;
+          if (bf) f = bf16_to_f32(f32_to_bf16(f));
+          p[e] = f;
+        }
+      }
+  }
+  return RWKVTTS_OK;
+}
+
+int rwkvtts_codec_create(int device, const rwkvtts_codec_dims* d, const float* weights, rwkvtts_codec** out) {
+  RT_CHECK(d && weights && out, RWKVTTS_EINVAL, "codec_create: null argument");
+  *out = nullptr;
+  try {
+    rwkvtts_codec* c = new rwkvtts_codec();
+    const int rc = c->c.init(device, *d, weights);
+    if (rc != RWKVTTS_OK) {
+      delete c;
+      return rc;
+    }
+    *out = c;
+    return RWKVTTS_OK;
+  } catch (const std::exception& ex) {
+    set_error(ex.what());
+    return RWKVTTS_ENOMEM;
+  }
+}
+
+int rwkvtts_codec_destroy(rwkvtts_codec* c) {
+  delete c;
+  return RWKVTTS_OK;
+}
+
+int rwkvtts_codec_decode(rwkvtts_codec* c, const int64_t* semantic, int T, const int64_t* global, float* pcm) {
+  RT_CHECK(c && semantic && global && pcm && T > 0, RWKVTTS_EINVAL, "codec_decode: bad arguments");
+  return c->c.decode(&semantic, &T, &global, 1, &pcm);
+}
+
+int rwkvtts_codec_decode_batch(rwkvtts_codec* c, const int64_t* const* semantic, const int* T,
+                               const int64_t* const* global, int n, float* const* pcm) {
+  RT_CHECK(c && semantic && T && global && pcm && n > 0, RWKVTTS_EINVAL, "codec_decode_batch: bad arguments");
+  try {
+    return c->c.decode(semantic, T, global, n, pcm);
+  } catch (const std::exception& ex) {
+    set_error(ex.what());
+    return RWKVTTS_ENOMEM;
+  }
+}
+
+int rwkvtts_codec_set_profiling(rwkvtts_codec* c, int on) {
+  RT_CHECK(c, RWKVTTS_EINVAL, "null codec");
+  c->c.profiling = on != 0;
+  c->c.prof.clear();
+  return RWKVTTS_OK;
+}
+
+int rwkvtts_codec_profile_entry(rwkvtts_codec* c, int idx, char* name, int name_cap, int64_t* launches,
+                                double* total_ms) {
+  RT_CHECK(c && idx >= 0 && idx < (int)c->c.prof.size(), RWKVTTS_EINVAL, "profile index out of range");
+  const auto& p = c->c.prof[idx];
+  if (name && name_cap > 0) {
+    strncpy(name, p.first.c_str(), name_cap - 1);
+    name[name_cap - 1] = 0;
+  }
+  if (launches) *launches = p.second.first;
+  if (total_ms) *total_ms = p.second.second;
+  return RWKVTTS_OK;
+}
+
+int rwkvtts_codec_profile_count(rwkvtts_codec* c) { return c ? (int)c->c.prof.size() : -1; }
+
+}  // extern "C"

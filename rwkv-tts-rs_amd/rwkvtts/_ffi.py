@@ -110,6 +110,10 @@ EXPORTS = {
                                             ctypes.c_void_p]),
     "rwkvtts_codec_decode_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                   ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
+    "rwkvtts_codec_set_profiling": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "rwkvtts_codec_profile_count": (ctypes.c_int, [ctypes.c_void_p]),
+    "rwkvtts_codec_profile_entry": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
+                                                   ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)]),
     "rwkvtts_mel": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                                    ctypes.POINTER(ctypes.c_int)]),
 }
