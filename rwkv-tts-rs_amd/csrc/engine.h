@@ -16,6 +16,7 @@ struct LayerW {
   const float* mu[6];  // x_r x_w x_k x_v x_a x_g
   const float *w0, *a0, *v0, *k_k, *k_a, *r_k, *lnx_w, *lnx_b, *ffn_xk;
   const bf16_t *wr, *wk, *wv, *wo, *w1t, *a1t, *v1t, *g1t, *w2t, *a2t, *v2t, *g2t, *ffn_k, *ffn_v;
+  const bf16_t* lup;  // LoRA-up rows repacked for k_wkv
 };
 
 // One forward step description (host side).
@@ -65,6 +66,7 @@ class Engine {
   void prof_begin(hipEvent_t* ev);
   void prof_end(const char* name, hipEvent_t ev);
   int flush_prof();
+  int dump_stamps();
 
   int device_ = 0;
   hipStream_t stream_ = nullptr;
@@ -72,6 +74,7 @@ class Engine {
   int splitA_ = 1, splitO_ = 1, splitK_ = 1, splitF_ = 1, splitH_ = 1;
   bool use_graphs_ = true;
   uint8_t* wblob_ = nullptr;
+  bf16_t* lora_pack_ = nullptr;  // [L][C][Dtot] LoRA-up rows in k_wkv's per-thread order
   const bf16_t* emb_ = nullptr;
   const bf16_t* head_ = nullptr;
   const float *ln0_w_ = nullptr, *ln0_b_ = nullptr, *lnout_w_ = nullptr, *lnout_b_ = nullptr;
@@ -109,6 +112,9 @@ class Engine {
   std::map<std::pair<int, int>, hipGraphExec_t> graphs_;
   std::vector<std::pair<std::string, hipEvent_t>> pending_prof_;
   std::vector<void*> allocs_;
+  uint64_t* dbg_stamps_ = nullptr;  // RWKVTTS_WKV_STAMPS=<file>: layer-5 WKV phase stamps
+  std::string dbg_stamp_path_;
+  int dbg_exp_ = 0;  // RWKVTTS_DEBUG_EXP: timing experiments (wrong numerics), never in production
   template <typename T>
   int alloc(T** p, size_t count);
 };

@@ -80,6 +80,12 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
   splitF_ = pick(F, 256);   // ffn value: 16 col tiles x 16
   splitH_ = pick(C, 512);   // head: 129 col tiles x 2
   RT_CHECK(C % 128 == 0 && F % 128 == 0, RWKVTTS_EUNSUPPORTED, "K dims must be multiples of 128");
+  RT_CHECK(splitA_ <= kMaxParts, RWKVTTS_EUNSUPPORTED, "n_embd too large for the WKV partial sum (raise kMaxParts)");
+  if (const char* ex = getenv("RWKVTTS_DEBUG_EXP")) dbg_exp_ = atoi(ex);
+  if (const char* sp = getenv("RWKVTTS_WKV_STAMPS")) {
+    dbg_stamp_path_ = sp;
+    RT_OK(alloc(&dbg_stamps_, 4096 * 8));
+  }
 
   // weights
   const size_t wbytes = (size_t)rwkvtts_blob_bytes(&dims);
@@ -109,6 +115,15 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
     w.w2t = Mv(RWKVTTS_L_W2T); w.a2t = Mv(RWKVTTS_L_A2T); w.v2t = Mv(RWKVTTS_L_V2T); w.g2t = Mv(RWKVTTS_L_G2T);
     w.ffn_k = Mv(RWKVTTS_L_FFN_K); w.ffn_v = Mv(RWKVTTS_L_FFN_V);
   }
+  RT_OK(alloc(&lora_pack_, (size_t)dims.n_layer * C * Dtot_));
+  for (int l = 0; l < dims.n_layer; ++l) {
+    LayerW& w = L_[l];
+    bf16_t* dst = lora_pack_ + (size_t)l * C * Dtot_;
+    launch_pack_lora(w.w2t, w.a2t, w.v2t, w.g2t, C, dims.d_decay, dims.d_aaa, dims.d_mv, dims.d_gate, dst, stream_);
+    RT_HIP(hipGetLastError());
+    w.lup = dst;
+  }
+  RT_HIP(hipStreamSynchronize(stream_));
   // state
   const int64_t Lc = dims.n_layer;
   RT_OK(alloc(&wkv_, (size_t)S_ * Lc * H_ * 64 * 64));
@@ -320,6 +335,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     // ---- WKV + LoRA-up + GroupNorm + bonus + gate
     WkvArgs k{};
     k.part = partA_; k.n_part = splitA_; k.ldp = ldA_; k.part_stride = (int64_t)Rmax_ * ldA_;
+    k.lup = w.lup;
     k.w2t = w.w2t; k.a2t = w.a2t; k.v2t = w.v2t; k.g2t = w.g2t;
     k.w0 = w.w0; k.a0 = w.a0; k.v0 = w.v0; k.k_k = w.k_k; k.k_a = w.k_a; k.r_k = w.r_k;
     k.lnx_w = w.lnx_w; k.lnx_b = w.lnx_b;
@@ -327,6 +343,8 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     k.v_first = vfirst_; k.ldv = C; k.z_hi = z_hi_; k.z_lo = z_lo_; k.ldz = C;
     k.segs = d_segs_; k.layer = l; k.C = C;
     k.Dw = dims.d_decay; k.Da = dims.d_aaa; k.Dv = dims.d_mv; k.Dg = dims.d_gate;
+    k.stamps = (l == 5) ? dbg_stamps_ : nullptr;
+    k.exp = dbg_exp_;
     prof_begin(&ev);
     launch_wkv(k, n_seg, H_, stream_);
     prof_end("wkv", ev);
@@ -521,7 +539,7 @@ int Engine::infer(const rwkvtts_input* in, int n, int head_rows, float* logits, 
   RT_HIP(hipStreamSynchronize(stream_));
   for (auto& om : out_map) has_logits[om.first] = 1;
   RT_OK(flush_prof());
-  return RWKVTTS_OK;
+  return dump_stamps();
 }
 
 // ------------------------------------------------------------------------------------------
@@ -783,6 +801,18 @@ int Engine::generate(const rwkvtts_request* reqs, int n, rwkvtts_result* res) {
   stats.decode_ms = decode_ms;
   stats.prefill_ms = prefill_ms;
   (void)t_start;
+  return dump_stamps();
+}
+
+int Engine::dump_stamps() {
+  if (!dbg_stamps_) return RWKVTTS_OK;
+  std::vector<uint64_t> hs(4096 * 8);  // debug: layer-5 WKV stamps of the last step -> file
+  RT_HIP(hipMemcpy(hs.data(), dbg_stamps_, hs.size() * 8, hipMemcpyDeviceToHost));
+  FILE* f = fopen(dbg_stamp_path_.c_str(), "wb");
+  if (f) {
+    fwrite(hs.data(), 8, hs.size(), f);
+    fclose(f);
+  }
   return RWKVTTS_OK;
 }
 

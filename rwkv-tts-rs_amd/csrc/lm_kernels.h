@@ -6,6 +6,7 @@ namespace rwkvtts {
 
 constexpr int kMaxPerThread = 8;     // C <= 2048 with 256-thread rows
 constexpr int kMaxLoraTotal = 512;   // Dw + Da + Dv + Dg
+constexpr int kMaxParts = 8;         // split-K slabs a WKV row sums (r, k, v, LoRA hidden)
 constexpr int kRowFirst = 1;         // row flags
 constexpr int kRowLast = 2;
 constexpr int kXPlanes = 0;  // gemm X: bf16 hi/lo planes
@@ -65,7 +66,8 @@ struct WkvArgs {
   int n_part;
   int ldp;
   int64_t part_stride;
-  const bf16_t *w2t, *a2t, *v2t, *g2t;
+  const bf16_t *w2t, *a2t, *v2t, *g2t;  // LoRA-up rows [C][D] (k_wkv1)
+  const bf16_t* lup;   // LoRA-up rows packed [C][4 quarters][(Dw+Da+Dv+Dg)/4] (launch_pack_lora)
   const float *w0, *a0, *v0, *k_k, *k_a, *r_k, *lnx_w, *lnx_b;
   float* state;
   int64_t slot_stride;
@@ -77,6 +79,8 @@ struct WkvArgs {
   int ldz;
   const int4* segs;    // slot, row_begin, n_rows, _
   int layer, C, Dw, Da, Dv, Dg;
+  uint64_t* stamps;    // debug: 8 s_memtime stamps per workgroup (null in production)
+  int exp;             // debug experiment bits (0 in production)
 };
 
 void launch_embed(const uint32_t* tokens, const bf16_t* emb, const float* w, const float* b,
@@ -84,5 +88,8 @@ void launch_embed(const uint32_t* tokens, const bf16_t* emb, const float* w, con
 void launch_ln_mix(const LnMixArgs& a, int n_out_rows, hipStream_t st);
 void launch_gemm(const GemmArgs& a, hipStream_t st);
 void launch_wkv(const WkvArgs& a, int n_seg, int H, hipStream_t st);
+// Repack one layer's w2t | a2t | v2t | g2t ([C][D] each) into the per-thread order of k_wkv.
+void launch_pack_lora(const bf16_t* w2t, const bf16_t* a2t, const bf16_t* v2t, const bf16_t* g2t, int C,
+                      int Dw, int Da, int Dv, int Dg, bf16_t* out, hipStream_t st);
 
 }  // namespace rwkvtts

@@ -13,6 +13,8 @@
 // precision with f32 accumulation; weights are read exactly once per step.
 #include "lm_kernels.h"
 
+#include <stdlib.h>
+
 namespace rwkvtts {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -366,126 +368,159 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
 __device__ inline float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
 
 
-__global__ __launch_bounds__(256) void k_wkv(WkvArgs a) {
+// MAXL: 8-byte LoRA-up weight units per thread (>= (Dw + Da + Dv + Dg) / 16);
+// MAXP: split-K slabs summed per row (>= n_part).
+template <int MAXL, int MAXP>
+__global__ __launch_bounds__(256, 2) void k_wkv(WkvArgs a) {
   constexpr int N = 64;
-  __shared__ float s_hid[kMaxLoraTotal];
+  __shared__ __attribute__((aligned(16))) float s_hid[kMaxLoraTotal];
   __shared__ float s_r[N], s_k[N], s_v[N], s_w[N], s_kk[N], s_b[N], s_g[N], s_y[N];
-  __shared__ float s_lora[4][N];
-  __shared__ __attribute__((aligned(16))) bf16_t s_lw[N * (kMaxLoraTotal + 8)];
+  __shared__ float s_red[2][4];
+  uint64_t* stp = (a.stamps && threadIdx.x == 0) ? a.stamps + (blockIdx.y * gridDim.x + blockIdx.x) * 8 : nullptr;
+#define WKV_STAMP(k) \
+  if (stp) stp[k] = __builtin_amdgcn_s_memtime();
+  WKV_STAMP(0)
+  // segs first: it heads the longest dependent chain (segs -> state / partials)
   const int4 sg = a.segs[blockIdx.x];
-  const int slot = sg.x, r_begin = sg.y, n_rows = sg.z;
   const int h = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int C = a.C;
   const int c = h * N + lane;  // this lane's channel (waves 0..3 all index the head's channels)
   const int i = tid >> 2, jq = (tid & 3) * 16;
+  // ---- LoRA-up weights, straight to registers: thread (cc = tid >> 2, pq = tid & 3) owns
+  // quarter pq of channel cc's rows of w2t | a2t | v2t | g2t (D/4 each), pre-packed into one
+  // contiguous run; these loads depend only on the head, so they are in flight with segs.
+  const int cc = tid >> 2, pq = tid & 3;
+  const int Dq0 = a.Dw / 4, Dq1 = a.Da / 4, Dq2 = a.Dv / 4, Dq3 = a.Dg / 4;
+  const int e1 = Dq0, e2 = Dq0 + Dq1, e3 = Dq0 + Dq1 + Dq2, eq = e3 + Dq3;  // quarter-vector bounds
+  uint2 lw[MAXL];
+  {
+    const bf16_t* src = a.lup + ((int64_t)(h * N + cc) * 4 + pq) * eq;  // one contiguous run
+#pragma unroll
+    for (int u = 0; u < MAXL; ++u) lw[u] = (u * 4 < eq) ? *(const uint2*)(src + u * 4) : make_uint2(0u, 0u);
+  }
+  // per-channel parameters: the 4 lanes of channel-owner group cc (all waves) hold channel
+  // h*N + cc; wave 0 lane l also holds channel h*N + l for the GroupNorm
+  const int co = h * N + cc;
+  const float w0 = a.w0[co], a0 = a.a0[co], v0 = a.v0[co], kkc = a.k_k[co], kac = a.k_a[co];
+  const float rkc = a.r_k[co];
+  float lnw = 0.f, lnb = 0.f;
+  if (wave == 0) {
+    lnw = a.lnx_w[c]; lnb = a.lnx_b[c];
+  }
+  // ---- segs-dependent loads: the slot's state tile and the first row's split-K partials
+  const int slot = sg.x, r_begin = sg.y, n_rows = sg.z;
   float* Sg = a.state + (int64_t)slot * a.slot_stride + a.layer_off + (int64_t)h * N * N + i * N + jq;
-  // ---- prologue: every load that does not depend on this step's activations
   float S[16];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const float4_ v4 = *(const float4_*)(Sg + q * 4);
+    const float4_ v4 = (a.exp & 4) ? (float4_){0.f, 0.f, 0.f, 0.f} : *(const float4_*)(Sg + q * 4);
     S[q * 4 + 0] = v4[0]; S[q * 4 + 1] = v4[1]; S[q * 4 + 2] = v4[2]; S[q * 4 + 3] = v4[3];
   }
-  // LoRA-up: 4 threads per channel (cc = tid >> 2, quarter pq = tid & 3 of each rank D)
-  const int cc = tid >> 2, pq = tid & 3;
-  const int Dv_eff = a.layer > 0 ? a.Dv : 0;
-  const int Dq[4] = {a.Dw / 4, a.Da / 4, Dv_eff / 4, a.Dg / 4};
-  // the head's LoRA-up rows (64 channels x Dtot bf16) staged once into LDS
-  const int Dall = a.Dw + a.Da + a.Dv + a.Dg, LDW = Dall + 8;
-  {
-    const int moff[4] = {0, a.Dw, a.Dw + a.Da, a.Dw + a.Da + a.Dv};
-    const int Dm[4] = {a.Dw, a.Da, a.Dv, a.Dg};
-    const bf16_t* Wb[4] = {a.w2t, a.a2t, a.v2t, a.g2t};
+  const int Dall = a.Dw + a.Da + a.Dv + a.Dg;
+  const int Dtot = Dall;
+  float hp0[MAXP], hp1[MAXP], rp[MAXP], kp[MAXP], vp[MAXP], vf = 0.f;
+  auto load_parts = [&](int row) {
+    const float* prow = a.part + (int64_t)row * a.ldp;
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const int ch8 = Dm[m] / 8;  // 16-byte chunks per row
-      for (int q = tid; q < N * ch8; q += 256) {
-        const int ch = q / ch8, k8 = (q % ch8) * 8;
-        *(short8*)(s_lw + ch * LDW + moff[m] + k8) = *(const short8*)(Wb[m] + (int64_t)(h * N + ch) * Dm[m] + k8);
-      }
+    for (int p = 0; p < MAXP; ++p) {
+      const float* pp = prow + p * a.part_stride;
+      const bool on = p < a.n_part && !(a.exp & 2);
+      hp0[p] = (on && tid < Dtot) ? pp[3 * C + tid] : 0.f;
+      hp1[p] = (on && tid + 256 < Dtot) ? pp[3 * C + tid + 256] : 0.f;
+      rp[p] = on ? pp[co] : 0.f;
+      kp[p] = on ? pp[C + co] : 0.f;
+      vp[p] = on ? pp[2 * C + co] : 0.f;
     }
-  }
-  float w0 = 0.f, a0 = 0.f, v0 = 0.f, kkc = 0.f, kac = 0.f, rkc = 0.f, lnw = 0.f, lnb = 0.f;
-  if (wave == 0) {
-    w0 = a.w0[c]; a0 = a.a0[c]; v0 = a.v0[c]; kkc = a.k_k[c]; kac = a.k_a[c];
-    rkc = a.r_k[c]; lnw = a.lnx_w[c]; lnb = a.lnx_b[c];
-  }
-  const int Dtot = a.Dw + a.Da + a.Dv + a.Dg;
+    vf = a.layer > 0 ? a.v_first[(int64_t)row * a.ldv + co] : 0.f;
+  };
+  load_parts(r_begin);
+  const int hb1 = a.Dw, hb2 = a.Dw + a.Da, hb3 = a.Dw + a.Da + a.Dv;  // s_hid bases per matrix
   for (int rr = 0; rr < n_rows; ++rr) {
     const int row = r_begin + rr;
-    const float* prow = a.part + (int64_t)row * a.ldp;
-    // ---- this row's activations: LoRA hidden (all), r/k/v (wave 0), v_first
-    float hx0 = 0.f, hx1 = 0.f;
-    for (int p = 0; p < a.n_part; ++p) {
-      if (tid < Dtot) hx0 += prow[p * a.part_stride + 3 * C + tid];
-      if (tid + 256 < Dtot) hx1 += prow[p * a.part_stride + 3 * C + tid + 256];
+    if (rr == 1) { WKV_STAMP(6) }
+    if (rr == 2) { WKV_STAMP(7) }
+    if (rr > 0) load_parts(row);
+    float hx0 = 0.f, hx1 = 0.f, r = 0.f, k = 0.f, v = 0.f;
+#pragma unroll
+    for (int p = 0; p < MAXP; ++p) {
+      hx0 += hp0[p];
+      hx1 += hp1[p];
+      r += rp[p];
+      k += kp[p];
+      v += vp[p];
     }
-    float r = 0.f, k = 0.f, v = 0.f, vf = 0.f;
-    if (wave == 0) {
-      for (int p = 0; p < a.n_part; ++p) {
-        const float* pp = prow + p * a.part_stride;
-        r += pp[c];
-        k += pp[C + c];
-        v += pp[2 * C + c];
+    // LoRA hidden activations, stored quarter-major: quarter pq of every matrix is one
+    // contiguous run s_hq[pq * eq + (w | a | v | g offset) + i], read with uniform stride below
+    auto put_hid = [&](int d, float x) {
+      int dl, dq, eb;
+      float y;
+      if (d < hb1) { dl = d; dq = Dq0; eb = 0; y = tanhf(x); }
+      else if (d < hb2) { dl = d - hb1; dq = Dq1; eb = e1; y = x; }
+      else if (d < hb3) { dl = d - hb2; dq = Dq2; eb = e2; y = x; }
+      else { dl = d - hb3; dq = Dq3; eb = e3; y = sigm(x); }
+      if (dq > 0) {
+        const int qt = dl / dq;
+        s_hid[qt * eq + eb + (dl - qt * dq)] = y;
       }
-      if (a.layer > 0) vf = a.v_first[(int64_t)row * a.ldv + c];
-    }
-    auto act = [&](int d, float x) {
-      if (d < a.Dw) return tanhf(x);
-      if (d >= a.Dw + a.Da + a.Dv) return sigm(x);
-      return x;
     };
-    if (tid < Dtot) s_hid[tid] = act(tid, hx0);
-    if (tid + 256 < Dtot) s_hid[tid + 256] = act(tid + 256, hx1);
+    if (tid < Dtot) put_hid(tid, hx0);
+    if (tid + 256 < Dtot) put_hid(tid + 256, hx1);
     __syncthreads();
-    // ---- LoRA up for this head's channels from the prefetched rows
+    if (rr == 0) { WKV_STAMP(1) }
+    // ---- LoRA up (branch-free, every LDS read independent) + this channel's mixing terms
+    float lo0 = 0.f, lo1 = 0.f, lo2 = 0.f, lo3 = 0.f;
     {
-      const int hoffs[4] = {0, a.Dw, a.Dw + a.Da, a.Dw + a.Da + a.Dv};
-      float accm[4];
+      const float* hq = s_hid + pq * eq;
 #pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        float acc = 0.f;
-        const bf16_t* wr = s_lw + cc * LDW + hoffs[m] + pq * Dq[m];
-        const float* hh = s_hid + hoffs[m] + pq * Dq[m];
-        for (int d = 0; d < Dq[m]; d += 4) {
-          const uint2 q = *(const uint2*)(wr + d);
-          acc += bf16_to_f32((uint16_t)(q.x & 0xFFFF)) * hh[d + 0];
-          acc += bf16_to_f32((uint16_t)(q.x >> 16)) * hh[d + 1];
-          acc += bf16_to_f32((uint16_t)(q.y & 0xFFFF)) * hh[d + 2];
-          acc += bf16_to_f32((uint16_t)(q.y >> 16)) * hh[d + 3];
+      for (int u = 0; u < MAXL; ++u) {
+        const int e = u * 4;
+        if (e < eq) {  // uniform
+          const float4_ hv = *(const float4_*)(hq + e);
+          const uint2 q = lw[u];
+          const float d = bf16_to_f32((uint16_t)(q.x & 0xFFFF)) * hv[0] + bf16_to_f32((uint16_t)(q.x >> 16)) * hv[1] +
+                          bf16_to_f32((uint16_t)(q.y & 0xFFFF)) * hv[2] + bf16_to_f32((uint16_t)(q.y >> 16)) * hv[3];
+          lo0 += e < e1 ? d : 0.f;
+          lo1 += (e >= e1 && e < e2) ? d : 0.f;
+          lo2 += (e >= e2 && e < e3) ? d : 0.f;
+          lo3 += e >= e3 ? d : 0.f;
         }
-        acc += __shfl_xor(acc, 1);
-        acc += __shfl_xor(acc, 2);
-        accm[m] = acc;
       }
-      if (pq == 0) {
-#pragma unroll
-        for (int m = 0; m < 4; ++m) s_lora[m][cc] = accm[m];
-      }
+      lo0 += __shfl_xor(lo0, 1); lo0 += __shfl_xor(lo0, 2);
+      lo1 += __shfl_xor(lo1, 1); lo1 += __shfl_xor(lo1, 2);
+      lo2 += __shfl_xor(lo2, 1); lo2 += __shfl_xor(lo2, 2);
+      lo3 += __shfl_xor(lo3, 1); lo3 += __shfl_xor(lo3, 2);
     }
-    __syncthreads();
-    if (wave == 0) {
-      const float w = expf(-0.60653066f * sigm(w0 + s_lora[0][lane]));
-      const float av = sigm(a0 + s_lora[1][lane]);
-      float kk = k * kkc;
-      const float nrm = sqrtf(wave_sum(kk * kk));
-      kk = kk / fmaxf(nrm, 1e-12f);
-      k = k * (1.0f + (av - 1.0f) * kac);
+    {
+      const float w = expf(-0.60653066f * sigm(w0 + lo0));
+      const float av = sigm(a0 + lo1);
+      const float kk = k * kkc;
+      const float kn = k * (1.0f + (av - 1.0f) * kac);
+      float vn = v;
       if (a.layer == 0) {
-        a.v_first[(int64_t)row * a.ldv + c] = v;
+        if (pq == 0) a.v_first[(int64_t)row * a.ldv + co] = v;
       } else {
-        const float gate = sigm(v0 + s_lora[2][lane]);
-        v = v + (vf - v) * gate;
+        vn = v + (vf - v) * sigm(v0 + lo2);
       }
-      s_r[lane] = r; s_k[lane] = k; s_v[lane] = v; s_w[lane] = w;
-      s_kk[lane] = kk; s_b[lane] = kk * av; s_g[lane] = s_lora[3][lane];
+      // per-wave partial sums over its 16 channels: |kk|^2 and the bonus sum r*k*r_k
+      const float ksq = wave_sum(pq == 0 ? kk * kk : 0.f);
+      const float bon = wave_sum(pq == 0 ? r * kn * rkc : 0.f);
+      if (lane == 0) { s_red[0][wave] = ksq; s_red[1][wave] = bon; }
+      if (pq == 0) {
+        s_r[cc] = r; s_k[cc] = kn; s_v[cc] = vn; s_w[cc] = w; s_kk[cc] = kk; s_b[cc] = av; s_g[cc] = lo3;
+      }
     }
     __syncthreads();
+    if (rr == 0) { WKV_STAMP(2) }
+    const float nrm = fmaxf(sqrtf(((s_red[0][0] + s_red[0][1]) + s_red[0][2]) + s_red[0][3]), 1e-12f);
+    if (rr == 0) { WKV_STAMP(3) }
     // ---- state update: S[i][j] = S[i][j]*w_j - sa_i*b_j + v_i*k_j ; y_i = sum_j S[i][j] r_j
+    float kkn[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) kkn[q] = s_kk[jq + q] / nrm;
     float sa = 0.f;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) sa += S[q] * s_kk[jq + q];
+    for (int q = 0; q < 16; ++q) sa += S[q] * kkn[q];
     sa += __shfl_xor(sa, 1);
     sa += __shfl_xor(sa, 2);
     const float vi = s_v[i];
@@ -493,23 +528,25 @@ __global__ __launch_bounds__(256) void k_wkv(WkvArgs a) {
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int jj = jq + q;
-      S[q] = S[q] * s_w[jj] - sa * s_b[jj] + vi * s_k[jj];
+      S[q] = S[q] * s_w[jj] - sa * (kkn[q] * s_b[jj]) + vi * s_k[jj];
       y += S[q] * s_r[jj];
     }
     y += __shfl_xor(y, 1);
     y += __shfl_xor(y, 2);
     if ((tid & 3) == 0) s_y[i] = y;
     __syncthreads();
+    if (rr == 0) { WKV_STAMP(4) }
     if (wave == 0) {
       const float yv = s_y[lane];
       const float mean = wave_sum(yv) * (1.0f / N);
       const float dv = yv - mean;
       const float var = wave_sum(dv * dv) * (1.0f / N);
       const float rstd = 1.0f / sqrtf(var + 64e-5f);
-      const float bonus = wave_sum(s_r[lane] * s_k[lane] * rkc);
+      const float bonus = ((s_red[1][0] + s_red[1][1]) + s_red[1][2]) + s_red[1][3];
       const float gn = dv * rstd * lnw + lnb;
       split_store((gn + bonus * s_v[lane]) * s_g[lane], a.z_hi, a.z_lo, (int64_t)row * a.ldz + c);
     }
+    if (rr == 0) { WKV_STAMP(5) }
     if (rr + 1 < n_rows) __syncthreads();
   }
 #pragma unroll
@@ -517,6 +554,8 @@ __global__ __launch_bounds__(256) void k_wkv(WkvArgs a) {
     float4_ v4 = {S[q * 4 + 0], S[q * 4 + 1], S[q * 4 + 2], S[q * 4 + 3]};
     *(float4_*)(Sg + q * 4) = v4;
   }
+  if (n_rows == 1) { WKV_STAMP(6) }
+#undef WKV_STAMP
 }
 
 // ------------------------------------------------------------------------------------
@@ -562,8 +601,218 @@ void launch_gemm(const GemmArgs& a, hipStream_t st) {
   }
 #undef GEMM_CASE
 }
+__global__ void k_pack_lora(const bf16_t* w2t, const bf16_t* a2t, const bf16_t* v2t, const bf16_t* g2t, int C,
+                            int Dw, int Da, int Dv, int Dg, bf16_t* out) {
+  const int Dall = Dw + Da + Dv + Dg, eq = Dall / 4;
+  const int e1 = Dw / 4, e2 = e1 + Da / 4, e3 = e2 + Dv / 4;
+  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < (int64_t)C * Dall;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int co = (int)(idx / Dall), r = (int)(idx % Dall), pq = r / eq, e = r % eq;
+    bf16_t v;
+    if (e < e1) v = w2t[(int64_t)co * Dw + pq * (Dw / 4) + e];
+    else if (e < e2) v = a2t[(int64_t)co * Da + pq * (Da / 4) + (e - e1)];
+    else if (e < e3) v = v2t[(int64_t)co * Dv + pq * (Dv / 4) + (e - e2)];
+    else v = g2t[(int64_t)co * Dg + pq * (Dg / 4) + (e - e3)];
+    out[idx] = v;
+  }
+}
+
+void launch_pack_lora(const bf16_t* w2t, const bf16_t* a2t, const bf16_t* v2t, const bf16_t* g2t, int C,
+                      int Dw, int Da, int Dv, int Dg, bf16_t* out, hipStream_t st) {
+  hipLaunchKernelGGL(k_pack_lora, dim3(1024), dim3(256), 0, st, w2t, a2t, v2t, g2t, C, Dw, Da, Dv, Dg, out);
+}
+
+// ------------------------------------------------------------------------------------
+// wkv, two waves per (slot segment, head): thread t = (row i = t >> 1, half hf = t & 1) owns
+// state row S[i][32 hf .. 32 hf + 31] (32 VGPRs) and half of channel c = h*64 + i's LoRA-up
+// dot products (halves combined by one shuffle), so reductions over j are in-lane plus one
+// pair shuffle; per-channel vectors (w, kk, a, k, r) and the LoRA hidden go through LDS as
+// broadcasts; cross-wave sums (|kk|^2, bonus, GroupNorm moments) take one barrier each.
+// Loads that need only the head (LoRA-up rows, parameters) are issued before the segment
+// descriptor arrives.
+// ------------------------------------------------------------------------------------
+template <int DW, int DA, int DV, int DG, int MAXP>
+__global__ __launch_bounds__(128) void k_wkv2(WkvArgs a) {
+  constexpr int N = 64, DALL = DW + DA + DV + DG;
+  __shared__ __attribute__((aligned(16))) float s_hid[DALL];
+  __shared__ __attribute__((aligned(16))) float s_vec[5][N];  // w, kk (unnormalised), a, k, r
+  __shared__ float s_red[4][2];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, i = t >> 1, hf = t & 1;
+  const int h = blockIdx.y, C = a.C, c = h * N + i;
+  const int4 sg = a.segs[blockIdx.x];
+  // ---- head-only loads: half of channel c's LoRA-up rows (bf16) and its parameters
+  constexpr int UW = DW / 16, UA = DA / 16, UV = DV / 16, UG = DG / 16, UL = UW + UA + UV + UG;
+  short8 lw[UL];
+#pragma unroll
+  for (int u = 0; u < UW; ++u) lw[u] = *(const short8*)(a.w2t + (int64_t)c * DW + hf * (DW / 2) + u * 8);
+#pragma unroll
+  for (int u = 0; u < UA; ++u) lw[UW + u] = *(const short8*)(a.a2t + (int64_t)c * DA + hf * (DA / 2) + u * 8);
+#pragma unroll
+  for (int u = 0; u < UV; ++u) lw[UW + UA + u] = *(const short8*)(a.v2t + (int64_t)c * DV + hf * (DV / 2) + u * 8);
+#pragma unroll
+  for (int u = 0; u < UG; ++u)
+    lw[UW + UA + UV + u] = *(const short8*)(a.g2t + (int64_t)c * DG + hf * (DG / 2) + u * 8);
+  const float w0 = a.w0[c], a0 = a.a0[c], v0 = a.v0[c], kkc = a.k_k[c], kac = a.k_a[c];
+  const float rkc = a.r_k[c], lnw = a.lnx_w[c], lnb = a.lnx_b[c];
+  // ---- segment-dependent loads: the half state row and the first row's split-K partials
+  const int slot = sg.x, r_begin = sg.y, n_rows = sg.z;
+  float* Srow = a.state + (int64_t)slot * a.slot_stride + a.layer_off + (int64_t)h * N * N + i * N + hf * 32;
+  float S[32];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const float4_ v4 = *(const float4_*)(Srow + q * 4);
+    S[q * 4 + 0] = v4[0]; S[q * 4 + 1] = v4[1]; S[q * 4 + 2] = v4[2]; S[q * 4 + 3] = v4[3];
+  }
+  constexpr int HPL = (DALL + 127) / 128;  // hidden elements per thread
+  float hp[MAXP][HPL], rp[MAXP], kp[MAXP], vp[MAXP], vf = 0.f;
+  auto load_parts = [&](int row) {
+    const float* prow = a.part + (int64_t)row * a.ldp;
+#pragma unroll
+    for (int p = 0; p < MAXP; ++p) {
+      const bool on = p < a.n_part;
+      const float* pp = prow + p * a.part_stride;
+#pragma unroll
+      for (int e = 0; e < HPL; ++e) {
+        const int d = t + 128 * e;
+        hp[p][e] = (on && d < DALL) ? pp[3 * C + d] : 0.f;
+      }
+      rp[p] = on ? pp[c] : 0.f;
+      kp[p] = on ? pp[C + c] : 0.f;
+      vp[p] = on ? pp[2 * C + c] : 0.f;
+    }
+    vf = a.layer > 0 ? a.v_first[(int64_t)row * a.ldv + c] : 0.f;
+  };
+  load_parts(r_begin);
+  for (int rr = 0; rr < n_rows; ++rr) {
+    const int row = r_begin + rr;
+    if (rr > 0) load_parts(row);
+#pragma unroll
+    for (int e = 0; e < HPL; ++e) {
+      float x = 0.f;
+#pragma unroll
+      for (int p = 0; p < MAXP; ++p) x += hp[p][e];
+      const int d = t + 128 * e;
+      if (d < DALL) s_hid[d] = d < DW ? tanhf(x) : (d >= DW + DA + DV ? sigm(x) : x);
+    }
+    float r = 0.f, k = 0.f, v = 0.f;
+#pragma unroll
+    for (int p = 0; p < MAXP; ++p) {
+      r += rp[p];
+      k += kp[p];
+      v += vp[p];
+    }
+    __syncthreads();
+    // ---- LoRA up: this thread's half of channel c's four dot products, pair-combined
+    float lo0 = 0.f, lo1 = 0.f, lo2 = 0.f, lo3 = 0.f;
+    auto dot8 = [&](const short8 q, const float* hsrc) {
+      const float4_ h0 = *(const float4_*)hsrc;
+      const float4_ h1 = *(const float4_*)(hsrc + 4);
+      float acc = 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc += bf16_to_f32((uint16_t)q[e]) * h0[e];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc += bf16_to_f32((uint16_t)q[4 + e]) * h1[e];
+      return acc;
+    };
+#pragma unroll
+    for (int u = 0; u < UW; ++u) lo0 += dot8(lw[u], s_hid + hf * (DW / 2) + u * 8);
+#pragma unroll
+    for (int u = 0; u < UA; ++u) lo1 += dot8(lw[UW + u], s_hid + DW + hf * (DA / 2) + u * 8);
+#pragma unroll
+    for (int u = 0; u < UV; ++u) lo2 += dot8(lw[UW + UA + u], s_hid + DW + DA + hf * (DV / 2) + u * 8);
+#pragma unroll
+    for (int u = 0; u < UG; ++u) lo3 += dot8(lw[UW + UA + UV + u], s_hid + DW + DA + DV + hf * (DG / 2) + u * 8);
+    lo0 += __shfl_xor(lo0, 1);
+    lo1 += __shfl_xor(lo1, 1);
+    lo2 += __shfl_xor(lo2, 1);
+    lo3 += __shfl_xor(lo3, 1);
+    // ---- channel mixing terms (both threads of the pair compute channel c)
+    const float w = expf(-0.60653066f * sigm(w0 + lo0));
+    const float av = sigm(a0 + lo1);
+    const float kk = k * kkc;
+    k = k * (1.0f + (av - 1.0f) * kac);
+    if (a.layer == 0) {
+      if (hf == 0) a.v_first[(int64_t)row * a.ldv + c] = v;
+    } else {
+      v = v + (vf - v) * sigm(v0 + lo2);
+    }
+    {
+      const float ksq = wave_sum(hf == 0 ? kk * kk : 0.f);
+      const float bon = wave_sum(hf == 0 ? r * k * rkc : 0.f);
+      if (lane == 0) { s_red[0][wave] = ksq; s_red[1][wave] = bon; }
+    }
+    if (hf == 0) {
+      s_vec[0][i] = w; s_vec[1][i] = kk; s_vec[2][i] = av; s_vec[3][i] = k; s_vec[4][i] = r;
+    }
+    __syncthreads();
+    const float inv = 1.0f / fmaxf(sqrtf(s_red[0][0] + s_red[0][1]), 1e-12f);
+    const float bonus = s_red[1][0] + s_red[1][1];
+    // ---- state half-row update: S[i][j] = S[i][j]*w_j - sa_i*kk_j*a_j + v_i*k_j ; y_i = S[i].r
+    const float* vj = &s_vec[0][hf * 32];
+    float sa = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float4_ kq = *(const float4_*)(vj + N + q * 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) sa += S[q * 4 + e] * (kq[e] * inv);
+    }
+    sa += __shfl_xor(sa, 1);
+    float y = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float4_ wq = *(const float4_*)(vj + q * 4);
+      const float4_ kq = *(const float4_*)(vj + N + q * 4);
+      const float4_ aq = *(const float4_*)(vj + 2 * N + q * 4);
+      const float4_ k4 = *(const float4_*)(vj + 3 * N + q * 4);
+      const float4_ rq = *(const float4_*)(vj + 4 * N + q * 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float& sv = S[q * 4 + e];
+        sv = sv * wq[e] - sa * ((kq[e] * inv) * aq[e]) + v * k4[e];
+        y += sv * rq[e];
+      }
+    }
+    y += __shfl_xor(y, 1);
+    // ---- GroupNorm over the head's 64 rows (eps 64e-5): one-barrier moments
+    {
+      const float s1 = wave_sum(hf == 0 ? y : 0.f);
+      const float s2 = wave_sum(hf == 0 ? y * y : 0.f);
+      if (lane == 0) { s_red[2][wave] = s1; s_red[3][wave] = s2; }
+    }
+    __syncthreads();
+    const float mean = (s_red[2][0] + s_red[2][1]) * (1.0f / N);
+    const float var = fmaxf((s_red[3][0] + s_red[3][1]) * (1.0f / N) - mean * mean, 0.f);
+    if (hf == 0) {
+      const float gn = (y - mean) * (1.0f / sqrtf(var + 64e-5f)) * lnw + lnb;
+      split_store((gn + bonus * v) * lo3, a.z_hi, a.z_lo, (int64_t)row * a.ldz + c);
+    }
+    if (rr + 1 < n_rows) __syncthreads();
+  }
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    float4_ v4 = {S[q * 4 + 0], S[q * 4 + 1], S[q * 4 + 2], S[q * 4 + 3]};
+    *(float4_*)(Srow + q * 4) = v4;
+  }
+}
+
 void launch_wkv(const WkvArgs& a, int n_seg, int H, hipStream_t st) {
-  hipLaunchKernelGGL(k_wkv, dim3(n_seg, H), dim3(256), 0, st, a);
+  const dim3 grid(n_seg, H);
+  if (a.Dw == 64 && a.Da == 64 && a.Dv == 32 && a.Dg == 128 && a.n_part <= 4 && !getenv("RWKVTTS_WKV_OLD")) {
+    hipLaunchKernelGGL((k_wkv2<64, 64, 32, 128, 4>), grid, dim3(128), 0, st, a);
+    return;
+  }
+  if (a.Dw == 16 && a.Da == 16 && a.Dv == 16 && a.Dg == 32 && a.n_part <= 1 && !getenv("RWKVTTS_WKV_OLD")) {
+    hipLaunchKernelGGL((k_wkv2<16, 16, 16, 32, 1>), grid, dim3(128), 0, st, a);
+    return;
+  }
+  if (a.Dw == 32 && a.Da == 32 && a.Dv == 16 && a.Dg == 64 && a.n_part <= 1 && !getenv("RWKVTTS_WKV_OLD")) {
+    hipLaunchKernelGGL((k_wkv2<32, 32, 16, 64, 1>), grid, dim3(128), 0, st, a);
+    return;
+  }
+  const int units = (a.Dw + a.Da + a.Dv + a.Dg + 15) / 16;
+  if (units <= 8 && a.n_part <= 4) hipLaunchKernelGGL((k_wkv<8, 4>), grid, dim3(256), 0, st, a);
+  else if (units <= 20 && a.n_part <= 4) hipLaunchKernelGGL((k_wkv<20, 4>), grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((k_wkv<32, 8>), grid, dim3(256), 0, st, a);
 }
 
 }  // namespace rwkvtts
