@@ -82,6 +82,10 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
   RT_CHECK(C % 128 == 0 && F % 128 == 0, RWKVTTS_EUNSUPPORTED, "K dims must be multiples of 128");
   RT_CHECK(splitA_ <= kMaxParts, RWKVTTS_EUNSUPPORTED, "n_embd too large for the WKV partial sum (raise kMaxParts)");
   if (const char* ex = getenv("RWKVTTS_DEBUG_EXP")) dbg_exp_ = atoi(ex);
+  if (const char* gp = getenv("RWKVTTS_GEMM_STAMPS")) {
+    dbg_gstamp_path_ = gp;
+    RT_OK(alloc(&dbg_gstamps_, 2 * 4096 * 4));
+  }
   if (const char* sp = getenv("RWKVTTS_WKV_STAMPS")) {
     dbg_stamp_path_ = sp;
     RT_OK(alloc(&dbg_stamps_, 4096 * 8));
@@ -330,6 +334,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     g.K = C; g.M = R; g.k_split = splitA_; g.kslice = C / splitA_;
     g.xmode = kXPlanes; g.out = partA_; g.split_stride = (int64_t)Rmax_ * ldA_; g.ldo = ldA_;
     prof_begin(&ev);
+    g.stamps = (l == 5 && dbg_gstamps_) ? dbg_gstamps_ : nullptr;
     launch_gemm(g, stream_);
     prof_end("gemm_rkv_lora", ev);
     // ---- WKV + LoRA-up + GroupNorm + bonus + gate
@@ -389,6 +394,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     gv.x_part_stride = (int64_t)Rmax_ * F;
     gv.out = partF_; gv.split_stride = RC; gv.ldo = C;
     prof_begin(&ev);
+    gv.stamps = (l == 5 && dbg_gstamps_) ? dbg_gstamps_ + 4096 * 4 : nullptr;
     launch_gemm(gv, stream_);
     prof_end("gemm_ffn_value", ev);
   }
@@ -805,6 +811,15 @@ int Engine::generate(const rwkvtts_request* reqs, int n, rwkvtts_result* res) {
 }
 
 int Engine::dump_stamps() {
+  if (dbg_gstamps_) {
+    std::vector<uint64_t> hg(2 * 4096 * 4);
+    RT_HIP(hipMemcpy(hg.data(), dbg_gstamps_, hg.size() * 8, hipMemcpyDeviceToHost));
+    FILE* f = fopen(dbg_gstamp_path_.c_str(), "wb");
+    if (f) {
+      fwrite(hg.data(), 8, hg.size(), f);
+      fclose(f);
+    }
+  }
   if (!dbg_stamps_) return RWKVTTS_OK;
   std::vector<uint64_t> hs(4096 * 8);  // debug: layer-5 WKV stamps of the last step -> file
   RT_HIP(hipMemcpy(hs.data(), dbg_stamps_, hs.size() * 8, hipMemcpyDeviceToHost));

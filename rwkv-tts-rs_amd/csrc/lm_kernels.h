@@ -59,6 +59,7 @@ struct GemmArgs {
   float* out;          // [k_split][rows][ldo] f32
   int64_t split_stride;
   int ldo;
+  uint64_t* stamps;    // debug: 4 s_memtime stamps per workgroup (null in production)
 };
 
 struct WkvArgs {

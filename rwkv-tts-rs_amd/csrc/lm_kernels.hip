@@ -249,6 +249,9 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
   constexpr int ROWS = MT * 16;
   bf16_t* xh = (bf16_t*)smem;
   bf16_t* xl = xh + ROWS * LD;
+  uint64_t* gst = (a.stamps && threadIdx.x == 0)
+                      ? a.stamps + ((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * 4 : nullptr;
+  if (gst) gst[0] = __builtin_amdgcn_s_memtime();
   const int tile = blockIdx.x;
   int s = 0;
   while (s + 1 < a.nseg && tile >= a.seg[s + 1].tile_start) ++s;
@@ -329,6 +332,7 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
     }
   }
   __syncthreads();
+  if (gst) gst[1] = __builtin_amdgcn_s_memtime();
   // 3) MFMA over the slice
   float4_ acc[MT];
 #pragma unroll
@@ -346,6 +350,7 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
                                                        __builtin_bit_cast(bf16x8, b[t]), acc[m], 0, 0, 0);
     }
   }
+  if (gst) gst[2] = __builtin_amdgcn_s_memtime() + (uint64_t)(acc[0][0] != acc[0][0]);
   // 4) store (D layout: col = lane&15, row = 4*(lane>>4) + j)
   const int col = col0 + li;
   if (col < sg.N) {
@@ -357,6 +362,7 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
         if (row < a.M) a.out[split * a.split_stride + (int64_t)row * a.ldo + sg.col_off + col] = acc[m][j];
       }
   }
+  if (gst) gst[3] = __builtin_amdgcn_s_memtime();
 }
 
 // ------------------------------------------------------------------------------------

@@ -82,6 +82,105 @@ __device__ inline float wave_serial_add(float s, const float* p, int b, int e) {
   for (int q = b; q < e; q += 64) s = add64(s, (q + lane < e) ? p[q + lane] : 0.0f);
   return s;
 }
+// Quantised increment of adding e (bits b) to an f32 s in binade E (ulp u = 2^(E-23); the
+// denormal range counts as E = -126): RN(s + e) = s + u * (a + [frac(e/u) > 1/2]) while the
+// result stays in the binade. Flags a tie (frac == 1/2: the result then depends on the parity of
+// s) and an increment too large for the binade.
+__device__ inline uint32_t qinc(uint32_t b, int E, bool& flag) {
+  const uint32_t ef = (b >> 23) & 0xFFu;
+  uint32_t M = b & 0x7FFFFFu;
+  int ex;
+  if (ef == 0) ex = -149;
+  else { M |= 0x800000u; ex = (int)ef - 150; }
+  if (M == 0) return 0u;
+  const int sh = (E - 23) - ex;  // e / u = M * 2^-sh
+  if (sh <= 0) {
+    if (sh < -7) { flag = true; return 0u; }
+    const uint32_t a = M << (-sh);
+    if (a >= 0x1000000u) flag = true;
+    return a;
+  }
+  if (sh > 25) return 0u;  // e < u / 4
+  const uint32_t a = M >> sh, r = M & ((1u << sh) - 1u), half = 1u << (sh - 1);
+  if (r == half) flag = true;
+  return a + (r > half ? 1u : 0u);
+}
+// u * mm for mm < 2^24 in binade E (E = -126: denormal or the lowest normal binade, bits = mm)
+__device__ inline float binade_value(uint32_t mm, int E) {
+  return __builtin_bit_cast(float, E == -126 ? mm : (((uint32_t)(E + 127) << 23) | (mm & 0x7FFFFFu)));
+}
+// Exact sequential f32 sum s + p[b] + ... + p[e-1] (p >= 0) by one wave, 128 elements per
+// round: every element's increment is quantised for s's binade and prefix-summed across the
+// wave; the first element that would leave the binade, tie or overflow the binade is added
+// with a real f32 add, and the round restarts after it. Bit-identical to the serial loop.
+__device__ float wave_exact_add(float s, const float* p, int b, int e) {
+  const int lane = threadIdx.x & 63;
+  int pos = b;
+  while (pos < e) {
+    const uint32_t sb = __builtin_bit_cast(uint32_t, s);
+    const int ef = (int)((sb >> 23) & 0xFFu);
+    const int E = ef ? ef - 127 : -126;
+    const uint32_t m = ef ? ((sb & 0x7FFFFFu) | 0x800000u) : (sb & 0x7FFFFFu);
+    const int i0 = pos + 2 * lane, i1 = i0 + 1;
+    bool f0 = false, f1 = false;
+    const uint32_t q0 = i0 < e ? qinc(__builtin_bit_cast(uint32_t, p[i0]), E, f0) : 0u;
+    const uint32_t q1 = i1 < e ? qinc(__builtin_bit_cast(uint32_t, p[i1]), E, f1) : 0u;
+    const uint32_t lt = q0 + q1;
+    uint32_t incl = lt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t v = __shfl_up(incl, o);
+      if (lane >= o) incl = min(incl + v, 0x4000000u);
+    }
+    uint32_t excl = __shfl_up(incl, 1);
+    if (lane == 0) excl = 0u;
+    const bool c0 = f0 || (i0 < e && m + excl + q0 >= 0x1000000u);
+    const bool c1 = f1 || (i1 < e && m + excl + q0 + q1 >= 0x1000000u);
+    const uint64_t bal = __ballot(c0 || c1);
+    if (bal == 0) {
+      s = binade_value(m + (uint32_t)readlane_i((int)incl, 63), E);
+      pos += 128;
+      continue;
+    }
+    const int fl = __ffsll((long long)bal) - 1;
+    const bool c0l = readlane_i(c0 ? 1 : 0, fl) != 0;
+    const uint32_t exl = (uint32_t)readlane_i((int)excl, fl);
+    const uint32_t pre = c0l ? exl : exl + (uint32_t)readlane_i((int)q0, fl);
+    const int f = pos + 2 * fl + (c0l ? 0 : 1);
+    s = binade_value(m + pre, E);
+    s = s + p[f];
+    pos = f + 1;
+  }
+  return s;
+}
+// Sequential f32 sum s + p[b] + ... + p[e-1] by ONE lane from its own registers: each 128-
+// element piece is pulled in with 32 back-to-back 16-byte LDS reads, then added in order -- one
+// dependent v_add per element, no cross-lane traffic. b must be a multiple of 4.
+__device__ inline float add128(float s, const float* p) {
+  float4_ v[32];
+#pragma unroll
+  for (int q = 0; q < 32; ++q) v[q] = *(const float4_*)(p + 4 * q);
+#pragma unroll
+  for (int q = 0; q < 32; ++q) {
+    s += v[q][0];
+    s += v[q][1];
+    s += v[q][2];
+    s += v[q][3];
+  }
+  return s;
+}
+__device__ inline float lane_serial_add(float s, const float* p, int b, int e) {
+  for (; b + 128 <= e; b += 128) s = add128(s, p + b);
+  for (; b + 4 <= e; b += 4) {
+    const float4_ v = *(const float4_*)(p + b);
+    s += v[0];
+    s += v[1];
+    s += v[2];
+    s += v[3];
+  }
+  for (; b < e; ++b) s += p[b];
+  return s;
+}
 // In-order prefix sums of one 64-block: lane i receives s + v[0] + ... + v[i] (sequential).
 __device__ inline float prefix64(float s, float v, float* total) {
   float out = 0.0f;
@@ -227,7 +326,7 @@ __device__ inline void sum_sim_elem(uint32_t b, int E, uint32_t& T0, uint32_t& T
 
 __device__ float exact_seq_sum(const SampleSmem& sm, int n, uint64_t* stamps = nullptr) {
   const int tid = threadIdx.x;
-  const int CH = (n + 63) / 64, SUB = (CH + 3) / 4;
+  const int CH = (((n + 63) / 64) + 3) & ~3, SUB = (CH + 3) / 4;  // chunks start 16-byte aligned
   const int chunk = tid >> 2, sub = tid & 3;
   const int cb = min(n, chunk * CH), ce = min(n, cb + CH);
   const int sb = min(ce, cb + sub * SUB), se = min(ce, sb + SUB);
@@ -269,26 +368,77 @@ __device__ float exact_seq_sum(const SampleSmem& sm, int n, uint64_t* stamps = n
   __syncthreads();
   STAMP(12);
   int nfast = 0;
-  if (tid < 64) {  // wave 0 walks the chunks; chunk c's map lives in lane c
-    const int okv = sm.chunk_ok[tid], ev = sm.chunk_e[tid];
-    const int t0v = (int)sm.chunk_t[2 * tid], t1v = (int)sm.chunk_t[2 * tid + 1];
-    float s = 0.0f;
+  if (tid < 64) {
+    // Wave 0. Chunk c's map lives in lane c. Runs of consecutive usable chunks predicted in the
+    // same binade are composed by a segmented parallel prefix of their parity maps, so the walk
+    // below does one O(1) step per run; unusable chunks (binade crossings) are added serially.
     const int nch = (n + CH - 1) / CH;
-    for (int c = 0; c < nch; ++c) {
-      const int b0 = c * CH, e0 = min(n, b0 + CH);
+    const int lane = tid;
+    const int okv = lane < nch ? sm.chunk_ok[lane] : 0, ev = sm.chunk_e[lane];
+    uint32_t P0 = sm.chunk_t[2 * lane], P1 = sm.chunk_t[2 * lane + 1];
+    const int okp = __shfl_up(okv, 1), evp = __shfl_up(ev, 1);
+    const bool head = lane == 0 || !okv || !okp || evp != ev;
+    bool F = head;
+    // segmented inclusive scan: P = (chunks from the run head to this chunk), composed in order
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t q0 = __shfl_up(P0, o), q1 = __shfl_up(P1, o);
+      const bool qf = __shfl_up(F ? 1 : 0, o) != 0;
+      if (lane >= o && !F) {
+        const uint32_t n0 = min(q0 + ((q0 & 1u) ? P1 : P0), 0x2000000u);        // incoming parity 0
+        const uint32_t n1 = min(q1 + (((1u + q1) & 1u) ? P1 : P0), 0x2000000u);  // incoming parity 1
+        P0 = n0;
+        P1 = n1;
+        F = qf;
+      }
+    }
+    const uint64_t heads = __ballot(head) & (nch >= 64 ? ~0ull : ((1ull << nch) - 1ull));
+    float s = 0.0f;
+    int c = 0;
+    while (c < nch) {
       const uint32_t sb2 = __builtin_bit_cast(uint32_t, s);
       const int ef = (int)((sb2 >> 23) & 0xFFu);
-      if (readlane_i(okv, c) && ef != 0 && ef - 127 == readlane_i(ev, c)) {
+      const bool is_head = (heads >> c) & 1ull;
+      if (is_head && readlane_i(okv, c) && ef != 0 && ef - 127 == readlane_i(ev, c)) {
+        const uint64_t later = heads >> (c + 1);
+        const int r = later ? c + __ffsll((long long)later) - 1 : nch - 1;  // last chunk of the run
         const uint32_t m = (sb2 & 0x7FFFFFu) | 0x800000u;
-        const uint32_t T = (uint32_t)((m & 1u) ? readlane_i(t1v, c) : readlane_i(t0v, c));
-        const uint32_t m2 = m + T;
-        if (m2 < 0x1000000u) {
-          s = __builtin_bit_cast(float, (sb2 & 0xFF800000u) | (m2 & 0x7FFFFFu));
-          ++nfast;
+        const uint32_t T = (uint32_t)((m & 1u) ? readlane_i((int)P1, r) : readlane_i((int)P0, r));
+        if (m + T < 0x1000000u) {
+          s = __builtin_bit_cast(float, (sb2 & 0xFF800000u) | ((m + T) & 0x7FFFFFu));
+          nfast += r - c + 1;
+          c = r + 1;
           continue;
         }
       }
-      s = wave_serial_add(s, sm.p, b0, e0);  // binade crossing: add this chunk one by one
+      // unusable chunk, or a run whose prediction failed: add chunk c in order on one lane
+      const int b0 = c * CH, e0 = min(n, b0 + CH);
+      float t = 0.0f;
+      if (lane == 0) t = lane_serial_add(s, sm.p, b0, e0);
+      s = readlane_f(t, 0);
+      ++c;
+      // the chunks after c (if inside a run) are no longer run heads; step them one at a time
+      while (c < nch && !((heads >> c) & 1ull)) {
+        const uint32_t sb3 = __builtin_bit_cast(uint32_t, s);
+        const int ef3 = (int)((sb3 >> 23) & 0xFFu);
+        bool fast = false;
+        if (readlane_i(okv, c) && ef3 != 0 && ef3 - 127 == readlane_i(ev, c)) {
+          const uint32_t m = (sb3 & 0x7FFFFFu) | 0x800000u;
+          const uint32_t T = (uint32_t)((m & 1u) ? sm.chunk_t[2 * c + 1] : sm.chunk_t[2 * c]);
+          if (m + T < 0x1000000u) {
+            s = __builtin_bit_cast(float, (sb3 & 0xFF800000u) | ((m + T) & 0x7FFFFFu));
+            fast = true;
+            ++nfast;
+          }
+        }
+        if (!fast) {
+          const int b1 = c * CH, e1 = min(n, b1 + CH);
+          float t1 = 0.0f;
+          if (lane == 0) t1 = lane_serial_add(s, sm.p, b1, e1);
+          s = readlane_f(t1, 0);
+        }
+        ++c;
+      }
     }
     if (tid == 0) {
       sm.fred[4] = s;
@@ -323,7 +473,7 @@ __device__ inline uint64_t pkey(float p, int i) {
 
 // The sampler. p holds the (masked) logits on entry. Returns the index in every thread.
 // status: 0 ok, RWKVTTS_EUNSUPPORTED for the documented limitation.
-__device__ int sample_block(const SampleSmem& sm, int n, float temperature, float top_p,
+__device__ __attribute__((always_inline)) int sample_block(const SampleSmem& sm, int n, float temperature, float top_p,
                             int top_k, const uint32_t* key, uint64_t draw, bool fixed42,
                             float* dbg, int* status, uint64_t* stamps = nullptr) {
   const int tid = threadIdx.x;

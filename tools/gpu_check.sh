@@ -4,7 +4,7 @@ mkdir -p gpurun_out
 timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/gpu_tests.log 2>&1
 rc=$?; echo "TESTS EXIT $rc"; tail -5 gpurun_out/gpu_tests.log
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 600 python bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/bench_quick.json 2> gpurun_out/bench_quick.err
+timeout -k 10 600 python bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/bench_quick.json 2> gpurun_out/bench_quick.err
 rc=$?; echo "BENCH EXIT $rc"
 python3 - <<'PY'
 import json
