@@ -48,6 +48,21 @@ def codec_flops(cd, T):
     return f
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per launch of a decode-step kernel from the newest committed PMC summary
+    (profiles/rNN_pmc_traffic.json, made by tools/gpu_profiles.sh + tools/make_pmc_json.py:
+    separate FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled per the gfx950 correction)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    if not files:
+        return None, None
+    k = json.load(open(files[-1]))["kernels"]
+    key = "ln_mix" if kernel.startswith("ln_mix") else kernel
+    if key not in k:
+        return None, None
+    return k[key]["traffic_bytes"], os.path.relpath(files[-1], ROOT)
+
+
 def algorithmic_bytes(d, R, head_rows):
     """Per-kernel algorithmic HBM bytes of one decode step with R rows."""
     C, F, L = d["n_embd"], d["n_ffn"], d["n_layer"]
@@ -205,9 +220,11 @@ def main():
             _, dom = max(cand)
             avg_s = kernels[dom]["avg_us"] * 1e-6
             ach = per_launch[dom] / avg_s / 1e9
+            traffic, tsrc = pmc_traffic(dom)
             roofline = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                        "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
-                        "bytes_per_launch": per_launch[dom], "avg_us": round(kernels[dom]["avg_us"], 2)}
+                        "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+                        "traffic_source": tsrc, "bytes_per_launch": per_launch[dom],
+                        "avg_us": round(kernels[dom]["avg_us"], 2)}
         # vocoder: MFMA-bound conv stack, achieved TFLOP/s per class and for the whole decoder
         cfl = codec_flops(cdims, B_PER_GPU * SEMANTIC)
         vk = {}

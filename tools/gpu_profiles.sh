@@ -1,0 +1,12 @@
+# Round profiles: rocprofv3 kernel-trace --stats of a bench run + separate PMC passes
+# (FETCH_SIZE, WRITE_SIZE) on the short LM workload. Outputs under gpurun_out/prof_r01/.
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/prof_r01
+mkdir -p $O
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o bench -- python3 $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline > $O/bench_trace.log 2>&1 || exit 1
+export LM_GRAPHS=0
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- python3 $R/tools/lm_short.py > $O/fetch.log 2>&1 || exit 1
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- python3 $R/tools/lm_short.py > $O/write.log 2>&1 || exit 1
+echo PROFILES_OK; find $O -name "*.csv" | head -20
