@@ -158,3 +158,15 @@ def codec_decode(dims_struct, weights: np.ndarray, semantic, global_tokens, thre
     if rc != 0:
         raise ValueError(f"oracle_codec_decode failed ({rc})")
     return pcm
+
+
+def mel(wav) -> np.ndarray:
+    """f32 restatement of extract_mel_spectrogram_consistent -> [128][n_frames]."""
+    w = np.ascontiguousarray(wav, dtype=np.float32)
+    n_frames = max(1, (w.size + 1024 - 1024) // 320 + 1) if w.size > 0 else 1
+    out = np.empty(128 * n_frames, dtype=np.float32)
+    nf = ctypes.c_int(0)
+    rc = lib().oracle_mel(w.ctypes.data if w.size else None, int(w.size), out.ctypes.data, ctypes.byref(nf))
+    if rc != 0:
+        raise ValueError(f"oracle_mel failed ({rc})")
+    return out[: 128 * nf.value].reshape(128, nf.value)

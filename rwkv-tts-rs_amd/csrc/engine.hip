@@ -346,7 +346,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     k.lnx_w = w.lnx_w; k.lnx_b = w.lnx_b;
     k.state = wkv_; k.slot_stride = (int64_t)Lc * H_ * 64 * 64; k.layer_off = (int64_t)l * H_ * 64 * 64;
     k.v_first = vfirst_; k.ldv = C; k.z_hi = z_hi_; k.z_lo = z_lo_; k.ldz = C;
-    k.segs = d_segs_; k.layer = l; k.C = C;
+    k.segs = d_segs_; k.layer = l; k.C = C; k.n_slots = S_;
     k.Dw = dims.d_decay; k.Da = dims.d_aaa; k.Dv = dims.d_mv; k.Dg = dims.d_gate;
     k.stamps = (l == 5) ? dbg_stamps_ : nullptr;
     k.exp = dbg_exp_;
@@ -750,7 +750,9 @@ int Engine::generate(const rwkvtts_request* reqs, int n, rwkvtts_result* res) {
       RT_OK(flush_prof());
       continue;
     }
-    // ---- decode steps over all active slots until one finishes
+    // ---- decode steps over all active slots until one finishes. Rows in slot order, so with
+    // every slot active row r is slot r (k_wkv2 speculates on that to start its state loads early).
+    std::sort(act.begin(), act.end(), [](const Active& x, const Active& y) { return x.slot < y.slot; });
     StepPlan p;
     p.tok_from_ctrl = true;
     p.advance = true;

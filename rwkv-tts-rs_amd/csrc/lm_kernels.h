@@ -80,6 +80,7 @@ struct WkvArgs {
   int ldz;
   const int4* segs;    // slot, row_begin, n_rows, _
   int layer, C, Dw, Da, Dv, Dg;
+  int n_slots;         // state slots (bounds the speculative slot = segment index)
   uint64_t* stamps;    // debug: 8 s_memtime stamps per workgroup (null in production)
   int exp;             // debug experiment bits (0 in production)
 };

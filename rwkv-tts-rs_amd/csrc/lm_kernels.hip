@@ -644,6 +644,8 @@ __global__ __launch_bounds__(128) void k_wkv2(WkvArgs a) {
   __shared__ __attribute__((aligned(16))) float s_vec[5][N];  // w, kk (unnormalised), a, k, r
   __shared__ float s_red[4][2];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, i = t >> 1, hf = t & 1;
+  uint64_t* stp = (a.stamps && t == 0) ? a.stamps + (blockIdx.y * gridDim.x + blockIdx.x) * 8 : nullptr;
+  if (stp) stp[0] = __builtin_amdgcn_s_memtime();
   const int h = blockIdx.y, C = a.C, c = h * N + i;
   const int4 sg = a.segs[blockIdx.x];
   // ---- head-only loads: half of channel c's LoRA-up rows (bf16) and its parameters
@@ -660,15 +662,20 @@ __global__ __launch_bounds__(128) void k_wkv2(WkvArgs a) {
     lw[UW + UA + UV + u] = *(const short8*)(a.g2t + (int64_t)c * DG + hf * (DG / 2) + u * 8);
   const float w0 = a.w0[c], a0 = a.a0[c], v0 = a.v0[c], kkc = a.k_k[c], kac = a.k_a[c];
   const float rkc = a.r_k[c], lnw = a.lnx_w[c], lnb = a.lnx_b[c];
-  // ---- segment-dependent loads: the half state row and the first row's split-K partials
-  const int slot = sg.x, r_begin = sg.y, n_rows = sg.z;
-  float* Srow = a.state + (int64_t)slot * a.slot_stride + a.layer_off + (int64_t)h * N * N + i * N + hf * 32;
+  // ---- segment-dependent loads, issued speculatively for slot = row = segment index (the
+  // decode layout: rows in slot order, one row per slot) and redone if the descriptor differs
+  const int spec = blockIdx.x;
+  const int64_t soff = a.layer_off + (int64_t)h * N * N + i * N + hf * 32;
   float S[32];
+  auto load_state = [&](int slot) {
+    const float* Sp = a.state + (int64_t)slot * a.slot_stride + soff;
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const float4_ v4 = *(const float4_*)(Srow + q * 4);
-    S[q * 4 + 0] = v4[0]; S[q * 4 + 1] = v4[1]; S[q * 4 + 2] = v4[2]; S[q * 4 + 3] = v4[3];
-  }
+    for (int q = 0; q < 8; ++q) {
+      const float4_ v4 = *(const float4_*)(Sp + q * 4);
+      S[q * 4 + 0] = v4[0]; S[q * 4 + 1] = v4[1]; S[q * 4 + 2] = v4[2]; S[q * 4 + 3] = v4[3];
+    }
+  };
+  load_state(spec < a.n_slots ? spec : 0);
   constexpr int HPL = (DALL + 127) / 128;  // hidden elements per thread
   float hp[MAXP][HPL], rp[MAXP], kp[MAXP], vp[MAXP], vf = 0.f;
   auto load_parts = [&](int row) {
@@ -688,7 +695,11 @@ __global__ __launch_bounds__(128) void k_wkv2(WkvArgs a) {
     }
     vf = a.layer > 0 ? a.v_first[(int64_t)row * a.ldv + c] : 0.f;
   };
-  load_parts(r_begin);
+  load_parts(spec);
+  const int slot = sg.x, r_begin = sg.y, n_rows = sg.z;
+  float* Srow = a.state + (int64_t)slot * a.slot_stride + soff;
+  if (slot != spec) load_state(slot);
+  if (r_begin != spec) load_parts(r_begin);
   for (int rr = 0; rr < n_rows; ++rr) {
     const int row = r_begin + rr;
     if (rr > 0) load_parts(row);
@@ -708,6 +719,7 @@ __global__ __launch_bounds__(128) void k_wkv2(WkvArgs a) {
       v += vp[p];
     }
     __syncthreads();
+    if (stp && rr == 0) stp[1] = __builtin_amdgcn_s_memtime();
     // ---- LoRA up: this thread's half of channel c's four dot products, pair-combined
     float lo0 = 0.f, lo1 = 0.f, lo2 = 0.f, lo3 = 0.f;
     auto dot8 = [&](const short8 q, const float* hsrc) {
@@ -751,6 +763,7 @@ __global__ __launch_bounds__(128) void k_wkv2(WkvArgs a) {
       s_vec[0][i] = w; s_vec[1][i] = kk; s_vec[2][i] = av; s_vec[3][i] = k; s_vec[4][i] = r;
     }
     __syncthreads();
+    if (stp && rr == 0) stp[2] = __builtin_amdgcn_s_memtime();
     const float inv = 1.0f / fmaxf(sqrtf(s_red[0][0] + s_red[0][1]), 1e-12f);
     const float bonus = s_red[1][0] + s_red[1][1];
     // ---- state half-row update: S[i][j] = S[i][j]*w_j - sa_i*kk_j*a_j + v_i*k_j ; y_i = S[i].r
@@ -786,12 +799,15 @@ __global__ __launch_bounds__(128) void k_wkv2(WkvArgs a) {
       if (lane == 0) { s_red[2][wave] = s1; s_red[3][wave] = s2; }
     }
     __syncthreads();
+    if (stp && rr == 0) stp[3] = __builtin_amdgcn_s_memtime();
     const float mean = (s_red[2][0] + s_red[2][1]) * (1.0f / N);
     const float var = fmaxf((s_red[3][0] + s_red[3][1]) * (1.0f / N) - mean * mean, 0.f);
     if (hf == 0) {
       const float gn = (y - mean) * (1.0f / sqrtf(var + 64e-5f)) * lnw + lnb;
       split_store((gn + bonus * v) * lo3, a.z_hi, a.z_lo, (int64_t)row * a.ldz + c);
     }
+    if (stp && rr == 0) stp[4] = __builtin_amdgcn_s_memtime();
+    if (stp && rr == 1) stp[6] = __builtin_amdgcn_s_memtime();
     if (rr + 1 < n_rows) __syncthreads();
   }
 #pragma unroll
@@ -799,6 +815,7 @@ __global__ __launch_bounds__(128) void k_wkv2(WkvArgs a) {
     float4_ v4 = {S[q * 4 + 0], S[q * 4 + 1], S[q * 4 + 2], S[q * 4 + 3]};
     *(float4_*)(Srow + q * 4) = v4;
   }
+  if (stp) stp[5] = __builtin_amdgcn_s_memtime();
 }
 
 void launch_wkv(const WkvArgs& a, int n_seg, int H, hipStream_t st) {
