@@ -60,6 +60,13 @@ __host__ __device__ inline float f16_to_f32(uint16_t h) {
   return as_f32(u);
 }
 
+// 16-bit weight / activation-plane formats: bf16 (default) or IEEE f16 (fp16 checkpoints, the
+// reference's web-rwkv numerics). Device conversions, f32 -> 16 bit round-to-nearest-even.
+__device__ inline float h16_to_f32(uint16_t h) { return (float)__builtin_bit_cast(_Float16, h); }
+__device__ inline uint16_t f32_to_h16(float x) { return __builtin_bit_cast(uint16_t, (_Float16)x); }
+__device__ inline float w16_to_f32(uint16_t v, bool f16) { return f16 ? h16_to_f32(v) : bf16_to_f32(v); }
+__device__ inline uint16_t f32_to_w16(float x, bool f16) { return f16 ? f32_to_h16(x) : f32_to_bf16(x); }
+
 inline int64_t align_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
 
 }  // namespace rwkvtts

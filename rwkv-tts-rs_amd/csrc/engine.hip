@@ -49,8 +49,9 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
     memcpy(&hdr, weights, sizeof(hdr));
   }
   RT_CHECK(hdr.magic == RWKVTTS_BLOB_MAGIC, RWKVTTS_EINVAL, "weight blob: bad magic");
-  RT_CHECK(hdr.dtype == RWKVTTS_DTYPE_BF16, RWKVTTS_EUNSUPPORTED,
-           "GPU path supports bf16 matrices (f16 blobs: convert with rwkvtts.weights)");
+  RT_CHECK(hdr.dtype == RWKVTTS_DTYPE_BF16 || hdr.dtype == RWKVTTS_DTYPE_F16, RWKVTTS_EUNSUPPORTED,
+           "weight blob: matrices must be bf16 or f16");
+  f16_ = hdr.dtype == RWKVTTS_DTYPE_F16 ? 1 : 0;
   dims = hdr.dims;
   const int C = dims.n_embd, F = dims.n_ffn;
   RT_CHECK(dims.head_size == 64, RWKVTTS_EUNSUPPORTED, "head_size must be 64");
@@ -285,13 +286,14 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
   if (tok_from_ctrl)
     hipLaunchKernelGGL(k_prepare_tokens, dim3(nb), dim3(256), 0, stream_, d_rows_, d_ctrl_, d_tok_, R);
   prof_begin(&ev);
-  launch_embed(d_tok_, emb_, ln0_w_, ln0_b_, h0_, R, C, stream_);
+  launch_embed(d_tok_, emb_, ln0_w_, ln0_b_, h0_, R, C, f16_, stream_);
   prof_end("embed", ev);
   const int64_t RC = (int64_t)Rmax_ * C;
   for (int l = 0; l < Lc; ++l) {
     const LayerW& w = L_[l];
     // ---- att: residual (+ previous layer's ffn partials) -> LN1 -> 6 mixes
     LnMixArgs m{};
+    m.f16 = f16_;
     m.h_in = h0_;
     m.h_out = h1_;
     m.part = partF_;
@@ -318,6 +320,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     prof_end("ln_mix_att", ev);
     // ---- r, k, v and the LoRA-down projections (w, a, v, g) in one launch (7 segments)
     GemmArgs g{};
+    g.f16 = f16_;
     int tiles = 0;
     auto seg = [&](int idx, const bf16_t* W, int mix, int N, int col_off) {
       g.seg[idx] = {W, xm_hi_ + mix * RC, xm_lo_ + mix * RC, C, N, col_off, tiles};
@@ -339,6 +342,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     prof_end("gemm_rkv_lora", ev);
     // ---- WKV + LoRA-up + GroupNorm + bonus + gate
     WkvArgs k{};
+    k.f16 = f16_;
     k.part = partA_; k.n_part = splitA_; k.ldp = ldA_; k.part_stride = (int64_t)Rmax_ * ldA_;
     k.lup = w.lup;
     k.w2t = w.w2t; k.a2t = w.a2t; k.v2t = w.v2t; k.g2t = w.g2t;
@@ -355,6 +359,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     prof_end("wkv", ev);
     // ---- output projection (split-K partials)
     GemmArgs go{};
+    go.f16 = f16_;
     go.nseg = 1;
     go.seg[0] = {w.wo, z_hi_, z_lo_, C, C, 0, 0};
     go.K = C; go.M = R; go.k_split = splitO_; go.kslice = C / splitO_;
@@ -379,6 +384,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     launch_ln_mix(f, R, stream_);
     prof_end("ln_mix_ffn", ev);
     GemmArgs gk{};
+    gk.f16 = f16_;
     gk.nseg = 1;
     gk.seg[0] = {w.ffn_k, xf_hi_, xf_lo_, C, F, 0, 0};
     gk.K = C; gk.M = R; gk.k_split = splitK_; gk.kslice = C / splitK_;
@@ -387,6 +393,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     launch_gemm(gk, stream_);
     prof_end("gemm_ffn_key", ev);
     GemmArgs gv{};
+    gv.f16 = f16_;
     gv.nseg = 1;
     gv.seg[0] = {w.ffn_v, nullptr, nullptr, F, C, 0, 0};
     gv.K = F; gv.M = R; gv.k_split = splitF_; gv.kslice = F / splitF_;
@@ -400,6 +407,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
   }
   if (n_lg > 0) {
     LnMixArgs o{};
+    o.f16 = f16_;
     o.h_in = h0_;
     o.h_out = nullptr;
     o.part = partF_;
@@ -420,6 +428,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     launch_ln_mix(o, n_lg, stream_);
     prof_end("ln_out", ev);
     GemmArgs gh{};
+    gh.f16 = f16_;
     gh.nseg = 1;
     gh.seg[0] = {head_, xo_hi_, xo_lo_, C, head_rows, 0, 0};
     gh.K = C; gh.M = n_lg; gh.k_split = splitH_; gh.kslice = C / splitH_;

@@ -32,6 +32,7 @@ struct LnMixArgs {
   const int4* rows;    // per row: slot, flags, prev_row, parity
   const int* row_map;  // output row -> source row (ln_out) or null
   int n_rows;          // set by the launcher
+  int f16;             // planes in f16 (fp16 model) instead of bf16
 };
 
 struct GemmSeg {
@@ -60,6 +61,7 @@ struct GemmArgs {
   int64_t split_stride;
   int ldo;
   uint64_t* stamps;    // debug: 4 s_memtime stamps per workgroup (null in production)
+  int f16;             // weights and activation planes in f16 (fp16 model)
 };
 
 struct WkvArgs {
@@ -81,12 +83,13 @@ struct WkvArgs {
   const int4* segs;    // slot, row_begin, n_rows, _
   int layer, C, Dw, Da, Dv, Dg;
   int n_slots;         // state slots (bounds the speculative slot = segment index)
+  int f16;             // fp16 model: LoRA-up rows and the z planes are f16
   uint64_t* stamps;    // debug: 8 s_memtime stamps per workgroup (null in production)
   int exp;             // debug experiment bits (0 in production)
 };
 
 void launch_embed(const uint32_t* tokens, const bf16_t* emb, const float* w, const float* b,
-                  float* h, int R, int C, hipStream_t st);
+                  float* h, int R, int C, int f16, hipStream_t st);
 void launch_ln_mix(const LnMixArgs& a, int n_out_rows, hipStream_t st);
 void launch_gemm(const GemmArgs& a, hipStream_t st);
 void launch_wkv(const WkvArgs& a, int n_seg, int H, hipStream_t st);

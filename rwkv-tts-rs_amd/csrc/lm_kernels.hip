@@ -18,6 +18,7 @@
 namespace rwkvtts {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 __device__ inline float wave_sum(float v) {
 #pragma unroll
@@ -35,18 +36,18 @@ __device__ inline float block_sum256(float v, float* red) {
   return (red[0] + red[1]) + (red[2] + red[3]);
 }
 
-__device__ inline void split_store(float x, bf16_t* hi, bf16_t* lo, int64_t idx) {
-  const uint16_t h = f32_to_bf16(x);
-  const float r = x - bf16_to_f32(h);
+__device__ inline void split_store(float x, bf16_t* hi, bf16_t* lo, int64_t idx, bool f16 = false) {
+  const uint16_t h = f32_to_w16(x, f16);
+  const float r = x - w16_to_f32(h, f16);
   hi[idx] = h;
-  lo[idx] = f32_to_bf16(r);
+  lo[idx] = f32_to_w16(r, f16);
 }
 
 // ------------------------------------------------------------------------------------
 // embed: h[r] = LN0(emb[token[r]])
 // ------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_embed(const uint32_t* tokens, const bf16_t* emb,
-                                               const float* w, const float* b, float* h, int C) {
+                                               const float* w, const float* b, float* h, int C, int f16) {
   __shared__ float red[4];
   const int r = blockIdx.x;
   const uint32_t tok = tokens[r];
@@ -56,7 +57,7 @@ __global__ __launch_bounds__(256) void k_embed(const uint32_t* tokens, const bf1
 #pragma unroll
   for (int i = 0; i < kMaxPerThread; ++i) {
     const int c = threadIdx.x + i * 256;
-    v[i] = c < C ? bf16_to_f32(e[c]) : 0.f;
+    v[i] = c < C ? w16_to_f32(e[c], f16 != 0) : 0.f;
     s += v[i];
   }
   const float mean = block_sum256(s, red) / (float)C;
@@ -149,12 +150,12 @@ __device__ inline void ln_apply(const LnMixArgs& a, const float4_* w, const floa
     for (int e = 0; e < 4; ++e) v[q][e] = (v[q][e] - mean) * rstd * w[q][e] + b[q][e];
 }
 
-__device__ inline void store_split4(const float4_& x, bf16_t* hi, bf16_t* lo, int64_t idx) {
+__device__ inline void store_split4(const float4_& x, bf16_t* hi, bf16_t* lo, int64_t idx, bool f16) {
   uint16_t h[4], l[4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
-    h[e] = f32_to_bf16(x[e]);
-    l[e] = f32_to_bf16(x[e] - bf16_to_f32(h[e]));
+    h[e] = f32_to_w16(x[e], f16);
+    l[e] = f32_to_w16(x[e] - w16_to_f32(h[e], f16), f16);
   }
   *(uint2*)(hi + idx) = make_uint2(h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16));
   *(uint2*)(lo + idx) = make_uint2(l[0] | ((uint32_t)l[1] << 16), l[2] | ((uint32_t)l[3] << 16));
@@ -197,7 +198,7 @@ __global__ __launch_bounds__(256) void k_ln_mix(LnMixArgs a) {
 #pragma unroll
     for (int q = 0; q < kLnVec; ++q) {
       const int c = t4 + 1024 * q;
-      if (c < a.C) store_split4(v[q], a.x_hi, a.x_lo, (int64_t)out_row * a.ldx + c);
+      if (c < a.C) store_split4(v[q], a.x_hi, a.x_lo, (int64_t)out_row * a.ldx + c, a.f16 != 0);
     }
     return;
   }
@@ -215,7 +216,8 @@ __global__ __launch_bounds__(256) void k_ln_mix(LnMixArgs a) {
         float4_ x;
 #pragma unroll
         for (int e = 0; e < 4; ++e) x[e] = v[q][e] + (pv[q][e] - v[q][e]) * mu[m][q][e];
-        store_split4(x, a.x_hi + m * a.mix_stride, a.x_lo + m * a.mix_stride, (int64_t)out_row * a.ldx + c);
+        store_split4(x, a.x_hi + m * a.mix_stride, a.x_lo + m * a.mix_stride, (int64_t)out_row * a.ldx + c,
+                     a.f16 != 0);
       }
     }
   }
@@ -241,7 +243,7 @@ __global__ __launch_bounds__(256) void k_ln_mix(LnMixArgs a) {
 //   Each wave owns complete output columns: no cross-wave reduction; split-K partial slabs
 //   are summed (fixed order) by the consumer.
 // ------------------------------------------------------------------------------------
-template <int MT, int KSTEPS, int XMODE>
+template <int MT, int KSTEPS, int XMODE, bool F16>
 __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int KS = KSTEPS * 32;      // K slice
@@ -324,8 +326,8 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const float y = x[u][e] > 0.f ? x[u][e] * x[u][e] : 0.f;
-        h[e] = f32_to_bf16(y);
-        l[e] = f32_to_bf16(y - bf16_to_f32(h[e]));
+        h[e] = f32_to_w16(y, F16);
+        l[e] = f32_to_w16(y - w16_to_f32(h[e], F16), F16);
       }
       *(uint2*)(xh + r * LD + k4) = make_uint2(h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16));
       *(uint2*)(xl + r * LD + k4) = make_uint2(l[0] | ((uint32_t)l[1] << 16), l[2] | ((uint32_t)l[3] << 16));
@@ -344,10 +346,17 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
       const int o = (m * 16 + li) * LD + t * 32 + g * 8;
       const short8 ah = *(const short8*)(xh + o);
       const short8 al = *(const short8*)(xl + o);
-      acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ah),
-                                                       __builtin_bit_cast(bf16x8, b[t]), acc[m], 0, 0, 0);
-      acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, al),
-                                                       __builtin_bit_cast(bf16x8, b[t]), acc[m], 0, 0, 0);
+      if constexpr (F16) {
+        acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, ah),
+                                                        __builtin_bit_cast(f16x8, b[t]), acc[m], 0, 0, 0);
+        acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, al),
+                                                        __builtin_bit_cast(f16x8, b[t]), acc[m], 0, 0, 0);
+      } else {
+        acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ah),
+                                                         __builtin_bit_cast(bf16x8, b[t]), acc[m], 0, 0, 0);
+        acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, al),
+                                                         __builtin_bit_cast(bf16x8, b[t]), acc[m], 0, 0, 0);
+      }
     }
   }
   if (gst) gst[2] = __builtin_amdgcn_s_memtime() + (uint64_t)(acc[0][0] != acc[0][0]);
@@ -484,8 +493,9 @@ __global__ __launch_bounds__(256, 2) void k_wkv(WkvArgs a) {
         if (e < eq) {  // uniform
           const float4_ hv = *(const float4_*)(hq + e);
           const uint2 q = lw[u];
-          const float d = bf16_to_f32((uint16_t)(q.x & 0xFFFF)) * hv[0] + bf16_to_f32((uint16_t)(q.x >> 16)) * hv[1] +
-                          bf16_to_f32((uint16_t)(q.y & 0xFFFF)) * hv[2] + bf16_to_f32((uint16_t)(q.y >> 16)) * hv[3];
+          const bool f16 = a.f16 != 0;
+          const float d = w16_to_f32((uint16_t)(q.x & 0xFFFF), f16) * hv[0] + w16_to_f32((uint16_t)(q.x >> 16), f16) * hv[1] +
+                          w16_to_f32((uint16_t)(q.y & 0xFFFF), f16) * hv[2] + w16_to_f32((uint16_t)(q.y >> 16), f16) * hv[3];
           lo0 += e < e1 ? d : 0.f;
           lo1 += (e >= e1 && e < e2) ? d : 0.f;
           lo2 += (e >= e2 && e < e3) ? d : 0.f;
@@ -550,7 +560,7 @@ __global__ __launch_bounds__(256, 2) void k_wkv(WkvArgs a) {
       const float rstd = 1.0f / sqrtf(var + 64e-5f);
       const float bonus = ((s_red[1][0] + s_red[1][1]) + s_red[1][2]) + s_red[1][3];
       const float gn = dv * rstd * lnw + lnb;
-      split_store((gn + bonus * s_v[lane]) * s_g[lane], a.z_hi, a.z_lo, (int64_t)row * a.ldz + c);
+      split_store((gn + bonus * s_v[lane]) * s_g[lane], a.z_hi, a.z_lo, (int64_t)row * a.ldz + c, a.f16 != 0);
     }
     if (rr == 0) { WKV_STAMP(5) }
     if (rr + 1 < n_rows) __syncthreads();
@@ -568,8 +578,8 @@ __global__ __launch_bounds__(256, 2) void k_wkv(WkvArgs a) {
 // host launchers
 // ------------------------------------------------------------------------------------
 void launch_embed(const uint32_t* tokens, const bf16_t* emb, const float* w, const float* b,
-                  float* h, int R, int C, hipStream_t st) {
-  hipLaunchKernelGGL(k_embed, dim3(R), dim3(256), 0, st, tokens, emb, w, b, h, C);
+                  float* h, int R, int C, int f16, hipStream_t st) {
+  hipLaunchKernelGGL(k_embed, dim3(R), dim3(256), 0, st, tokens, emb, w, b, h, C, f16);
 }
 void launch_ln_mix(const LnMixArgs& a, int n_out_rows, hipStream_t st) {
   LnMixArgs b = a;
@@ -582,8 +592,13 @@ void launch_ln_mix(const LnMixArgs& a, int n_out_rows, hipStream_t st) {
 template <int MT, int KSTEPS>
 static void launch_gemm_t(const GemmArgs& a, dim3 grid, hipStream_t st) {
   const size_t lds = (size_t)MT * 16 * (KSTEPS * 32 + 8) * 2 * 2;
-  if (a.xmode == kXPlanes) hipLaunchKernelGGL((k_gemm<MT, KSTEPS, kXPlanes>), grid, dim3(256), lds, st, a);
-  else hipLaunchKernelGGL((k_gemm<MT, KSTEPS, kXRelu2>), grid, dim3(256), lds, st, a);
+  if (a.f16) {
+    if (a.xmode == kXPlanes) hipLaunchKernelGGL((k_gemm<MT, KSTEPS, kXPlanes, true>), grid, dim3(256), lds, st, a);
+    else hipLaunchKernelGGL((k_gemm<MT, KSTEPS, kXRelu2, true>), grid, dim3(256), lds, st, a);
+  } else {
+    if (a.xmode == kXPlanes) hipLaunchKernelGGL((k_gemm<MT, KSTEPS, kXPlanes, false>), grid, dim3(256), lds, st, a);
+    else hipLaunchKernelGGL((k_gemm<MT, KSTEPS, kXRelu2, false>), grid, dim3(256), lds, st, a);
+  }
 }
 
 int gemm_ksteps(int kslice) { return kslice / 32; }
@@ -727,9 +742,9 @@ __global__ __launch_bounds__(128) void k_wkv2(WkvArgs a) {
       const float4_ h1 = *(const float4_*)(hsrc + 4);
       float acc = 0.f;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) acc += bf16_to_f32((uint16_t)q[e]) * h0[e];
+      for (int e = 0; e < 4; ++e) acc += w16_to_f32((uint16_t)q[e], a.f16 != 0) * h0[e];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) acc += bf16_to_f32((uint16_t)q[4 + e]) * h1[e];
+      for (int e = 0; e < 4; ++e) acc += w16_to_f32((uint16_t)q[4 + e], a.f16 != 0) * h1[e];
       return acc;
     };
 #pragma unroll
@@ -804,7 +819,7 @@ __global__ __launch_bounds__(128) void k_wkv2(WkvArgs a) {
     const float var = fmaxf((s_red[3][0] + s_red[3][1]) * (1.0f / N) - mean * mean, 0.f);
     if (hf == 0) {
       const float gn = (y - mean) * (1.0f / sqrtf(var + 64e-5f)) * lnw + lnb;
-      split_store((gn + bonus * v) * lo3, a.z_hi, a.z_lo, (int64_t)row * a.ldz + c);
+      split_store((gn + bonus * v) * lo3, a.z_hi, a.z_lo, (int64_t)row * a.ldz + c, a.f16 != 0);
     }
     if (stp && rr == 0) stp[4] = __builtin_amdgcn_s_memtime();
     if (stp && rr == 1) stp[6] = __builtin_amdgcn_s_memtime();

@@ -14,10 +14,11 @@ pytestmark = pytest.mark.gpu
 LOGIT_ATOL = 2e-3
 
 
-@pytest.fixture(scope="module", params=["tiny", "small"])
+@pytest.fixture(scope="module", params=["tiny", "small", "tiny_f16", "small_f16"])
 def models(request):
-    dims = W.DIMS_TINY if request.param == "tiny" else W.DIMS_SMALL
-    blob = W.synth_blob(dims, seed=123)
+    dims = W.DIMS_TINY if request.param.startswith("tiny") else W.DIMS_SMALL
+    dt = rwkvtts._ffi.DTYPE_F16 if request.param.endswith("f16") else rwkvtts._ffi.DTYPE_BF16
+    blob = W.synth_blob(dims, seed=123, dtype=dt)
     import oracle
     om = oracle.Model(blob)
     rt = rwkvtts.SharedRwkvRuntime(blob, max_slots=8, token_chunk_size=64, use_graphs=False)

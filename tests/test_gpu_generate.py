@@ -14,9 +14,11 @@ pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
 
-@pytest.fixture(scope="module")
-def setup():
-    blob = W.synth_blob(W.DIMS_TINY, seed=99)
+@pytest.fixture(scope="module", params=["bf16", "f16"])
+def setup(request):
+    # f16 = fp16 matrices (config 5 / the reference's web-rwkv numerics): f16 MFMA + f16 planes
+    dt = rwkvtts._ffi.DTYPE_F16 if request.param == "f16" else rwkvtts._ffi.DTYPE_BF16
+    blob = W.synth_blob(W.DIMS_TINY, seed=99, dtype=dt)
     import oracle
     om = oracle.Model(blob)
     rt = rwkvtts.SharedRwkvRuntime(blob, max_slots=8, token_chunk_size=128, use_graphs=True)
