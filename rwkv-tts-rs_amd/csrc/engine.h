@@ -75,6 +75,7 @@ class Engine {
   int splitA_ = 1, splitO_ = 1, splitK_ = 1, splitF_ = 1, splitH_ = 1;
   bool use_graphs_ = true;
   uint8_t* wblob_ = nullptr;
+  bf16_t* wpack_ = nullptr;      // GEMM matrices in MFMA fragment blocks (launch_pack_frag)
   bf16_t* lora_pack_ = nullptr;  // [L][C][Dtot] LoRA-up rows in k_wkv's per-thread order
   const bf16_t* emb_ = nullptr;
   const bf16_t* head_ = nullptr;

@@ -121,12 +121,38 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
     w.ffn_k = Mv(RWKVTTS_L_FFN_K); w.ffn_v = Mv(RWKVTTS_L_FFN_V);
   }
   RT_OK(alloc(&lora_pack_, (size_t)dims.n_layer * C * Dtot_));
+  RT_HIP(hipDeviceSynchronize());  // alloc's memset runs on the null stream; stream_ is non-blocking
   for (int l = 0; l < dims.n_layer; ++l) {
     LayerW& w = L_[l];
     bf16_t* dst = lora_pack_ + (size_t)l * C * Dtot_;
     launch_pack_lora(w.w2t, w.a2t, w.v2t, w.g2t, C, dims.d_decay, dims.d_aaa, dims.d_mv, dims.d_gate, dst, stream_);
     RT_HIP(hipGetLastError());
     w.lup = dst;
+  }
+  // GEMM matrices -> MFMA fragment blocks (k_gemm streams each wave's weights as contiguous 1 KB
+  // blocks); the blob's row-major copies stay for the embedding gather and the oracle layout
+  {
+    auto packed_elems = [](int N, int K) { return (size_t)((N + 15) / 16) * 16 * K; };
+    const int Dw = dims.d_decay, Da = dims.d_aaa, Dv = dims.d_mv, Dg = dims.d_gate;
+    size_t per_layer = 3 * packed_elems(C, C) + packed_elems(Dw, C) + packed_elems(Da, C) + packed_elems(Dv, C) +
+                       packed_elems(Dg, C) + packed_elems(C, C) + packed_elems(F, C) + packed_elems(C, F);
+    size_t total = per_layer * dims.n_layer + packed_elems(dims.n_vocab, C);
+    RT_OK(alloc(&wpack_, total));
+    RT_HIP(hipDeviceSynchronize());  // alloc's memset runs on the null stream; stream_ is non-blocking
+    bf16_t* dst = wpack_;
+    auto pack = [&](const bf16_t*& Wm, int N, int K) {
+      launch_pack_frag(Wm, N, K, dst, stream_);
+      Wm = dst;
+      dst += packed_elems(N, K);
+    };
+    for (int l = 0; l < dims.n_layer; ++l) {
+      LayerW& w = L_[l];
+      pack(w.wr, C, C); pack(w.wk, C, C); pack(w.wv, C, C);
+      pack(w.w1t, Dw, C); pack(w.a1t, Da, C); pack(w.v1t, Dv, C); pack(w.g1t, Dg, C);
+      pack(w.wo, C, C); pack(w.ffn_k, F, C); pack(w.ffn_v, C, F);
+    }
+    pack(head_, dims.n_vocab, C);
+    RT_HIP(hipGetLastError());
   }
   RT_HIP(hipStreamSynchronize(stream_));
   // state
@@ -316,7 +342,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     m.rows = d_rows_;
     m.row_map = nullptr;
     prof_begin(&ev);
-    launch_ln_mix(m, R, stream_);
+    if (!(dbg_exp_ & 0x10000)) launch_ln_mix(m, R, stream_);
     prof_end("ln_mix_att", ev);
     // ---- r, k, v and the LoRA-down projections (w, a, v, g) in one launch (7 segments)
     GemmArgs g{};
@@ -338,7 +364,8 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     g.xmode = kXPlanes; g.out = partA_; g.split_stride = (int64_t)Rmax_ * ldA_; g.ldo = ldA_;
     prof_begin(&ev);
     g.stamps = (l == 5 && dbg_gstamps_) ? dbg_gstamps_ : nullptr;
-    launch_gemm(g, stream_);
+    g.exp = dbg_exp_ >> 8;
+    if (!(dbg_exp_ & 0x40000)) launch_gemm(g, stream_);
     prof_end("gemm_rkv_lora", ev);
     // ---- WKV + LoRA-up + GroupNorm + bonus + gate
     WkvArgs k{};
@@ -355,7 +382,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     k.stamps = (l == 5) ? dbg_stamps_ : nullptr;
     k.exp = dbg_exp_;
     prof_begin(&ev);
-    launch_wkv(k, n_seg, H_, stream_);
+    if (!(dbg_exp_ & 0x20000)) launch_wkv(k, n_seg, H_, stream_);
     prof_end("wkv", ev);
     // ---- output projection (split-K partials)
     GemmArgs go{};
@@ -365,7 +392,8 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     go.K = C; go.M = R; go.k_split = splitO_; go.kslice = C / splitO_;
     go.xmode = kXPlanes; go.out = partO_; go.split_stride = RC; go.ldo = C;
     prof_begin(&ev);
-    launch_gemm(go, stream_);
+    go.exp = dbg_exp_ >> 8;
+    if (!(dbg_exp_ & 0x40000)) launch_gemm(go, stream_);
     prof_end("gemm_wo", ev);
     // ---- ffn: residual + Wo partials -> LN2 -> mix
     LnMixArgs f = m;
@@ -381,7 +409,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     f.x_lo = xf_lo_;
     f.shift = ffn_sh_;
     prof_begin(&ev);
-    launch_ln_mix(f, R, stream_);
+    if (!(dbg_exp_ & 0x10000)) launch_ln_mix(f, R, stream_);
     prof_end("ln_mix_ffn", ev);
     GemmArgs gk{};
     gk.f16 = f16_;
@@ -390,7 +418,8 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     gk.K = C; gk.M = R; gk.k_split = splitK_; gk.kslice = C / splitK_;
     gk.xmode = kXPlanes; gk.out = partK_; gk.split_stride = (int64_t)Rmax_ * F; gk.ldo = F;
     prof_begin(&ev);
-    launch_gemm(gk, stream_);
+    gk.exp = dbg_exp_ >> 8;
+    if (!(dbg_exp_ & 0x40000)) launch_gemm(gk, stream_);
     prof_end("gemm_ffn_key", ev);
     GemmArgs gv{};
     gv.f16 = f16_;
@@ -402,7 +431,8 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     gv.out = partF_; gv.split_stride = RC; gv.ldo = C;
     prof_begin(&ev);
     gv.stamps = (l == 5 && dbg_gstamps_) ? dbg_gstamps_ + 4096 * 4 : nullptr;
-    launch_gemm(gv, stream_);
+    gv.exp = dbg_exp_ >> 8;
+    if (!(dbg_exp_ & 0x40000)) launch_gemm(gv, stream_);
     prof_end("gemm_ffn_value", ev);
   }
   if (n_lg > 0) {
@@ -434,7 +464,8 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     gh.K = C; gh.M = n_lg; gh.k_split = splitH_; gh.kslice = C / splitH_;
     gh.xmode = kXPlanes; gh.out = logits_; gh.split_stride = (int64_t)Rmax_ * Vpad_; gh.ldo = Vpad_;
     prof_begin(&ev);
-    launch_gemm(gh, stream_);
+    gh.exp = dbg_exp_ >> 8;
+    if (!(dbg_exp_ & 0x40000)) launch_gemm(gh, stream_);
     prof_end("gemm_head", ev);
     if (advance) {
       AdvanceArgs a{};

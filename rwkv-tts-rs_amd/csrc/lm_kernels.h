@@ -36,7 +36,7 @@ struct LnMixArgs {
 };
 
 struct GemmSeg {
-  const bf16_t* W;     // [N][K]
+  const bf16_t* W;     // packed by launch_pack_frag (ceil(N/16) blocks of 16 x K)
   const bf16_t* Xhi;   // [rows][ldx]
   const bf16_t* Xlo;
   int ldx;
@@ -62,6 +62,7 @@ struct GemmArgs {
   int ldo;
   uint64_t* stamps;    // debug: 4 s_memtime stamps per workgroup (null in production)
   int f16;             // weights and activation planes in f16 (fp16 model)
+  int exp;             // debug experiment bits (0 in production): 1 skip X loads, 2 skip W loads
 };
 
 struct WkvArgs {
@@ -93,6 +94,9 @@ void launch_embed(const uint32_t* tokens, const bf16_t* emb, const float* w, con
 void launch_ln_mix(const LnMixArgs& a, int n_out_rows, hipStream_t st);
 void launch_gemm(const GemmArgs& a, hipStream_t st);
 void launch_wkv(const WkvArgs& a, int n_seg, int H, hipStream_t st);
+// Repack a GEMM matrix W [N][K] (K % 32 == 0) into MFMA fragment blocks (k_gemm's layout):
+// out holds ceil(N/16)*16*K elements.
+void launch_pack_frag(const bf16_t* W, int N, int K, bf16_t* out, hipStream_t st);
 // Repack one layer's w2t | a2t | v2t | g2t ([C][D] each) into the per-thread order of k_wkv.
 void launch_pack_lora(const bf16_t* w2t, const bf16_t* a2t, const bf16_t* v2t, const bf16_t* g2t, int C,
                       int Dw, int Da, int Dv, int Dg, bf16_t* out, hipStream_t st);

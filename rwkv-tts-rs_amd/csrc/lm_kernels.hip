@@ -84,13 +84,32 @@ __global__ __launch_bounds__(256) void k_embed(const uint32_t* tokens, const bf1
 // ------------------------------------------------------------------------------------
 __device__ inline float4_ ld4(const float* p) { return *(const float4_*)p; }
 
-template <int kLnVec>
+template <int kLnVec, int NP>  // NP >= 0: exactly NP partial slabs (all loads in flight at once); -1: a.n_part
 __device__ inline void ln_load_row(const LnMixArgs& a, int src, float4_* v) {
   const int t4 = 4 * threadIdx.x;
+  const float4_ z = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int q = 0; q < kLnVec; ++q) {
     const int c = t4 + 1024 * q;
-    v[q] = c < a.C ? ld4(a.h_in + (int64_t)src * a.C + c) : (float4_){0.f, 0.f, 0.f, 0.f};
+    v[q] = c < a.C ? ld4(a.h_in + (int64_t)src * a.C + c) : z;
+  }
+  if constexpr (NP >= 0) {
+    if constexpr (NP > 0) {
+      const float* pp = a.part + (int64_t)src * a.ldp;
+      float4_ t[NP][kLnVec];
+#pragma unroll
+      for (int u = 0; u < NP; ++u)
+#pragma unroll
+        for (int q = 0; q < kLnVec; ++q) {
+          const int c = t4 + 1024 * q;
+          t[u][q] = c < a.C ? ld4(pp + u * a.part_stride + c) : z;
+        }
+#pragma unroll
+      for (int u = 0; u < NP; ++u)
+#pragma unroll
+        for (int q = 0; q < kLnVec; ++q) v[q] += t[u][q];
+    }
+    return;
   }
   int p = 0;
   for (; p + 4 <= a.n_part; p += 4) {
@@ -101,7 +120,7 @@ __device__ inline void ln_load_row(const LnMixArgs& a, int src, float4_* v) {
 #pragma unroll
       for (int q = 0; q < kLnVec; ++q) {
         const int c = t4 + 1024 * q;
-        t[u][q] = c < a.C ? ld4(pp + u * a.part_stride + c) : (float4_){0.f, 0.f, 0.f, 0.f};
+        t[u][q] = c < a.C ? ld4(pp + u * a.part_stride + c) : z;
       }
 #pragma unroll
     for (int u = 0; u < 4; ++u)
@@ -161,7 +180,7 @@ __device__ inline void store_split4(const float4_& x, bf16_t* hi, bf16_t* lo, in
   *(uint2*)(lo + idx) = make_uint2(l[0] | ((uint32_t)l[1] << 16), l[2] | ((uint32_t)l[3] << 16));
 }
 
-template <int kLnVec>  // C <= 1024 * kLnVec
+template <int kLnVec, int NP>  // C <= 1024 * kLnVec; NP: partial slabs (-1: runtime a.n_part)
 __global__ __launch_bounds__(256) void k_ln_mix(LnMixArgs a) {
   __shared__ float red[16];
   const int out_row = blockIdx.x;
@@ -185,7 +204,7 @@ __global__ __launch_bounds__(256) void k_ln_mix(LnMixArgs a) {
 #pragma unroll
     for (int m = 0; m < 6; ++m) mu[m][q] = (ok && m < a.n_mix && a.mu[m]) ? ld4(a.mu[m] + c) : z;
   }
-  ln_load_row<kLnVec>(a, row, v);
+  ln_load_row<kLnVec, NP>(a, row, v);
   if (a.h_out) {
 #pragma unroll
     for (int q = 0; q < kLnVec; ++q) {
@@ -203,7 +222,7 @@ __global__ __launch_bounds__(256) void k_ln_mix(LnMixArgs a) {
     return;
   }
   if (prev_row >= 0) {  // prefill row: the previous token's LN output, recomputed identically
-    ln_load_row<kLnVec>(a, prev_row, pv);
+    ln_load_row<kLnVec, NP>(a, prev_row, pv);
     ln_apply<kLnVec>(a, w, b, pv, red, 2);
   }
 #pragma unroll
@@ -264,13 +283,17 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
   const int split = blockIdx.y;
   const int kbeg = split * KS;
   const int row0 = blockIdx.z * ROWS;
-  // 1) weight stream for this wave's 16 columns
-  int n = col0 + li;
-  if (n >= sg.N) n = sg.N - 1;
-  const bf16_t* wrow = sg.W + (int64_t)n * a.K + kbeg + g * 8;
+  // 1) weight stream for this wave's 16 columns: W is pre-packed in MFMA fragment order
+  // (launch_pack_frag), so each load instruction reads one contiguous 1 KB block and the
+  // wave's KSTEPS blocks are consecutive
+  int nb = col0 >> 4;
+  const int nblk = (sg.N + 15) >> 4;
+  if (nb >= nblk) nb = nblk - 1;
+  const bf16_t* wp = sg.W + (((int64_t)nb * (a.K >> 5) + (kbeg >> 5)) * 64 + lane) * 8;
   short8 b[KSTEPS];
 #pragma unroll
-  for (int t = 0; t < KSTEPS; ++t) b[t] = __builtin_nontemporal_load((const short8*)(wrow + t * 32));
+  for (int t = 0; t < KSTEPS; ++t)
+    b[t] = (a.exp & 2) ? (short8){0, 0, 0, 0, 0, 0, 0, 0} : __builtin_nontemporal_load((const short8*)(wp + t * 512));
   // 2) stage X slice
   constexpr int CH = KS / 8;  // 16-byte chunks per row
   if constexpr (XMODE == kXPlanes) {
@@ -282,7 +305,7 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
       const int r = c / CH, k8 = (c % CH) * 8;
       const int src = row0 + r;
       vh[u] = vl[u] = (short8){0, 0, 0, 0, 0, 0, 0, 0};
-      if (src < a.M) {
+      if (src < a.M && !(a.exp & 1)) {
         const int64_t o = (int64_t)src * sg.ldx + kbeg + k8;
         vh[u] = *(const short8*)(sg.Xhi + o);
         vl[u] = *(const short8*)(sg.Xlo + o);
@@ -309,7 +332,7 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
           const int c = threadIdx.x + u * 256;
           const int r = c / (KS / 4), k4 = (c % (KS / 4)) * 4;
           const int src = row0 + r;
-          t[pp][u] = (src < a.M && p0 + pp < a.x_nsplit)
+          t[pp][u] = (src < a.M && p0 + pp < a.x_nsplit && !(a.exp & 1))
                          ? *(const float4_*)(a.x_part + (p0 + pp) * a.x_part_stride + (int64_t)src * a.x_ld + kbeg + k4)
                          : (float4_){0.f, 0.f, 0.f, 0.f};
         }
@@ -585,8 +608,16 @@ void launch_ln_mix(const LnMixArgs& a, int n_out_rows, hipStream_t st) {
   LnMixArgs b = a;
   b.n_rows = n_out_rows;
   const dim3 grid(n_out_rows);
-  if (a.C <= 1024) hipLaunchKernelGGL(k_ln_mix<1>, grid, dim3(256), 0, st, b);
-  else hipLaunchKernelGGL(k_ln_mix<2>, grid, dim3(256), 0, st, b);
+  if (a.C <= 1024) {
+    switch (a.n_part) {  // slab counts of the 0.4B configuration: every load in flight at once
+      case 0: hipLaunchKernelGGL((k_ln_mix<1, 0>), grid, dim3(256), 0, st, b); break;
+      case 8: hipLaunchKernelGGL((k_ln_mix<1, 8>), grid, dim3(256), 0, st, b); break;
+      case 16: hipLaunchKernelGGL((k_ln_mix<1, 16>), grid, dim3(256), 0, st, b); break;
+      default: hipLaunchKernelGGL((k_ln_mix<1, -1>), grid, dim3(256), 0, st, b); break;
+    }
+  } else {
+    hipLaunchKernelGGL((k_ln_mix<2, -1>), grid, dim3(256), 0, st, b);
+  }
 }
 
 template <int MT, int KSTEPS>
@@ -622,6 +653,24 @@ void launch_gemm(const GemmArgs& a, hipStream_t st) {
   }
 #undef GEMM_CASE
 }
+// W [N][K] -> MFMA B-fragment blocks: block (nb, kb) = 16 columns x 32 k = 1 KB, lane
+// l = 16 g + li holding W[16 nb + li][32 kb + 8 g .. + 8]; blocks ordered nb-major. Rows >= N are 0.
+__global__ void k_pack_frag(const bf16_t* W, int N, int K, bf16_t* out) {
+  const int64_t nblk = (N + 15) / 16, total = nblk * 16 * K;
+  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int e = (int)(idx & 7), lane = (int)((idx >> 3) & 63);
+    const int64_t blk = idx >> 9;
+    const int kb = (int)(blk % (K / 32)), nb = (int)(blk / (K / 32));
+    const int n = nb * 16 + (lane & 15), k = kb * 32 + (lane >> 4) * 8 + e;
+    out[idx] = n < N ? W[(int64_t)n * K + k] : (bf16_t)0;
+  }
+}
+
+void launch_pack_frag(const bf16_t* W, int N, int K, bf16_t* out, hipStream_t st) {
+  hipLaunchKernelGGL(k_pack_frag, dim3(4096), dim3(256), 0, st, W, N, K, out);
+}
+
 __global__ void k_pack_lora(const bf16_t* w2t, const bf16_t* a2t, const bf16_t* v2t, const bf16_t* g2t, int C,
                             int Dw, int Da, int Dv, int Dg, bf16_t* out) {
   const int Dall = Dw + Da + Dv + Dg, eq = Dall / 4;

@@ -8,7 +8,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "librwkvtts.so")
+# RWKVTTS_LIB: an alternative build of the same library (A/B timing tools only)
+LIB_PATH = os.environ.get("RWKVTTS_LIB") or os.path.join(_HERE, "librwkvtts.so")
 
 EOS_TOKEN = 8192
 TAG_0, TAG_1, TAG_2 = 8193, 8194, 8195

@@ -23,6 +23,6 @@ for name, nwg, s in (("rkv_lora", 53 * 4, st[0]), ("ffn_value", 16 * 16, st[1]))
     s = s[:nwg]
     d = np.diff(s, axis=1)
     print(f"{name}: per-WG median total {np.median(s[:,3]-s[:,0]):.0f} cyc; phases "
-          f"stage {np.median(d[:,0]):.0f} / mfma(+W wait) {np.median(d[:,1]):.0f} / store {np.median(d[:,2]):.0f}; "
+          f"{' / '.join(f'{np.median(d[:,i]):.0f}' for i in range(3))}; "
           f"p90 total {np.percentile(s[:,3]-s[:,0], 90):.0f}; start spread {s[:,0].max()-s[:,0].min()} "
           f"span {s[:,3].max()-s[:,0].min()}")
