@@ -65,7 +65,31 @@ __host__ __device__ inline float f16_to_f32(uint16_t h) {
 __device__ inline float h16_to_f32(uint16_t h) { return (float)__builtin_bit_cast(_Float16, h); }
 __device__ inline uint16_t f32_to_h16(float x) { return __builtin_bit_cast(uint16_t, (_Float16)x); }
 __device__ inline float w16_to_f32(uint16_t v, bool f16) { return f16 ? h16_to_f32(v) : bf16_to_f32(v); }
-__device__ inline uint16_t f32_to_w16(float x, bool f16) { return f16 ? f32_to_h16(x) : f32_to_bf16(x); }
+// device f32 -> bf16 by the hardware converter (v_cvt_pk_bf16_f32, round-to-nearest-even: the
+// same bits as f32_to_bf16 for every finite input)
+__device__ inline uint16_t f32_to_bf16_hw(float x) { return __builtin_bit_cast(uint16_t, (__bf16)x); }
+__device__ inline uint16_t f32_to_w16(float x, bool f16) { return f16 ? f32_to_h16(x) : f32_to_bf16_hw(x); }
+
+// x = hi + lo split of two floats into packed 16-bit pairs (hi = RNE(x), lo = RNE(x - hi)):
+// one packed convert per plane.
+typedef float float2_ __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_ __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2_ __attribute__((ext_vector_type(2)));
+template <bool F16>
+__device__ inline void split2(float a, float b, uint32_t& hi, uint32_t& lo) {
+  if constexpr (F16) {
+    const f16x2_ h = __builtin_convertvector((float2_){a, b}, f16x2_);
+    const float2_ hf = __builtin_convertvector(h, float2_);
+    hi = __builtin_bit_cast(uint32_t, h);
+    lo = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_){a, b} - hf, f16x2_));
+  } else {
+    const bf16x2_ h = __builtin_convertvector((float2_){a, b}, bf16x2_);
+    const uint32_t hb = __builtin_bit_cast(uint32_t, h);
+    const float2_ hf = {__builtin_bit_cast(float, hb << 16), __builtin_bit_cast(float, hb & 0xFFFF0000u)};
+    hi = hb;
+    lo = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_){a, b} - hf, bf16x2_));
+  }
+}
 
 inline int64_t align_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
 

@@ -84,6 +84,7 @@ struct WkvArgs {
   const int4* segs;    // slot, row_begin, n_rows, _
   int layer, C, Dw, Da, Dv, Dg;
   int n_slots;         // state slots (bounds the speculative slot = segment index)
+  int n_seg;           // segments in this step (k_wkv3 groups SG segments per workgroup)
   int f16;             // fp16 model: LoRA-up rows and the z planes are f16
   uint64_t* stamps;    // debug: 8 s_memtime stamps per workgroup (null in production)
   int exp;             // debug experiment bits (0 in production)

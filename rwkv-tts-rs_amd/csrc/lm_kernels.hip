@@ -251,6 +251,77 @@ __global__ __launch_bounds__(256) void k_ln_mix(LnMixArgs a) {
 }
 
 // ------------------------------------------------------------------------------------
+// ln1024: k_ln_mix for C = 1024 with the weight format, the mix count and the partial-slab count
+// as template parameters (no per-element guards, no runtime format select, packed hardware
+// bf16/f16 conversion of the hi/lo planes). MODE 1: LN + NMIX token-shift mixes + shift update;
+// MODE 0: ln_out (x = LN(h) planes only). Loads that need only the row (residual, slabs, LN and
+// mix vectors) are issued before the row descriptor that addresses the shift state.
+// ------------------------------------------------------------------------------------
+template <bool F16, int MODE, int NMIX, int NP>
+__global__ __launch_bounds__(256) void k_ln1024(LnMixArgs a) {
+  constexpr int C = 1024;
+  __shared__ float red[16];
+  const int out_row = blockIdx.x;
+  const int row = a.row_map ? a.row_map[out_row] : out_row;
+  const int c = 4 * threadIdx.x;
+  float4_ v = ld4(a.h_in + (int64_t)row * C + c);
+  float4_ t[NP > 0 ? NP : 1];
+#pragma unroll
+  for (int p = 0; p < NP; ++p) t[p] = ld4(a.part + p * a.part_stride + (int64_t)row * a.ldp + c);
+  const float4_ w = ld4(a.ln_w + c), b = ld4(a.ln_b + c);
+  float4_ mu[NMIX > 0 ? NMIX : 1];
+#pragma unroll
+  for (int m = 0; m < NMIX; ++m) mu[m] = ld4(a.mu[m] + c);
+  int slot = 0, flags = 0, prev_row = -1, par = 0;
+  float4_ pv = {0.f, 0.f, 0.f, 0.f};
+  const float* sh = nullptr;
+  if constexpr (MODE == 1) {
+    const int4 info = a.rows[row];
+    slot = info.x; flags = info.y; prev_row = info.z; par = info.w;
+    sh = a.shift + (((int64_t)par * a.S + slot) * a.L + a.layer) * C;
+    if (prev_row < 0) pv = ld4(sh + c);
+  }
+#pragma unroll
+  for (int p = 0; p < NP; ++p) v += t[p];
+  if (a.h_out) *(float4_*)(a.h_out + (int64_t)row * C + c) = v;
+  auto ln = [&](float4_& x, int slot_base) {
+    const float mean = block_sum_1b((x[0] + x[1]) + (x[2] + x[3]), red, slot_base) * (1.0f / C);
+    const float4_ d = x - mean;
+    const float var = block_sum_1b((d[0] * d[0] + d[1] * d[1]) + (d[2] * d[2] + d[3] * d[3]), red, slot_base + 1) * (1.0f / C);
+    const float rstd = 1.0f / sqrtf(var + 1e-5f);
+    x = d * rstd * w + b;
+  };
+  ln(v, 0);
+  auto store = [&](const float4_& x, bf16_t* hi, bf16_t* lo, int64_t idx) {
+    uint32_t h0, l0, h1, l1;
+    split2<F16>(x[0], x[1], h0, l0);
+    split2<F16>(x[2], x[3], h1, l1);
+    *(uint2*)(hi + idx) = make_uint2(h0, h1);
+    *(uint2*)(lo + idx) = make_uint2(l0, l1);
+  };
+  if constexpr (MODE == 0) {
+    store(v, a.x_hi, a.x_lo, (int64_t)out_row * a.ldx + c);
+    return;
+  } else {
+    if (prev_row >= 0) {  // prefill row: the previous token's LN output, recomputed identically
+      pv = ld4(a.h_in + (int64_t)prev_row * C + c);
+      float4_ tp[NP > 0 ? NP : 1];
+#pragma unroll
+      for (int p = 0; p < NP; ++p) tp[p] = ld4(a.part + p * a.part_stride + (int64_t)prev_row * a.ldp + c);
+#pragma unroll
+      for (int p = 0; p < NP; ++p) pv += tp[p];
+      ln(pv, 2);
+    }
+#pragma unroll
+    for (int m = 0; m < NMIX; ++m) {
+      const float4_ x = v + (pv - v) * mu[m];
+      store(x, a.x_hi + m * a.mix_stride, a.x_lo + m * a.mix_stride, (int64_t)out_row * a.ldx + c);
+    }
+    if (flags & kRowLast) *(float4_*)(a.shift + (((int64_t)(par ^ 1) * a.S + slot) * a.L + a.layer) * C + c) = v;
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // gemm: out[split][row][col_off + n] = sum_{k in split} X[row][k] * W[n][k]
 //   W bf16 [N][K] row-major; X as bf16 hi/lo planes (or, mode kXRelu2, relu(sum of f32
 //   partial slabs)^2 split on the fly). MFMA 16x16x32 bf16.
@@ -608,6 +679,23 @@ void launch_ln_mix(const LnMixArgs& a, int n_out_rows, hipStream_t st) {
   LnMixArgs b = a;
   b.n_rows = n_out_rows;
   const dim3 grid(n_out_rows);
+  static const bool fast = !getenv("RWKVTTS_LN_OLD");
+  if (fast && a.C == 1024 && (a.shift ? (a.n_mix == 6 || a.n_mix == 1) : true) &&
+      (a.n_part == 0 || a.n_part == 8 || a.n_part == 16)) {
+#define LN_CASE(F, MO, NM)                                                                                  \
+  switch (a.n_part) {                                                                                      \
+    case 0: hipLaunchKernelGGL((k_ln1024<F, MO, NM, 0>), grid, dim3(256), 0, st, b); break;                \
+    case 8: hipLaunchKernelGGL((k_ln1024<F, MO, NM, 8>), grid, dim3(256), 0, st, b); break;                \
+    default: hipLaunchKernelGGL((k_ln1024<F, MO, NM, 16>), grid, dim3(256), 0, st, b); break;              \
+  }
+    if (a.f16) {
+      if (!a.shift) { LN_CASE(true, 0, 0) } else if (a.n_mix == 6) { LN_CASE(true, 1, 6) } else { LN_CASE(true, 1, 1) }
+    } else {
+      if (!a.shift) { LN_CASE(false, 0, 0) } else if (a.n_mix == 6) { LN_CASE(false, 1, 6) } else { LN_CASE(false, 1, 1) }
+    }
+#undef LN_CASE
+    return;
+  }
   if (a.C <= 1024) {
     switch (a.n_part) {  // slab counts of the 0.4B configuration: every load in flight at once
       case 0: hipLaunchKernelGGL((k_ln_mix<1, 0>), grid, dim3(256), 0, st, b); break;
@@ -882,10 +970,443 @@ __global__ __launch_bounds__(128) void k_wkv2(WkvArgs a) {
   if (stp) stp[5] = __builtin_amdgcn_s_memtime();
 }
 
+// ------------------------------------------------------------------------------------
+// wkv3: k_wkv2's per-(segment, head) arithmetic, SG segments per workgroup (128 threads each).
+// The head's LoRA-up rows (64 channels x (Dw+Da+Dv+Dg) bf16, 36 KB at the 0.4B dims) are staged
+// in LDS once per workgroup and shared by its SG segments, which divides the L2 -> CU traffic
+// of these rows (re-read by every slot in k_wkv2) by SG. Barriers are workgroup-wide; groups
+// whose segment has fewer rows (prefill) idle through the extra iterations.
+// ------------------------------------------------------------------------------------
+template <int DW, int DA, int DV, int DG, int MAXP, int SG>
+__global__ __launch_bounds__(128 * SG) void k_wkv3(WkvArgs a) {
+  constexpr int N = 64, DALL = DW + DA + DV + DG;
+  constexpr int LWS = DALL + 8;  // LDS row stride (bf16): +16 B spreads the channel rows over banks
+  __shared__ __attribute__((aligned(16))) bf16_t s_lw[N * LWS];
+  __shared__ __attribute__((aligned(16))) float s_hid[SG][DALL];
+  __shared__ __attribute__((aligned(16))) float s_vec[SG][5][N];  // w, kk (unnormalised), a, k, r
+  __shared__ float s_red[SG][4][2];
+  const int tid = threadIdx.x, grp = tid >> 7, t = tid & 127;
+  const int lane = t & 63, wave = t >> 6, i = t >> 1, hf = t & 1;
+  const int h = blockIdx.y, C = a.C, c = h * N + i;
+  const int segi = blockIdx.x * SG + grp;
+  const bool active = segi < a.n_seg;
+  const int4 sg = a.segs[active ? segi : 0];
+  // ---- head-only loads: this workgroup's share of the LoRA-up rows (16-B pieces) + parameters
+  constexpr int PW = DW / 8, PA = DA / 8, PV = DV / 8, PG = DG / 8, PC = PW + PA + PV + PG;  // pieces/channel
+  constexpr int NPIECE = N * PC, PPT = (NPIECE + 128 * SG - 1) / (128 * SG);
+  short8 lw[PPT];
+#pragma unroll
+  for (int u = 0; u < PPT; ++u) {
+    const int q = tid + u * 128 * SG;
+    const int ch = q / PC, pc = q - ch * PC;
+    const int cc = h * N + ch;
+    const bf16_t* src;
+    if (pc < PW) src = a.w2t + (int64_t)cc * DW + pc * 8;
+    else if (pc < PW + PA) src = a.a2t + (int64_t)cc * DA + (pc - PW) * 8;
+    else if (pc < PW + PA + PV) src = a.v2t + (int64_t)cc * DV + (pc - PW - PA) * 8;
+    else src = a.g2t + (int64_t)cc * DG + (pc - PW - PA - PV) * 8;
+    lw[u] = (q < NPIECE && !(a.exp & 32)) ? *(const short8*)src : (short8){0, 0, 0, 0, 0, 0, 0, 0};
+  }
+  const float w0 = a.w0[c], a0 = a.a0[c], v0 = a.v0[c], kkc = a.k_k[c], kac = a.k_a[c];
+  const float rkc = a.r_k[c], lnw = a.lnx_w[c], lnb = a.lnx_b[c];
+  // ---- segment-dependent loads, issued speculatively for slot = row = segment index
+  const int spec = segi;
+  const int64_t soff = a.layer_off + (int64_t)h * N * N + i * N + hf * 32;
+  float S[32];
+  auto load_state = [&](int slot) {
+    const float* Sp = a.state + (int64_t)slot * a.slot_stride + soff;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float4_ v4 = (a.exp & 8) ? (float4_){0.f, 0.f, 0.f, 0.f} : *(const float4_*)(Sp + q * 4);
+      S[q * 4 + 0] = v4[0]; S[q * 4 + 1] = v4[1]; S[q * 4 + 2] = v4[2]; S[q * 4 + 3] = v4[3];
+    }
+  };
+  load_state(spec < a.n_slots ? spec : 0);
+  constexpr int HPL = (DALL + 127) / 128;
+  float hp[MAXP][HPL], rp[MAXP], kp[MAXP], vp[MAXP], vf = 0.f;
+  auto load_parts = [&](int row) {
+    const float* prow = a.part + (int64_t)row * a.ldp;
+#pragma unroll
+    for (int p = 0; p < MAXP; ++p) {
+      const bool on = p < a.n_part && !(a.exp & 16);
+      const float* pp = prow + p * a.part_stride;
+#pragma unroll
+      for (int e = 0; e < HPL; ++e) {
+        const int d = t + 128 * e;
+        hp[p][e] = (on && d < DALL) ? pp[3 * C + d] : 0.f;
+      }
+      rp[p] = on ? pp[c] : 0.f;
+      kp[p] = on ? pp[C + c] : 0.f;
+      vp[p] = on ? pp[2 * C + c] : 0.f;
+    }
+    vf = a.layer > 0 ? a.v_first[(int64_t)row * a.ldv + c] : 0.f;
+  };
+  const int spec_row = spec < a.n_slots ? spec : 0;
+  load_parts(spec_row);
+  // LoRA-up rows -> LDS (after the state/partials loads are in flight)
+#pragma unroll
+  for (int u = 0; u < PPT; ++u) {
+    const int q = tid + u * 128 * SG;
+    if (q < NPIECE) {
+      const int ch = q / PC, pc = q - ch * PC;
+      *(short8*)(s_lw + ch * LWS + pc * 8) = lw[u];
+    }
+  }
+  const int slot = sg.x, r_begin = sg.y, n_rows = active ? sg.z : 0;
+  float* Srow = a.state + (int64_t)slot * a.slot_stride + soff;
+  if (active && slot != spec_row) load_state(slot);
+  if (active && r_begin != spec_row) load_parts(r_begin);
+  int max_rows = 0;
+#pragma unroll
+  for (int g2 = 0; g2 < SG; ++g2) {
+    const int sj = blockIdx.x * SG + g2;
+    if (sj < a.n_seg) max_rows = max(max_rows, a.segs[sj].z);
+  }
+  float* hid = s_hid[grp];
+  float(*vec)[N] = s_vec[grp];
+  float(*red)[2] = s_red[grp];
+  const bf16_t* myw = s_lw + i * LWS;
+  for (int rr = 0; rr < max_rows; ++rr) {
+    const bool on = rr < n_rows;
+    const int row = r_begin + rr;
+    if (rr > 0 && on) load_parts(row);
+#pragma unroll
+    for (int e = 0; e < HPL; ++e) {
+      float x = 0.f;
+#pragma unroll
+      for (int p = 0; p < MAXP; ++p) x += hp[p][e];
+      const int d = t + 128 * e;
+      if (d < DALL) hid[d] = d < DW ? tanhf(x) : (d >= DW + DA + DV ? sigm(x) : x);
+    }
+    float r = 0.f, k = 0.f, v = 0.f;
+#pragma unroll
+    for (int p = 0; p < MAXP; ++p) {
+      r += rp[p];
+      k += kp[p];
+      v += vp[p];
+    }
+    __syncthreads();
+    // ---- LoRA up: this thread's half of channel c's four dot products (weights from LDS)
+    float lo0 = 0.f, lo1 = 0.f, lo2 = 0.f, lo3 = 0.f;
+    auto dot8 = [&](const bf16_t* wsrc, const float* hsrc) {
+      const short8 q = *(const short8*)wsrc;
+      const float4_ h0 = *(const float4_*)hsrc;
+      const float4_ h1 = *(const float4_*)(hsrc + 4);
+      float acc = 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc += w16_to_f32((uint16_t)q[e], a.f16 != 0) * h0[e];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc += w16_to_f32((uint16_t)q[4 + e], a.f16 != 0) * h1[e];
+      return acc;
+    };
+#pragma unroll
+    for (int u = 0; u < DW / 16; ++u) lo0 += dot8(myw + hf * (DW / 2) + u * 8, hid + hf * (DW / 2) + u * 8);
+#pragma unroll
+    for (int u = 0; u < DA / 16; ++u) lo1 += dot8(myw + DW + hf * (DA / 2) + u * 8, hid + DW + hf * (DA / 2) + u * 8);
+#pragma unroll
+    for (int u = 0; u < DV / 16; ++u)
+      lo2 += dot8(myw + DW + DA + hf * (DV / 2) + u * 8, hid + DW + DA + hf * (DV / 2) + u * 8);
+#pragma unroll
+    for (int u = 0; u < DG / 16; ++u)
+      lo3 += dot8(myw + DW + DA + DV + hf * (DG / 2) + u * 8, hid + DW + DA + DV + hf * (DG / 2) + u * 8);
+    lo0 += __shfl_xor(lo0, 1);
+    lo1 += __shfl_xor(lo1, 1);
+    lo2 += __shfl_xor(lo2, 1);
+    lo3 += __shfl_xor(lo3, 1);
+    const float w = expf(-0.60653066f * sigm(w0 + lo0));
+    const float av = sigm(a0 + lo1);
+    const float kk = k * kkc;
+    k = k * (1.0f + (av - 1.0f) * kac);
+    if (a.layer == 0) {
+      if (hf == 0 && on) a.v_first[(int64_t)row * a.ldv + c] = v;
+    } else {
+      v = v + (vf - v) * sigm(v0 + lo2);
+    }
+    {
+      const float ksq = wave_sum(hf == 0 ? kk * kk : 0.f);
+      const float bon = wave_sum(hf == 0 ? r * k * rkc : 0.f);
+      if (lane == 0) { red[0][wave] = ksq; red[1][wave] = bon; }
+    }
+    if (hf == 0) {
+      vec[0][i] = w; vec[1][i] = kk; vec[2][i] = av; vec[3][i] = k; vec[4][i] = r;
+    }
+    __syncthreads();
+    const float inv = 1.0f / fmaxf(sqrtf(red[0][0] + red[0][1]), 1e-12f);
+    const float bonus = red[1][0] + red[1][1];
+    const float* vj = &vec[0][hf * 32];
+    float sa = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float4_ kq = *(const float4_*)(vj + N + q * 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) sa += S[q * 4 + e] * (kq[e] * inv);
+    }
+    sa += __shfl_xor(sa, 1);
+    float y = 0.f;
+    float Sn[32];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float4_ wq = *(const float4_*)(vj + q * 4);
+      const float4_ kq = *(const float4_*)(vj + N + q * 4);
+      const float4_ aq = *(const float4_*)(vj + 2 * N + q * 4);
+      const float4_ k4 = *(const float4_*)(vj + 3 * N + q * 4);
+      const float4_ rq = *(const float4_*)(vj + 4 * N + q * 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float sv = S[q * 4 + e] * wq[e] - sa * ((kq[e] * inv) * aq[e]) + v * k4[e];
+        Sn[q * 4 + e] = sv;
+        y += sv * rq[e];
+      }
+    }
+    if (on) {
+#pragma unroll
+      for (int q = 0; q < 32; ++q) S[q] = Sn[q];
+      if (rr + 1 == n_rows && !(a.exp & 64)) {  // last row of the segment: the state is final, store it now
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          float4_ v4 = {S[q * 4 + 0], S[q * 4 + 1], S[q * 4 + 2], S[q * 4 + 3]};
+          *(float4_*)(Srow + q * 4) = v4;
+        }
+      }
+    }
+    y += __shfl_xor(y, 1);
+    {
+      const float s1 = wave_sum(hf == 0 ? y : 0.f);
+      const float s2 = wave_sum(hf == 0 ? y * y : 0.f);
+      if (lane == 0) { red[2][wave] = s1; red[3][wave] = s2; }
+    }
+    __syncthreads();
+    const float mean = (red[2][0] + red[2][1]) * (1.0f / N);
+    const float var = fmaxf((red[3][0] + red[3][1]) * (1.0f / N) - mean * mean, 0.f);
+    if (hf == 0 && on) {
+      const float gn = (y - mean) * (1.0f / sqrtf(var + 64e-5f)) * lnw + lnb;
+      split_store((gn + bonus * v) * lo3, a.z_hi, a.z_lo, (int64_t)row * a.ldz + c, a.f16 != 0);
+    }
+    if (rr + 1 < max_rows) __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// wkv4: the 0.4B shape (LoRA ranks 64/64/32/128, 4 split-K slabs) cut down to the instruction
+// stream the arithmetic needs. The decode WKV is VALU-issue-bound (one wave per SIMD, every
+// wave a straight ~2k-instruction program), so this variant removes work rather than adding
+// parallelism: the weight format is a template (no runtime f16/bf16 select), the LoRA hidden
+// is summed from float4 slab loads by 72 threads, LoRA-up dot products and the state update run
+// on packed f32 pairs (v_pk_fma_f32), sigmoid / tanh / exp use the hardware exp2 (|rel err|
+// ~1e-7, far inside the logits tolerance), and the slot / row speculation of k_wkv2 is kept.
+// Thread t = (channel i = t >> 1, half hf = t & 1) owns state row S[i][32 hf .. 32 hf + 31].
+// ------------------------------------------------------------------------------------
+__device__ inline float fexp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
+__device__ inline float fsigm(float x) { return __builtin_amdgcn_rcpf(1.0f + fexp(-x)); }
+__device__ inline float ftanh(float x) {
+  const float e = fexp(2.0f * fminf(fmaxf(x, -20.f), 20.f));
+  return 1.0f - 2.0f * __builtin_amdgcn_rcpf(e + 1.0f);
+}
+template <bool F16>
+__device__ inline float2_ w2f(uint32_t u) {  // two packed 16-bit weights -> f32 pair
+  if constexpr (F16) {
+    return (float2_){h16_to_f32((uint16_t)(u & 0xFFFFu)), h16_to_f32((uint16_t)(u >> 16))};
+  } else {
+    return (float2_){__builtin_bit_cast(float, u << 16), __builtin_bit_cast(float, u & 0xFFFF0000u)};
+  }
+}
+
+template <bool F16>
+__global__ __launch_bounds__(128) void k_wkv4(WkvArgs a) {
+  constexpr int N = 64, DW = 64, DA = 64, DV = 32, DG = 128, DALL = DW + DA + DV + DG, NP = 4;
+  __shared__ __attribute__((aligned(16))) float s_hid[DALL];
+  __shared__ __attribute__((aligned(16))) float s_vec[5][N];  // w, kk (unnormalised), a, k, r
+  __shared__ float s_red[4][2];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, i = t >> 1, hf = t & 1;
+  const int h = blockIdx.y, C = a.C, c = h * N + i;
+  const int4 sg = a.segs[blockIdx.x];
+  // ---- head-only loads: half of channel c's LoRA-up rows + parameters
+  uint4 lw[18];  // 8 bf16 per entry: w 0..3 | a 4..7 | v 8..9 | g 10..17
+  {
+    const uint4* pw = (const uint4*)(a.w2t + (int64_t)c * DW + hf * (DW / 2));
+    const uint4* pa = (const uint4*)(a.a2t + (int64_t)c * DA + hf * (DA / 2));
+    const uint4* pv = (const uint4*)(a.v2t + (int64_t)c * DV + hf * (DV / 2));
+    const uint4* pg = (const uint4*)(a.g2t + (int64_t)c * DG + hf * (DG / 2));
+#pragma unroll
+    for (int u = 0; u < 4; ++u) lw[u] = pw[u];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) lw[4 + u] = pa[u];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) lw[8 + u] = pv[u];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) lw[10 + u] = pg[u];
+  }
+  const float w0 = a.w0[c], a0 = a.a0[c], v0 = a.v0[c], kkc = a.k_k[c], kac = a.k_a[c];
+  const float rkc = a.r_k[c], lnw = a.lnx_w[c], lnb = a.lnx_b[c];
+  // ---- segment-dependent loads, speculated for slot = row = segment index (decode layout)
+  const int spec = blockIdx.x < a.n_slots ? blockIdx.x : 0;
+  const int64_t soff = a.layer_off + (int64_t)h * N * N + i * N + hf * 32;
+  float4_ S4[8];
+  auto load_state = [&](int slot) {
+    const float4_* Sp = (const float4_*)(a.state + (int64_t)slot * a.slot_stride + soff);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) S4[q] = Sp[q];
+  };
+  load_state(spec);
+  const bool hid_thread = t < DALL / 4;
+  float4_ hp[NP];
+  float rp[NP], kp[NP], vp[NP], vf = 0.f;
+  auto load_parts = [&](int row) {
+    const float* prow = a.part + (int64_t)row * a.ldp;
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const float* pp = prow + p * a.part_stride;
+      hp[p] = *(const float4_*)(pp + 3 * C + (hid_thread ? 4 * t : 0));
+      rp[p] = pp[c];
+      kp[p] = pp[C + c];
+      vp[p] = pp[2 * C + c];
+    }
+    vf = a.layer > 0 ? a.v_first[(int64_t)row * a.ldv + c] : 0.f;
+  };
+  load_parts(spec);
+  const int slot = sg.x, r_begin = sg.y, n_rows = sg.z;
+  if (slot != spec) load_state(slot);
+  if (r_begin != spec) load_parts(r_begin);
+  float4_* Srow = (float4_*)(a.state + (int64_t)slot * a.slot_stride + soff);
+  for (int rr = 0; rr < n_rows; ++rr) {
+    const int row = r_begin + rr;
+    if (rr > 0) load_parts(row);
+    // LoRA hidden: threads 0..71 each own 4 consecutive entries (one region: w | a | v | g)
+    if (hid_thread) {
+      float4_ x = hp[0];
+#pragma unroll
+      for (int p = 1; p < NP; ++p) x += hp[p];
+      float4_ y;
+      if (t < DW / 4) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) y[e] = ftanh(x[e]);
+      } else if (t < (DW + DA + DV) / 4) {
+        y = x;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) y[e] = fsigm(x[e]);
+      }
+      *(float4_*)(s_hid + 4 * t) = y;
+    }
+    float r = rp[0], k = kp[0], v = vp[0];
+#pragma unroll
+    for (int p = 1; p < NP; ++p) {
+      r += rp[p];
+      k += kp[p];
+      v += vp[p];
+    }
+    __syncthreads();
+    // ---- LoRA up on packed pairs: this thread's half of channel c's four dot products
+    float2_ l0 = {0.f, 0.f}, l1 = {0.f, 0.f}, l2 = {0.f, 0.f}, l3 = {0.f, 0.f};
+    auto dot = [&](float2_ acc, const uint4 q, const float* hsrc) {
+      const float4_ h0 = *(const float4_*)hsrc;
+      const float4_ h1 = *(const float4_*)(hsrc + 4);
+      acc += w2f<F16>(q.x) * (float2_){h0[0], h0[1]};
+      acc += w2f<F16>(q.y) * (float2_){h0[2], h0[3]};
+      acc += w2f<F16>(q.z) * (float2_){h1[0], h1[1]};
+      acc += w2f<F16>(q.w) * (float2_){h1[2], h1[3]};
+      return acc;
+    };
+#pragma unroll
+    for (int u = 0; u < 4; ++u) l0 = dot(l0, lw[u], s_hid + hf * (DW / 2) + u * 8);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) l1 = dot(l1, lw[4 + u], s_hid + DW + hf * (DA / 2) + u * 8);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) l2 = dot(l2, lw[8 + u], s_hid + DW + DA + hf * (DV / 2) + u * 8);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) l3 = dot(l3, lw[10 + u], s_hid + DW + DA + DV + hf * (DG / 2) + u * 8);
+    float lo0 = l0[0] + l0[1], lo1 = l1[0] + l1[1], lo2 = l2[0] + l2[1], lo3 = l3[0] + l3[1];
+    lo0 += __shfl_xor(lo0, 1);
+    lo1 += __shfl_xor(lo1, 1);
+    lo2 += __shfl_xor(lo2, 1);
+    lo3 += __shfl_xor(lo3, 1);
+    // ---- channel mixing terms (both threads of the pair compute channel c)
+    const float w = fexp(-0.60653066f * fsigm(w0 + lo0));
+    const float av = fsigm(a0 + lo1);
+    const float kk = k * kkc;
+    k = k * (1.0f + (av - 1.0f) * kac);
+    if (a.layer == 0) {
+      if (hf == 0) a.v_first[(int64_t)row * a.ldv + c] = v;
+    } else {
+      v = v + (vf - v) * fsigm(v0 + lo2);
+    }
+    {
+      const float ksq = wave_sum(hf == 0 ? kk * kk : 0.f);
+      const float bon = wave_sum(hf == 0 ? r * k * rkc : 0.f);
+      if (lane == 0) { s_red[0][wave] = ksq; s_red[1][wave] = bon; }
+    }
+    if (hf == 0) {
+      s_vec[0][i] = w; s_vec[1][i] = kk; s_vec[2][i] = av; s_vec[3][i] = k; s_vec[4][i] = r;
+    }
+    __syncthreads();
+    const float inv = __builtin_amdgcn_rcpf(fmaxf(sqrtf(s_red[0][0] + s_red[0][1]), 1e-12f));
+    const float bonus = s_red[1][0] + s_red[1][1];
+    // ---- state half-row update on packed pairs: S = S*w - sa*(kk*inv*a) + v*k ; y = S.r
+    const float* vj = &s_vec[0][hf * 32];
+    float2_ sa2 = {0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float4_ kq = *(const float4_*)(vj + N + q * 4);
+      sa2 += (float2_){S4[q][0], S4[q][1]} * (float2_){kq[0], kq[1]};
+      sa2 += (float2_){S4[q][2], S4[q][3]} * (float2_){kq[2], kq[3]};
+    }
+    float sa = (sa2[0] + sa2[1]) * inv;
+    sa += __shfl_xor(sa, 1);
+    float2_ y2 = {0.f, 0.f};
+    const float2_ sav = {sa * inv, sa * inv}, vv = {v, v};
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float4_ wq = *(const float4_*)(vj + q * 4);
+      const float4_ kq = *(const float4_*)(vj + N + q * 4);
+      const float4_ aq = *(const float4_*)(vj + 2 * N + q * 4);
+      const float4_ k4 = *(const float4_*)(vj + 3 * N + q * 4);
+      const float4_ rq = *(const float4_*)(vj + 4 * N + q * 4);
+#pragma unroll
+      for (int e = 0; e < 4; e += 2) {
+        float2_ sv = (float2_){S4[q][e], S4[q][e + 1]} * (float2_){wq[e], wq[e + 1]};
+        sv -= sav * ((float2_){kq[e], kq[e + 1]} * (float2_){aq[e], aq[e + 1]});
+        sv += vv * (float2_){k4[e], k4[e + 1]};
+        S4[q][e] = sv[0];
+        S4[q][e + 1] = sv[1];
+        y2 += sv * (float2_){rq[e], rq[e + 1]};
+      }
+    }
+    if (rr + 1 == n_rows) {  // the segment's final state: stored before the GroupNorm tail
+#pragma unroll
+      for (int q = 0; q < 8; ++q) Srow[q] = S4[q];
+    }
+    float y = y2[0] + y2[1];
+    y += __shfl_xor(y, 1);
+    {
+      const float s1 = wave_sum(hf == 0 ? y : 0.f);
+      const float s2 = wave_sum(hf == 0 ? y * y : 0.f);
+      if (lane == 0) { s_red[2][wave] = s1; s_red[3][wave] = s2; }
+    }
+    __syncthreads();
+    const float mean = (s_red[2][0] + s_red[2][1]) * (1.0f / N);
+    const float var = fmaxf((s_red[3][0] + s_red[3][1]) * (1.0f / N) - mean * mean, 0.f);
+    if (hf == 0) {
+      const float gn = (y - mean) * __builtin_amdgcn_rsqf(var + 64e-5f) * lnw + lnb;
+      split_store((gn + bonus * v) * lo3, a.z_hi, a.z_lo, (int64_t)row * a.ldz + c, F16);
+    }
+    if (rr + 1 < n_rows) __syncthreads();
+  }
+}
+
 void launch_wkv(const WkvArgs& a, int n_seg, int H, hipStream_t st) {
   const dim3 grid(n_seg, H);
   if (a.Dw == 64 && a.Da == 64 && a.Dv == 32 && a.Dg == 128 && a.n_part <= 4 && !getenv("RWKVTTS_WKV_OLD")) {
-    hipLaunchKernelGGL((k_wkv2<64, 64, 32, 128, 4>), grid, dim3(128), 0, st, a);
+    static const int sgw = getenv("RWKVTTS_WKV_SG") ? atoi(getenv("RWKVTTS_WKV_SG")) : 0;
+    if (sgw == 0 && a.n_part == 4) {
+      if (a.f16) hipLaunchKernelGGL((k_wkv4<true>), grid, dim3(128), 0, st, a);
+      else hipLaunchKernelGGL((k_wkv4<false>), grid, dim3(128), 0, st, a);
+    } else if (sgw == 2) {
+      hipLaunchKernelGGL((k_wkv3<64, 64, 32, 128, 4, 2>), dim3((n_seg + 1) / 2, H), dim3(256), 0, st, a);
+    } else if (sgw == 4) {
+      hipLaunchKernelGGL((k_wkv3<64, 64, 32, 128, 4, 4>), dim3((n_seg + 3) / 4, H), dim3(512), 0, st, a);
+    } else {
+      hipLaunchKernelGGL((k_wkv2<64, 64, 32, 128, 4>), grid, dim3(128), 0, st, a);
+    }
     return;
   }
   if (a.Dw == 16 && a.Da == 16 && a.Dv == 16 && a.Dg == 32 && a.n_part <= 1 && !getenv("RWKVTTS_WKV_OLD")) {

@@ -22,6 +22,11 @@ DIMS_TINY = dict(n_layer=2, n_embd=128, head_size=64, n_ffn=512, n_vocab=77923,
 DIMS_SMALL = dict(n_layer=4, n_embd=256, head_size=64, n_ffn=1024, n_vocab=77923,
                   d_decay=32, d_aaa=32, d_mv=16, d_gate=64)
 
+# two layers at the full 0.4B widths: exercises the 0.4B-specialised decode kernels against the
+# oracle at a cost the CPU restatement finishes in seconds
+DIMS_MID = dict(n_layer=2, n_embd=1024, head_size=64, n_ffn=4096, n_vocab=77923,
+                d_decay=64, d_aaa=64, d_mv=32, d_gate=128)
+
 G_EMB, G_LN0_W, G_LN0_B, G_LNOUT_W, G_LNOUT_B, G_HEAD, G_COUNT = range(7)
 (L_LN1_W, L_LN1_B, L_LN2_W, L_LN2_B, L_XR, L_XW, L_XK, L_XV, L_XA, L_XG, L_W0, L_A0, L_V0, L_KK,
  L_KA, L_RK, L_LNX_W, L_LNX_B, L_FFN_XK, L_WR, L_WK, L_WV, L_WO, L_W1T, L_A1T, L_V1T, L_G1T,

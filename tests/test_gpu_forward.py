@@ -14,9 +14,9 @@ pytestmark = pytest.mark.gpu
 LOGIT_ATOL = 2e-3
 
 
-@pytest.fixture(scope="module", params=["tiny", "small", "tiny_f16", "small_f16"])
+@pytest.fixture(scope="module", params=["tiny", "small", "mid", "tiny_f16", "small_f16", "mid_f16"])
 def models(request):
-    dims = W.DIMS_TINY if request.param.startswith("tiny") else W.DIMS_SMALL
+    dims = {"tiny": W.DIMS_TINY, "small": W.DIMS_SMALL, "mid": W.DIMS_MID}[request.param.split("_")[0]]
     dt = rwkvtts._ffi.DTYPE_F16 if request.param.endswith("f16") else rwkvtts._ffi.DTYPE_BF16
     blob = W.synth_blob(dims, seed=123, dtype=dt)
     import oracle

@@ -74,3 +74,21 @@ def test_zero_shot_with_raf_globals(setup):
     assert g == og == raf["global_tokens"]
     assert s == os_
     assert len(s) >= 18  # hard minimum ceil(10 * 1.8)
+
+
+@pytest.mark.parametrize("dt", ["bf16", "f16"])
+def test_mid_model_generation_matches_oracle(dt):
+    """Two layers at the full 0.4B widths: the 0.4B-specialised decode kernels (LoRA ranks
+    64/64/32/128, 4 split-K slabs, C = 1024) stay token-exact against the oracle."""
+    dtype = rwkvtts._ffi.DTYPE_F16 if dt == "f16" else rwkvtts._ffi.DTYPE_BF16
+    blob = W.synth_blob(W.DIMS_MID, seed=5, dtype=dtype)
+    import oracle
+    om = oracle.Model(blob)
+    rt = rwkvtts.SharedRwkvRuntime(blob, max_slots=4, token_chunk_size=128, use_graphs=True)
+    try:
+        reqs = [make_request(synth_text(400 + i), seed=600 + i, fixed=24) for i in range(3)]
+        got = rt.generate_batch(reqs)
+        for r, (g, s) in zip(reqs, got):
+            assert (g, s) == _oracle(om, r)
+    finally:
+        rt.close()
