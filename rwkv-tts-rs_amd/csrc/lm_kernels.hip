@@ -469,6 +469,144 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
 }
 
 // ------------------------------------------------------------------------------------
+// gemm2: k_gemm with a shorter critical path.
+//  * segment lookup without dependent scalar loads: every segment's fields are read in one
+//    round and the tile's segment is picked by selects;
+//  * the X slice (L2-resident activations) is requested BEFORE the weight stream, so staging X
+//    into LDS waits only for X (vmcnt counts in issue order) and overlaps the HBM weight
+//    latency; in kXRelu2 mode all NX key slabs are in flight at once;
+//  * hi and lo products accumulate in separate MFMA chains (2*MT independent accumulators).
+// ------------------------------------------------------------------------------------
+template <int MT, int KSTEPS, int XMODE, bool F16, int NX>
+__global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int KS = KSTEPS * 32;
+  constexpr int LD = KS + 8;
+  constexpr int ROWS = MT * 16;
+  bf16_t* xh = (bf16_t*)smem;
+  bf16_t* xl = xh + ROWS * LD;
+  const int tile = blockIdx.x;
+  int s = 0;
+#pragma unroll
+  for (int j = 1; j < 8; ++j) s += (j < a.nseg && tile >= a.seg[j].tile_start) ? 1 : 0;
+  const bf16_t* Wm = a.seg[0].W;
+  const bf16_t* Xhi = a.seg[0].Xhi;
+  const bf16_t* Xlo = a.seg[0].Xlo;
+  int ldx = a.seg[0].ldx, Nn = a.seg[0].N, col_off = a.seg[0].col_off, tstart = a.seg[0].tile_start;
+#pragma unroll
+  for (int j = 1; j < 8; ++j)
+    if (s == j) {
+      Wm = a.seg[j].W; Xhi = a.seg[j].Xhi; Xlo = a.seg[j].Xlo;
+      ldx = a.seg[j].ldx; Nn = a.seg[j].N; col_off = a.seg[j].col_off; tstart = a.seg[j].tile_start;
+    }
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int g = lane >> 4, li = lane & 15;
+  const int col0 = (tile - tstart) * 64 + wave * 16;
+  const int split = blockIdx.y;
+  const int kbeg = split * KS;
+  const int row0 = blockIdx.z * ROWS;
+  // 1) X slice requests
+  constexpr int CH = KS / 8;
+  constexpr int PERP = ROWS * CH / 256;        // kXPlanes: 16-byte chunks per thread per plane
+  constexpr int PERR = ROWS * KS / 4 / 256;    // kXRelu2: float4 chunks per thread per slab
+  short8 vh[XMODE == kXPlanes ? PERP : 1], vl[XMODE == kXPlanes ? PERP : 1];
+  float4_ xr[XMODE == kXPlanes ? 1 : NX][XMODE == kXPlanes ? 1 : PERR];
+  if constexpr (XMODE == kXPlanes) {
+#pragma unroll
+    for (int u = 0; u < PERP; ++u) {
+      const int c = threadIdx.x + u * 256;
+      const int r = c / CH, k8 = (c % CH) * 8;
+      const int src = min(row0 + r, a.M - 1);
+      const int64_t o = (int64_t)src * ldx + kbeg + k8;
+      vh[u] = *(const short8*)(Xhi + o);
+      vl[u] = *(const short8*)(Xlo + o);
+    }
+  } else {
+#pragma unroll
+    for (int p = 0; p < NX; ++p)
+#pragma unroll
+      for (int u = 0; u < PERR; ++u) {
+        const int c = threadIdx.x + u * 256;
+        const int r = c / (KS / 4), k4 = (c % (KS / 4)) * 4;
+        const int src = min(row0 + r, a.M - 1);
+        xr[p][u] = *(const float4_*)(a.x_part + p * a.x_part_stride + (int64_t)src * a.x_ld + kbeg + k4);
+      }
+  }
+  // 2) weight stream (packed fragment blocks, 1 KB per wave instruction)
+  int nb = col0 >> 4;
+  const int nblk = (Nn + 15) >> 4;
+  if (nb >= nblk) nb = nblk - 1;
+  const bf16_t* wp = Wm + (((int64_t)nb * (a.K >> 5) + (kbeg >> 5)) * 64 + lane) * 8;
+  short8 b[KSTEPS];
+#pragma unroll
+  for (int t = 0; t < KSTEPS; ++t) b[t] = __builtin_nontemporal_load((const short8*)(wp + t * 512));
+  // 3) X -> LDS (rows past M hold a copy of row M-1; their outputs are not stored)
+  if constexpr (XMODE == kXPlanes) {
+#pragma unroll
+    for (int u = 0; u < PERP; ++u) {
+      const int c = threadIdx.x + u * 256;
+      const int r = c / CH, k8 = (c % CH) * 8;
+      *(short8*)(xh + r * LD + k8) = vh[u];
+      *(short8*)(xl + r * LD + k8) = vl[u];
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < PERR; ++u) {
+      float4_ x = xr[0][u];
+#pragma unroll
+      for (int p = 1; p < NX; ++p) x += xr[p][u];
+      const int c = threadIdx.x + u * 256;
+      const int r = c / (KS / 4), k4 = (c % (KS / 4)) * 4;
+      float y[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) y[e] = x[e] > 0.f ? x[e] * x[e] : 0.f;
+      uint32_t h0, l0, h1, l1;
+      split2<F16>(y[0], y[1], h0, l0);
+      split2<F16>(y[2], y[3], h1, l1);
+      *(uint2*)(xh + r * LD + k4) = make_uint2(h0, h1);
+      *(uint2*)(xl + r * LD + k4) = make_uint2(l0, l1);
+    }
+  }
+  __syncthreads();
+  // 4) MFMA: hi and lo chains separate
+  float4_ acc_h[MT], acc_l[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) acc_h[m] = acc_l[m] = (float4_){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < KSTEPS; ++t) {
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const int o = (m * 16 + li) * LD + t * 32 + g * 8;
+      const short8 ah = *(const short8*)(xh + o);
+      const short8 al = *(const short8*)(xl + o);
+      if constexpr (F16) {
+        acc_h[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, ah), __builtin_bit_cast(f16x8, b[t]),
+                                                          acc_h[m], 0, 0, 0);
+        acc_l[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, al), __builtin_bit_cast(f16x8, b[t]),
+                                                          acc_l[m], 0, 0, 0);
+      } else {
+        acc_h[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ah), __builtin_bit_cast(bf16x8, b[t]),
+                                                           acc_h[m], 0, 0, 0);
+        acc_l[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, al), __builtin_bit_cast(bf16x8, b[t]),
+                                                           acc_l[m], 0, 0, 0);
+      }
+    }
+  }
+  // 5) store (D layout: col = lane&15, row = 4*(lane>>4) + j)
+  const int col = col0 + li;
+  if (col < Nn) {
+    float* out = a.out + split * a.split_stride + col_off + col;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = row0 + m * 16 + 4 * g + j;
+        if (row < a.M) out[(int64_t)row * a.ldo] = acc_h[m][j] + acc_l[m][j];
+      }
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // wkv: one workgroup per (slot segment, head); rows of the segment run in order.
 //   part columns: [0,C) r | [C,2C) k | [2C,3C) v | [3C, 3C+Dw) w-hidden | +Da a-hidden |
 //   +Dv v-hidden | +Dg g-hidden   (split-K partial slabs, summed in fixed order here)
@@ -711,6 +849,17 @@ void launch_ln_mix(const LnMixArgs& a, int n_out_rows, hipStream_t st) {
 template <int MT, int KSTEPS>
 static void launch_gemm_t(const GemmArgs& a, dim3 grid, hipStream_t st) {
   const size_t lds = (size_t)MT * 16 * (KSTEPS * 32 + 8) * 2 * 2;
+  static const bool v2 = !getenv("RWKVTTS_GEMM_OLD");
+  if (v2 && (a.xmode == kXPlanes || a.x_nsplit == 4) && a.stamps == nullptr && a.exp == 0) {
+    if (a.f16) {
+      if (a.xmode == kXPlanes) hipLaunchKernelGGL((k_gemm2<MT, KSTEPS, kXPlanes, true, 1>), grid, dim3(256), lds, st, a);
+      else hipLaunchKernelGGL((k_gemm2<MT, KSTEPS, kXRelu2, true, 4>), grid, dim3(256), lds, st, a);
+    } else {
+      if (a.xmode == kXPlanes) hipLaunchKernelGGL((k_gemm2<MT, KSTEPS, kXPlanes, false, 1>), grid, dim3(256), lds, st, a);
+      else hipLaunchKernelGGL((k_gemm2<MT, KSTEPS, kXRelu2, false, 4>), grid, dim3(256), lds, st, a);
+    }
+    return;
+  }
   if (a.f16) {
     if (a.xmode == kXPlanes) hipLaunchKernelGGL((k_gemm<MT, KSTEPS, kXPlanes, true>), grid, dim3(256), lds, st, a);
     else hipLaunchKernelGGL((k_gemm<MT, KSTEPS, kXRelu2, true>), grid, dim3(256), lds, st, a);
