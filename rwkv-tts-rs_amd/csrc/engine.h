@@ -31,6 +31,8 @@ struct StepPlan {
   bool advance = false;        // run the phase controller on the logits rows
 };
 
+constexpr int kLookahead = 8;  // decode steps queued per host poll of the control blocks
+
 struct ProfEntry {
   std::string name;
   int64_t launches = 0;

@@ -248,10 +248,6 @@ int Engine::slot_write(int slot, const float* in) {
 // ------------------------------------------------------------------------------------------
 // forward step
 // ------------------------------------------------------------------------------------------
-__global__ void k_prepare_tokens(const int4* rows, const SlotCtrl* ctrl, uint32_t* tok, int R) {
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r < R) tok[r] = (uint32_t)ctrl[rows[r].x].next_token;
-}
 __global__ void k_rows_parity(int4* rows, const int* slot_par, int R) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r < R) rows[r].w = slot_par[rows[r].x];
@@ -308,11 +304,13 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
   const int C = dims.n_embd, F = dims.n_ffn, Lc = dims.n_layer;
   hipEvent_t ev;
   const int nb = (R + 255) / 256;
-  hipLaunchKernelGGL(k_rows_parity, dim3(nb), dim3(256), 0, stream_, d_rows_, slot_par_, R);
-  if (tok_from_ctrl)
-    hipLaunchKernelGGL(k_prepare_tokens, dim3(nb), dim3(256), 0, stream_, d_rows_, d_ctrl_, d_tok_, R);
+  // decode steps (tokens from the control blocks, one row per slot) keep each slot's shift
+  // state in place: no parity refresh / flip kernels (rows[].w was set once at upload)
+  const bool inplace = tok_from_ctrl;
+  if (!inplace) hipLaunchKernelGGL(k_rows_parity, dim3(nb), dim3(256), 0, stream_, d_rows_, slot_par_, R);
   prof_begin(&ev);
-  launch_embed(d_tok_, emb_, ln0_w_, ln0_b_, h0_, R, C, f16_, stream_);
+  launch_embed(d_tok_, d_rows_, tok_from_ctrl ? &d_ctrl_[0].next_token : nullptr, (int)(sizeof(SlotCtrl) / 4), emb_,
+               ln0_w_, ln0_b_, h0_, R, C, f16_, stream_);
   prof_end("embed", ev);
   const int64_t RC = (int64_t)Rmax_ * C;
   for (int l = 0; l < Lc; ++l) {
@@ -341,6 +339,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     m.C = C;
     m.rows = d_rows_;
     m.row_map = nullptr;
+    m.inplace = inplace ? 1 : 0;
     prof_begin(&ev);
     if (!(dbg_exp_ & 0x10000)) launch_ln_mix(m, R, stream_);
     prof_end("ln_mix_att", ev);
@@ -482,7 +481,8 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
       prof_end("sample_advance", ev);
     }
   }
-  hipLaunchKernelGGL(k_flip_parity, dim3((n_seg + 255) / 256), dim3(256), 0, stream_, d_segs_, slot_par_, n_seg);
+  if (!inplace)
+    hipLaunchKernelGGL(k_flip_parity, dim3((n_seg + 255) / 256), dim3(256), 0, stream_, d_segs_, slot_par_, n_seg);
   RT_HIP(hipGetLastError());
   return RWKVTTS_OK;
 }
@@ -496,6 +496,8 @@ int Engine::upload_plan(const StepPlan& p) {
     RT_HIP(hipMemcpyAsync(d_lg_rows_, p.lg_rows.data(), p.lg_rows.size() * 4, hipMemcpyHostToDevice, stream_));
     RT_HIP(hipMemcpyAsync(d_lg_slot_, p.lg_slot.data(), p.lg_slot.size() * 4, hipMemcpyHostToDevice, stream_));
   }
+  if (p.tok_from_ctrl)  // decode steps keep the parity fixed: set rows[].w once here
+    hipLaunchKernelGGL(k_rows_parity, dim3((R + 255) / 256), dim3(256), 0, stream_, d_rows_, slot_par_, R);
   return RWKVTTS_OK;
 }
 
@@ -674,6 +676,15 @@ struct Active {
 };
 }  // namespace
 
+// semantic-step limit of a request, as set at admission (c.sem_limit)
+static int sem_limit_of(const rwkvtts_request& q) {
+  const bool zero_shot = q.ref_global != nullptr && q.ref_semantic != nullptr;
+  int limit = q.max_tokens > 0 ? std::min(q.max_tokens, RWKVTTS_SEMANTIC_LIMIT) : RWKVTTS_SEMANTIC_LIMIT;
+  if (q.fixed_semantic > 0) limit = std::min(q.fixed_semantic, RWKVTTS_SEMANTIC_LIMIT);
+  if (zero_shot) return q.fixed_semantic > 0 ? limit : RWKVTTS_SEMANTIC_LIMIT;
+  return limit;
+}
+
 int Engine::generate(const rwkvtts_request* reqs, int n, rwkvtts_result* res) {
   RT_HIP(hipSetDevice(device_));
   auto t_start = std::chrono::steady_clock::now();
@@ -807,21 +818,32 @@ int Engine::generate(const rwkvtts_request* reqs, int n, rwkvtts_result* res) {
     const int R = (int)p.rows.size();
     bool finished = false;
     while (!finished) {
-      // head rows: 4096 while every slot samples global tokens (or feeds g31), else 8193
-      bool all_global = true;
-      for (auto& a : act) all_global &= !a.zero_shot && a.advances <= RWKVTTS_N_GLOBAL;
-      p.head_rows = std::min(all_global ? 4096 : 8193, dims.n_vocab);
+      // Up to kLookahead decode steps are queued back to back before the host reads the control
+      // blocks: no slot can pass its step limit inside the window (EOS may end a request
+      // earlier: its slot then idles through the rest of the window, k_advance skips it).
+      int K = profiling ? 1 : kLookahead;
+      for (auto& a : act) {
+        const Active& aa = a;
+        const int total = aa.zero_shot ? sem_limit_of(reqs[aa.req]) : RWKVTTS_N_GLOBAL + 1 + sem_limit_of(reqs[aa.req]);
+        K = std::min(K, std::max(1, total - aa.advances));
+      }
       RT_HIP(hipEventRecord(e0, stream_));
-      RT_OK(run_step(p, false));
-      for (auto& a : act) a.advances++;
+      for (int k = 0; k < K; ++k) {
+        // head rows: 4096 while every slot samples global tokens (or feeds g31), else 8193
+        bool all_global = true;
+        for (auto& a : act) all_global &= !a.zero_shot && a.advances <= RWKVTTS_N_GLOBAL;
+        p.head_rows = std::min(all_global ? 4096 : 8193, dims.n_vocab);
+        RT_OK(run_step(p, false));
+        for (auto& a : act) a.advances++;
+      }
       RT_HIP(hipMemcpyAsync(h_ctrl_, d_ctrl_, sizeof(SlotCtrl) * S_, hipMemcpyDeviceToHost, stream_));
       RT_HIP(hipEventRecord(e1, stream_));
       RT_HIP(hipEventSynchronize(e1));
       float ms = 0;
       hipEventElapsedTime(&ms, e0, e1);
       decode_ms += ms;
-      stats.steps++;
-      stats.decode_rows += R;
+      stats.steps += K;
+      stats.decode_rows += (int64_t)R * K;
       RT_OK(flush_prof());
       for (auto& a : act) {
         if (h_ctrl_[a.slot].phase == kPhDone) finished = true;

@@ -33,6 +33,8 @@ struct LnMixArgs {
   const int* row_map;  // output row -> source row (ln_out) or null
   int n_rows;          // set by the launcher
   int f16;             // planes in f16 (fp16 model) instead of bf16
+  int inplace;         // decode step (one row per slot): the shift update overwrites the parity it
+                       // read (same thread, read before write) and the parity is not flipped
 };
 
 struct GemmSeg {
@@ -90,8 +92,9 @@ struct WkvArgs {
   int exp;             // debug experiment bits (0 in production)
 };
 
-void launch_embed(const uint32_t* tokens, const bf16_t* emb, const float* w, const float* b,
-                  float* h, int R, int C, int f16, hipStream_t st);
+// tokens: per-row ids, or (ctrl_tok != null, decode) row r's id = ctrl_tok[rows[r].x * ctrl_stride]
+void launch_embed(const uint32_t* tokens, const int4* rows, const int* ctrl_tok, int ctrl_stride,
+                  const bf16_t* emb, const float* w, const float* b, float* h, int R, int C, int f16, hipStream_t st);
 void launch_ln_mix(const LnMixArgs& a, int n_out_rows, hipStream_t st);
 void launch_gemm(const GemmArgs& a, hipStream_t st);
 void launch_wkv(const WkvArgs& a, int n_seg, int H, hipStream_t st);

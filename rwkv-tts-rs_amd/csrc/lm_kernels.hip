@@ -46,11 +46,12 @@ __device__ inline void split_store(float x, bf16_t* hi, bf16_t* lo, int64_t idx,
 // ------------------------------------------------------------------------------------
 // embed: h[r] = LN0(emb[token[r]])
 // ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_embed(const uint32_t* tokens, const bf16_t* emb,
-                                               const float* w, const float* b, float* h, int C, int f16) {
+__global__ __launch_bounds__(256) void k_embed(const uint32_t* tokens, const int4* rows, const int* ctrl_tok,
+                                               int ctrl_stride, const bf16_t* emb, const float* w, const float* b,
+                                               float* h, int C, int f16) {
   __shared__ float red[4];
   const int r = blockIdx.x;
-  const uint32_t tok = tokens[r];
+  const uint32_t tok = ctrl_tok ? (uint32_t)ctrl_tok[(int64_t)rows[r].x * ctrl_stride] : tokens[r];
   const bf16_t* e = emb + (int64_t)tok * C;
   float v[kMaxPerThread];
   float s = 0.f;
@@ -241,7 +242,7 @@ __global__ __launch_bounds__(256) void k_ln_mix(LnMixArgs a) {
     }
   }
   if (flags & kRowLast) {
-    float* sn = a.shift + (((int64_t)(par ^ 1) * a.S + slot) * a.L + a.layer) * a.C;
+    float* sn = a.shift + (((int64_t)(a.inplace ? par : par ^ 1) * a.S + slot) * a.L + a.layer) * a.C;
 #pragma unroll
     for (int q = 0; q < kLnVec; ++q) {
       const int c = t4 + 1024 * q;
@@ -317,7 +318,8 @@ __global__ __launch_bounds__(256) void k_ln1024(LnMixArgs a) {
       const float4_ x = v + (pv - v) * mu[m];
       store(x, a.x_hi + m * a.mix_stride, a.x_lo + m * a.mix_stride, (int64_t)out_row * a.ldx + c);
     }
-    if (flags & kRowLast) *(float4_*)(a.shift + (((int64_t)(par ^ 1) * a.S + slot) * a.L + a.layer) * C + c) = v;
+    if (flags & kRowLast)
+      *(float4_*)(a.shift + (((int64_t)(a.inplace ? par : par ^ 1) * a.S + slot) * a.L + a.layer) * C + c) = v;
   }
 }
 
@@ -809,9 +811,9 @@ __global__ __launch_bounds__(256, 2) void k_wkv(WkvArgs a) {
 // ------------------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------------------
-void launch_embed(const uint32_t* tokens, const bf16_t* emb, const float* w, const float* b,
-                  float* h, int R, int C, int f16, hipStream_t st) {
-  hipLaunchKernelGGL(k_embed, dim3(R), dim3(256), 0, st, tokens, emb, w, b, h, C, f16);
+void launch_embed(const uint32_t* tokens, const int4* rows, const int* ctrl_tok, int ctrl_stride,
+                  const bf16_t* emb, const float* w, const float* b, float* h, int R, int C, int f16, hipStream_t st) {
+  hipLaunchKernelGGL(k_embed, dim3(R), dim3(256), 0, st, tokens, rows, ctrl_tok, ctrl_stride, emb, w, b, h, C, f16);
 }
 void launch_ln_mix(const LnMixArgs& a, int n_out_rows, hipStream_t st) {
   LnMixArgs b = a;
