@@ -73,6 +73,7 @@ __device__ inline uint16_t f32_to_w16(float x, bool f16) { return f16 ? f32_to_h
 // x = hi + lo split of two floats into packed 16-bit pairs (hi = RNE(x), lo = RNE(x - hi)):
 // one packed convert per plane.
 typedef float float2_ __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4_ __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x2_ __attribute__((ext_vector_type(2)));
 typedef _Float16 f16x2_ __attribute__((ext_vector_type(2)));
 template <bool F16>
@@ -92,5 +93,23 @@ __device__ inline void split2(float a, float b, uint32_t& hi, uint32_t& lo) {
 }
 
 inline int64_t align_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
+
+// Debug timeline (RWKVTTS_TIMELINE): start of the launch's first workgroup and end of its last
+// one in s_memrealtime ticks (100 MHz, one clock for every CU); ends are max-reduced over 64
+// slots to keep the atomics off one address. Slot layout per launch: [0] start, [2..65] ends.
+// Null in production.
+constexpr int kTlStride = 66;
+__device__ inline int tl_block() { return (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x; }
+// The hooks compile to nothing unless the library is built with -DRWKVTTS_TL (make TL=1).
+__device__ inline void tl_begin(unsigned long long* tl) {
+#ifdef RWKVTTS_TL
+  if (tl && threadIdx.x == 0 && tl_block() == 0) tl[0] = (unsigned long long)__builtin_amdgcn_s_memrealtime();
+#endif
+}
+__device__ inline void tl_end(unsigned long long* tl) {
+#ifdef RWKVTTS_TL
+  if (tl && threadIdx.x == 0) atomicMax(&tl[2 + (tl_block() & 63)], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+#endif
+}
 
 }  // namespace rwkvtts

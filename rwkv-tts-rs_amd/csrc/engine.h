@@ -77,6 +77,22 @@ class Engine {
   int splitA_ = 1, splitO_ = 1, splitK_ = 1, splitF_ = 1, splitH_ = 1;
   bool use_graphs_ = true;
   uint8_t* wblob_ = nullptr;
+  // debug timeline (RWKVTTS_TIMELINE=path): per launch of a decode step, earliest WG start and
+  // latest WG end (s_memrealtime); accumulated over steps and written at the end of generate()
+  unsigned long long* d_tl_ = nullptr;  // [kTlMax][kTlStride]
+  std::string tl_path_;
+  std::vector<std::string> tl_names_;
+  std::vector<double> tl_start_, tl_dur_;
+  int tl_steps_ = 0;
+  int tl_n_ = 0;
+  unsigned long long* tl_next(const char* name) {
+    if (!d_tl_ || tl_n_ >= kTlMax) return nullptr;
+    if ((int)tl_names_.size() <= tl_n_) tl_names_.push_back(name);
+    unsigned long long* p = d_tl_ + (size_t)kTlStride * tl_n_;
+    ++tl_n_;
+    return p;
+  }
+  static constexpr int kTlMax = 1024;
   bf16_t* wpack_ = nullptr;      // GEMM matrices in MFMA fragment blocks (launch_pack_frag)
   bf16_t* lora_pack_ = nullptr;  // [L][C][Dtot] LoRA-up rows in k_wkv's per-thread order
   const bf16_t* emb_ = nullptr;

@@ -87,6 +87,11 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
     dbg_gstamp_path_ = gp;
     RT_OK(alloc(&dbg_gstamps_, 2 * 4096 * 4));
   }
+  if (const char* tp = getenv("RWKVTTS_TIMELINE")) {
+    tl_path_ = tp;
+    RT_OK(alloc(&d_tl_, (size_t)kTlStride * kTlMax));
+    use_graphs_ = desc.use_graphs != 0;
+  }
   if (const char* sp = getenv("RWKVTTS_WKV_STAMPS")) {
     dbg_stamp_path_ = sp;
     RT_OK(alloc(&dbg_stamps_, 4096 * 8));
@@ -309,8 +314,9 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
   const bool inplace = tok_from_ctrl;
   if (!inplace) hipLaunchKernelGGL(k_rows_parity, dim3(nb), dim3(256), 0, stream_, d_rows_, slot_par_, R);
   prof_begin(&ev);
+  tl_n_ = 0;
   launch_embed(d_tok_, d_rows_, tok_from_ctrl ? &d_ctrl_[0].next_token : nullptr, (int)(sizeof(SlotCtrl) / 4), emb_,
-               ln0_w_, ln0_b_, h0_, R, C, f16_, stream_);
+               ln0_w_, ln0_b_, h0_, R, C, f16_, stream_, tl_next("embed"));
   prof_end("embed", ev);
   const int64_t RC = (int64_t)Rmax_ * C;
   for (int l = 0; l < Lc; ++l) {
@@ -340,6 +346,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     m.rows = d_rows_;
     m.row_map = nullptr;
     m.inplace = inplace ? 1 : 0;
+    m.tl = tl_next("ln_att");
     prof_begin(&ev);
     if (!(dbg_exp_ & 0x10000)) launch_ln_mix(m, R, stream_);
     prof_end("ln_mix_att", ev);
@@ -364,6 +371,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     prof_begin(&ev);
     g.stamps = (l == 5 && dbg_gstamps_) ? dbg_gstamps_ : nullptr;
     g.exp = dbg_exp_ >> 8;
+    g.tl = tl_next("gemm_rkv");
     if (!(dbg_exp_ & 0x40000)) launch_gemm(g, stream_);
     prof_end("gemm_rkv_lora", ev);
     // ---- WKV + LoRA-up + GroupNorm + bonus + gate
@@ -380,6 +388,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     k.Dw = dims.d_decay; k.Da = dims.d_aaa; k.Dv = dims.d_mv; k.Dg = dims.d_gate;
     k.stamps = (l == 5) ? dbg_stamps_ : nullptr;
     k.exp = dbg_exp_;
+    k.tl = tl_next("wkv");
     prof_begin(&ev);
     if (!(dbg_exp_ & 0x20000)) launch_wkv(k, n_seg, H_, stream_);
     prof_end("wkv", ev);
@@ -392,6 +401,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     go.xmode = kXPlanes; go.out = partO_; go.split_stride = RC; go.ldo = C;
     prof_begin(&ev);
     go.exp = dbg_exp_ >> 8;
+    go.tl = tl_next("gemm_wo");
     if (!(dbg_exp_ & 0x40000)) launch_gemm(go, stream_);
     prof_end("gemm_wo", ev);
     // ---- ffn: residual + Wo partials -> LN2 -> mix
@@ -407,6 +417,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     f.x_hi = xf_hi_;
     f.x_lo = xf_lo_;
     f.shift = ffn_sh_;
+    f.tl = tl_next("ln_ffn");
     prof_begin(&ev);
     if (!(dbg_exp_ & 0x10000)) launch_ln_mix(f, R, stream_);
     prof_end("ln_mix_ffn", ev);
@@ -418,6 +429,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     gk.xmode = kXPlanes; gk.out = partK_; gk.split_stride = (int64_t)Rmax_ * F; gk.ldo = F;
     prof_begin(&ev);
     gk.exp = dbg_exp_ >> 8;
+    gk.tl = tl_next("gemm_key");
     if (!(dbg_exp_ & 0x40000)) launch_gemm(gk, stream_);
     prof_end("gemm_ffn_key", ev);
     GemmArgs gv{};
@@ -431,6 +443,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     prof_begin(&ev);
     gv.stamps = (l == 5 && dbg_gstamps_) ? dbg_gstamps_ + 4096 * 4 : nullptr;
     gv.exp = dbg_exp_ >> 8;
+    gv.tl = tl_next("gemm_value");
     if (!(dbg_exp_ & 0x40000)) launch_gemm(gv, stream_);
     prof_end("gemm_ffn_value", ev);
   }
@@ -453,6 +466,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     o.shift = nullptr;
     o.C = C;
     o.row_map = d_lg_rows_;
+    o.tl = tl_next("ln_out");
     prof_begin(&ev);
     launch_ln_mix(o, n_lg, stream_);
     prof_end("ln_out", ev);
@@ -464,6 +478,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     gh.xmode = kXPlanes; gh.out = logits_; gh.split_stride = (int64_t)Rmax_ * Vpad_; gh.ldo = Vpad_;
     prof_begin(&ev);
     gh.exp = dbg_exp_ >> 8;
+    gh.tl = tl_next("gemm_head");
     if (!(dbg_exp_ & 0x40000)) launch_gemm(gh, stream_);
     prof_end("gemm_head", ev);
     if (advance) {
@@ -476,6 +491,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
       a.ctrl = d_ctrl_;
       a.sem_out = d_sem_;
       a.n_rows = n_lg;
+      a.tl = tl_next("advance");
       prof_begin(&ev);
       launch_advance(a, stream_);
       prof_end("sample_advance", ev);
@@ -821,7 +837,10 @@ int Engine::generate(const rwkvtts_request* reqs, int n, rwkvtts_result* res) {
       // Up to kLookahead decode steps are queued back to back before the host reads the control
       // blocks: no slot can pass its step limit inside the window (EOS may end a request
       // earlier: its slot then idles through the rest of the window, k_advance skips it).
-      int K = profiling ? 1 : kLookahead;
+      int K = (profiling || d_tl_) ? 1 : kLookahead;
+      if (d_tl_) {
+        RT_HIP(hipMemsetAsync(d_tl_, 0, (size_t)kTlStride * kTlMax * 8, stream_));
+      }
       for (auto& a : act) {
         const Active& aa = a;
         const int total = aa.zero_shot ? sem_limit_of(reqs[aa.req]) : RWKVTTS_N_GLOBAL + 1 + sem_limit_of(reqs[aa.req]);
@@ -845,6 +864,21 @@ int Engine::generate(const rwkvtts_request* reqs, int n, rwkvtts_result* res) {
       stats.steps += K;
       stats.decode_rows += (int64_t)R * K;
       RT_OK(flush_prof());
+      if (d_tl_ && stats.steps > 40) {  // semantic-phase steps only
+        std::vector<unsigned long long> h((size_t)kTlStride * kTlMax);
+        RT_HIP(hipMemcpy(h.data(), d_tl_, h.size() * 8, hipMemcpyDeviceToHost));
+        const int n = (int)tl_names_.size();
+        tl_start_.resize(n, 0.0);
+        tl_dur_.resize(n, 0.0);
+        for (int i = 0; i < n; ++i) {
+          const unsigned long long* q = h.data() + (size_t)kTlStride * i;
+          unsigned long long e = 0;
+          for (int j = 2; j < kTlStride; ++j) e = std::max(e, q[j]);
+          tl_start_[i] += (double)(q[0] - h[0]) * 0.01;  // us
+          tl_dur_[i] += (double)(e - q[0]) * 0.01;
+        }
+        tl_steps_++;
+      }
       for (auto& a : act) {
         if (h_ctrl_[a.slot].phase == kPhDone) finished = true;
       }
@@ -875,6 +909,15 @@ int Engine::generate(const rwkvtts_request* reqs, int n, rwkvtts_result* res) {
 }
 
 int Engine::dump_stamps() {
+  if (d_tl_ && tl_steps_ > 0) {
+    FILE* f = fopen(tl_path_.c_str(), "w");
+    if (f) {
+      fprintf(f, "# steps %d: launch index, name, mean start (us from the step's first launch), mean duration (us)\n", tl_steps_);
+      for (size_t i = 0; i < tl_dur_.size(); ++i)
+        fprintf(f, "%zu %s %.3f %.3f\n", i, tl_names_[i].c_str(), tl_start_[i] / tl_steps_, tl_dur_[i] / tl_steps_);
+      fclose(f);
+    }
+  }
   if (dbg_gstamps_) {
     std::vector<uint64_t> hg(2 * 4096 * 4);
     RT_HIP(hipMemcpy(hg.data(), dbg_gstamps_, hg.size() * 8, hipMemcpyDeviceToHost));

@@ -33,6 +33,7 @@ struct LnMixArgs {
   const int* row_map;  // output row -> source row (ln_out) or null
   int n_rows;          // set by the launcher
   int f16;             // planes in f16 (fp16 model) instead of bf16
+  unsigned long long* tl;  // debug timeline slot (null in production)
   int inplace;         // decode step (one row per slot): the shift update overwrites the parity it
                        // read (same thread, read before write) and the parity is not flipped
 };
@@ -65,6 +66,7 @@ struct GemmArgs {
   uint64_t* stamps;    // debug: 4 s_memtime stamps per workgroup (null in production)
   int f16;             // weights and activation planes in f16 (fp16 model)
   int exp;             // debug experiment bits (0 in production): 1 skip X loads, 2 skip W loads
+  unsigned long long* tl;  // debug timeline slot (null in production)
 };
 
 struct WkvArgs {
@@ -90,11 +92,13 @@ struct WkvArgs {
   int f16;             // fp16 model: LoRA-up rows and the z planes are f16
   uint64_t* stamps;    // debug: 8 s_memtime stamps per workgroup (null in production)
   int exp;             // debug experiment bits (0 in production)
+  unsigned long long* tl;  // debug timeline slot (null in production)
 };
 
 // tokens: per-row ids, or (ctrl_tok != null, decode) row r's id = ctrl_tok[rows[r].x * ctrl_stride]
 void launch_embed(const uint32_t* tokens, const int4* rows, const int* ctrl_tok, int ctrl_stride,
-                  const bf16_t* emb, const float* w, const float* b, float* h, int R, int C, int f16, hipStream_t st);
+                  const bf16_t* emb, const float* w, const float* b, float* h, int R, int C, int f16, hipStream_t st,
+                  unsigned long long* tl = nullptr);
 void launch_ln_mix(const LnMixArgs& a, int n_out_rows, hipStream_t st);
 void launch_gemm(const GemmArgs& a, hipStream_t st);
 void launch_wkv(const WkvArgs& a, int n_seg, int H, hipStream_t st);

@@ -48,8 +48,9 @@ __device__ inline void split_store(float x, bf16_t* hi, bf16_t* lo, int64_t idx,
 // ------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_embed(const uint32_t* tokens, const int4* rows, const int* ctrl_tok,
                                                int ctrl_stride, const bf16_t* emb, const float* w, const float* b,
-                                               float* h, int C, int f16) {
+                                               float* h, int C, int f16, unsigned long long* tl) {
   __shared__ float red[4];
+  tl_begin(tl);
   const int r = blockIdx.x;
   const uint32_t tok = ctrl_tok ? (uint32_t)ctrl_tok[(int64_t)rows[r].x * ctrl_stride] : tokens[r];
   const bf16_t* e = emb + (int64_t)tok * C;
@@ -75,6 +76,7 @@ __global__ __launch_bounds__(256) void k_embed(const uint32_t* tokens, const int
     const int c = threadIdx.x + i * 256;
     if (c < C) h[(int64_t)r * C + c] = (v[i] - mean) * rstd * w[c] + b[c];
   }
+  tl_end(tl);
 }
 
 // ------------------------------------------------------------------------------------
@@ -262,6 +264,7 @@ template <bool F16, int MODE, int NMIX, int NP>
 __global__ __launch_bounds__(256) void k_ln1024(LnMixArgs a) {
   constexpr int C = 1024;
   __shared__ float red[16];
+  tl_begin(a.tl);
   const int out_row = blockIdx.x;
   const int row = a.row_map ? a.row_map[out_row] : out_row;
   const int c = 4 * threadIdx.x;
@@ -302,6 +305,7 @@ __global__ __launch_bounds__(256) void k_ln1024(LnMixArgs a) {
   };
   if constexpr (MODE == 0) {
     store(v, a.x_hi, a.x_lo, (int64_t)out_row * a.ldx + c);
+    tl_end(a.tl);
     return;
   } else {
     if (prev_row >= 0) {  // prefill row: the previous token's LN output, recomputed identically
@@ -320,6 +324,7 @@ __global__ __launch_bounds__(256) void k_ln1024(LnMixArgs a) {
     }
     if (flags & kRowLast)
       *(float4_*)(a.shift + (((int64_t)(a.inplace ? par : par ^ 1) * a.S + slot) * a.L + a.layer) * C + c) = v;
+    tl_end(a.tl);
   }
 }
 
@@ -487,6 +492,7 @@ __global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
   constexpr int ROWS = MT * 16;
   bf16_t* xh = (bf16_t*)smem;
   bf16_t* xl = xh + ROWS * LD;
+  tl_begin(a.tl);
   const int tile = blockIdx.x;
   int s = 0;
 #pragma unroll
@@ -606,6 +612,7 @@ __global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
         if (row < a.M) out[(int64_t)row * a.ldo] = acc_h[m][j] + acc_l[m][j];
       }
   }
+  tl_end(a.tl);
 }
 
 // ------------------------------------------------------------------------------------
@@ -812,8 +819,9 @@ __global__ __launch_bounds__(256, 2) void k_wkv(WkvArgs a) {
 // host launchers
 // ------------------------------------------------------------------------------------
 void launch_embed(const uint32_t* tokens, const int4* rows, const int* ctrl_tok, int ctrl_stride,
-                  const bf16_t* emb, const float* w, const float* b, float* h, int R, int C, int f16, hipStream_t st) {
-  hipLaunchKernelGGL(k_embed, dim3(R), dim3(256), 0, st, tokens, rows, ctrl_tok, ctrl_stride, emb, w, b, h, C, f16);
+                  const bf16_t* emb, const float* w, const float* b, float* h, int R, int C, int f16, hipStream_t st,
+                  unsigned long long* tl) {
+  hipLaunchKernelGGL(k_embed, dim3(R), dim3(256), 0, st, tokens, rows, ctrl_tok, ctrl_stride, emb, w, b, h, C, f16, tl);
 }
 void launch_ln_mix(const LnMixArgs& a, int n_out_rows, hipStream_t st) {
   LnMixArgs b = a;
@@ -1370,6 +1378,7 @@ __global__ __launch_bounds__(128) void k_wkv4(WkvArgs a) {
   __shared__ float s_red[4][2];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, i = t >> 1, hf = t & 1;
   const int h = blockIdx.y, C = a.C, c = h * N + i;
+  tl_begin(a.tl);
   const int4 sg = a.segs[blockIdx.x];
   // ---- head-only loads: half of channel c's LoRA-up rows + parameters
   uint4 lw[18];  // 8 bf16 per entry: w 0..3 | a 4..7 | v 8..9 | g 10..17
@@ -1542,6 +1551,7 @@ __global__ __launch_bounds__(128) void k_wkv4(WkvArgs a) {
     }
     if (rr + 1 < n_rows) __syncthreads();
   }
+  tl_end(a.tl);
 }
 
 void launch_wkv(const WkvArgs& a, int n_seg, int H, hipStream_t st) {

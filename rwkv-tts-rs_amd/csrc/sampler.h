@@ -56,6 +56,7 @@ struct AdvanceArgs {
   SlotCtrl* ctrl;
   int32_t* sem_out;      // [S][2048]
   int n_rows;
+  unsigned long long* tl;  // debug timeline slot (null in production)
 };
 
 void launch_sample_rows(const SampleRowArgs& a, int rows, hipStream_t st);

@@ -777,6 +777,7 @@ __device__ inline float load_logit(const AdvanceArgs& a, const float* lg, int i)
 
 __global__ __launch_bounds__(256) void k_advance(AdvanceArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  tl_begin(a.tl);
   const int row = blockIdx.x;
   const int slot = a.row_slot[row];
   SlotCtrl* c = a.ctrl + slot;
@@ -853,6 +854,7 @@ __global__ __launch_bounds__(256) void k_advance(AdvanceArgs a) {
       if (c->n_sem >= c->sem_limit) c->phase = kPhDone;
     }
   }
+  tl_end(a.tl);
 }
 
 void launch_advance(const AdvanceArgs& a, hipStream_t st) {
