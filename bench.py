@@ -57,7 +57,7 @@ def pmc_traffic(kernel):
     if not files:
         return None, None
     k = json.load(open(files[-1]))["kernels"]
-    key = "ln_mix" if kernel.startswith("ln_mix") else kernel
+    key = kernel if kernel in k else ("ln_mix" if kernel.startswith("ln_mix") else kernel)
     if key not in k:
         return None, None
     return k[key]["traffic_bytes"], os.path.relpath(files[-1], ROOT)

@@ -98,7 +98,7 @@ struct WkvArgs {
 // tokens: per-row ids, or (ctrl_tok != null, decode) row r's id = ctrl_tok[rows[r].x * ctrl_stride]
 void launch_embed(const uint32_t* tokens, const int4* rows, const int* ctrl_tok, int ctrl_stride,
                   const bf16_t* emb, const float* w, const float* b, float* h, int R, int C, int f16, hipStream_t st,
-                  unsigned long long* tl = nullptr);
+                  unsigned long long* tl, int n_vocab);
 void launch_ln_mix(const LnMixArgs& a, int n_out_rows, hipStream_t st);
 void launch_gemm(const GemmArgs& a, hipStream_t st);
 void launch_wkv(const WkvArgs& a, int n_seg, int H, hipStream_t st);

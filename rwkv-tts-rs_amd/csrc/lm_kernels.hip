@@ -48,11 +48,12 @@ __device__ inline void split_store(float x, bf16_t* hi, bf16_t* lo, int64_t idx,
 // ------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_embed(const uint32_t* tokens, const int4* rows, const int* ctrl_tok,
                                                int ctrl_stride, const bf16_t* emb, const float* w, const float* b,
-                                               float* h, int C, int f16, unsigned long long* tl) {
+                                               float* h, int C, int f16, unsigned long long* tl, int n_vocab) {
   __shared__ float red[4];
   tl_begin(tl);
   const int r = blockIdx.x;
-  const uint32_t tok = ctrl_tok ? (uint32_t)ctrl_tok[(int64_t)rows[r].x * ctrl_stride] : tokens[r];
+  uint32_t tok = ctrl_tok ? (uint32_t)ctrl_tok[(int64_t)rows[r].x * ctrl_stride] : tokens[r];
+  if (tok >= (uint32_t)n_vocab) tok = 0;  // ids are validated on the host; never index past the table
   const bf16_t* e = emb + (int64_t)tok * C;
   float v[kMaxPerThread];
   float s = 0.f;
@@ -820,8 +821,9 @@ __global__ __launch_bounds__(256, 2) void k_wkv(WkvArgs a) {
 // ------------------------------------------------------------------------------------
 void launch_embed(const uint32_t* tokens, const int4* rows, const int* ctrl_tok, int ctrl_stride,
                   const bf16_t* emb, const float* w, const float* b, float* h, int R, int C, int f16, hipStream_t st,
-                  unsigned long long* tl) {
-  hipLaunchKernelGGL(k_embed, dim3(R), dim3(256), 0, st, tokens, rows, ctrl_tok, ctrl_stride, emb, w, b, h, C, f16, tl);
+                  unsigned long long* tl, int n_vocab) {
+  hipLaunchKernelGGL(k_embed, dim3(R), dim3(256), 0, st, tokens, rows, ctrl_tok, ctrl_stride, emb, w, b, h, C, f16, tl,
+                     n_vocab);
 }
 void launch_ln_mix(const LnMixArgs& a, int n_out_rows, hipStream_t st) {
   LnMixArgs b = a;
@@ -860,13 +862,15 @@ template <int MT, int KSTEPS>
 static void launch_gemm_t(const GemmArgs& a, dim3 grid, hipStream_t st) {
   const size_t lds = (size_t)MT * 16 * (KSTEPS * 32 + 8) * 2 * 2;
   static const bool v2 = !getenv("RWKVTTS_GEMM_OLD");
-  if (v2 && (a.xmode == kXPlanes || a.x_nsplit == 4) && a.stamps == nullptr && a.exp == 0) {
+  if (v2 && (a.xmode == kXPlanes || a.x_nsplit == 4 || a.x_nsplit == 2) && a.stamps == nullptr && a.exp == 0) {
     if (a.f16) {
       if (a.xmode == kXPlanes) hipLaunchKernelGGL((k_gemm2<MT, KSTEPS, kXPlanes, true, 1>), grid, dim3(256), lds, st, a);
-      else hipLaunchKernelGGL((k_gemm2<MT, KSTEPS, kXRelu2, true, 4>), grid, dim3(256), lds, st, a);
+      else if (a.x_nsplit == 4) hipLaunchKernelGGL((k_gemm2<MT, KSTEPS, kXRelu2, true, 4>), grid, dim3(256), lds, st, a);
+      else hipLaunchKernelGGL((k_gemm2<MT, KSTEPS, kXRelu2, true, 2>), grid, dim3(256), lds, st, a);
     } else {
       if (a.xmode == kXPlanes) hipLaunchKernelGGL((k_gemm2<MT, KSTEPS, kXPlanes, false, 1>), grid, dim3(256), lds, st, a);
-      else hipLaunchKernelGGL((k_gemm2<MT, KSTEPS, kXRelu2, false, 4>), grid, dim3(256), lds, st, a);
+      else if (a.x_nsplit == 4) hipLaunchKernelGGL((k_gemm2<MT, KSTEPS, kXRelu2, false, 4>), grid, dim3(256), lds, st, a);
+      else hipLaunchKernelGGL((k_gemm2<MT, KSTEPS, kXRelu2, false, 2>), grid, dim3(256), lds, st, a);
     }
     return;
   }

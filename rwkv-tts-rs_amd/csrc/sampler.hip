@@ -772,6 +772,7 @@ void launch_sample_rows(const SampleRowArgs& a, int rows, hipStream_t st) {
 __device__ inline float load_logit(const AdvanceArgs& a, const float* lg, int i) {
   float v = lg[i];
   for (int p = 1; p < a.n_part; ++p) v += lg[p * a.part_stride + i];
+  if (a.sanitize && !(fabsf(v) < 1e30f)) v = 0.f;
   return v;
 }
 

@@ -1,8 +1,9 @@
 # Round profiles: rocprofv3 kernel-trace --stats of a bench run + separate PMC passes
-# (FETCH_SIZE, WRITE_SIZE) on the short LM workload. Outputs under gpurun_out/prof_r01/.
+# (FETCH_SIZE, WRITE_SIZE) on the short LM workload. Usage: gpu_profiles.sh TAG
+# Outputs under gpurun_out/prof_TAG/.
 set -o pipefail
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/prof_r01
+O=$R/gpurun_out/prof_${1:-r01}
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o bench -- python3 $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline > $O/bench_trace.log 2>&1 || exit 1
