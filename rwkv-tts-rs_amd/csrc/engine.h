@@ -73,10 +73,6 @@ class Engine {
   int device_ = 0;
   int f16_ = 0;  // fp16 matrices (else bf16): MFMA f16 and f16 activation planes
   hipStream_t stream_ = nullptr;
-  hipStream_t stream2_ = nullptr;     // pipelined-launch experiment
-  hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;
-  bool pipe_ = false;
-  int kidx_ = 0;
   int S_ = 0, Rmax_ = 0, chunk_ = 0, H_ = 0, Vpad_ = 0, Dtot_ = 0, ldA_ = 0;
   int splitA_ = 1, splitO_ = 1, splitK_ = 1, splitF_ = 1, splitH_ = 1;
   bool use_graphs_ = true;

@@ -42,12 +42,7 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
   device_ = desc.device;
   RT_HIP(hipSetDevice(device_));
   RT_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-  pipe_ = getenv("RWKVTTS_PIPE_RACE") != nullptr;  // timing experiment only: results are racy
-  if (pipe_) {
-    RT_HIP(hipStreamCreateWithFlags(&stream2_, hipStreamNonBlocking));
-    RT_HIP(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
-    RT_HIP(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
-  }
+
   rwkvtts_blob_header hdr;
   if (on_device) {
     RT_HIP(hipMemcpy(&hdr, weights, sizeof(hdr), hipMemcpyDeviceToHost));
@@ -200,6 +195,7 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
   RT_OK(alloc(&d_ctrl_, (size_t)S_));
   RT_OK(alloc(&d_sem_, (size_t)S_ * RWKVTTS_SEMANTIC_LIMIT));
   RT_HIP(hipHostMalloc((void**)&h_ctrl_, sizeof(SlotCtrl) * S_, hipHostMallocDefault));
+
   RT_HIP(hipDeviceSynchronize());
   return RWKVTTS_OK;
 }
@@ -321,13 +317,6 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
   if (!inplace) hipLaunchKernelGGL(k_rows_parity, dim3(nb), dim3(256), 0, stream_, d_rows_, slot_par_, R);
   prof_begin(&ev);
   tl_n_ = 0;
-  kidx_ = 0;
-  const bool pipe = pipe_ && tok_from_ctrl;
-  auto ks = [&]() -> hipStream_t { return (pipe && (kidx_++ & 1)) ? stream2_ : stream_; };
-  if (pipe) {  // experiment: successive launches alternate between two forked streams
-    RT_HIP(hipEventRecord(ev_fork_, stream_));
-    RT_HIP(hipStreamWaitEvent(stream2_, ev_fork_, 0));
-  }
   launch_embed(d_tok_, d_rows_, tok_from_ctrl ? &d_ctrl_[0].next_token : nullptr, (int)(sizeof(SlotCtrl) / 4), emb_,
                ln0_w_, ln0_b_, h0_, R, C, f16_, stream_, tl_next("embed"), dims.n_vocab);
   prof_end("embed", ev);
@@ -361,7 +350,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     m.inplace = inplace ? 1 : 0;
     m.tl = tl_next("ln_att");
     prof_begin(&ev);
-    if (!(dbg_exp_ & 0x10000)) launch_ln_mix(m, R, ks());
+    if (!(dbg_exp_ & 0x10000)) launch_ln_mix(m, R, stream_);
     prof_end("ln_mix_att", ev);
     // ---- r, k, v and the LoRA-down projections (w, a, v, g) in one launch (7 segments)
     GemmArgs g{};
@@ -385,7 +374,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     g.stamps = (l == 5 && dbg_gstamps_) ? dbg_gstamps_ : nullptr;
     g.exp = dbg_exp_ >> 8;
     g.tl = tl_next("gemm_rkv");
-    if (!(dbg_exp_ & 0x40000)) launch_gemm(g, ks());
+    if (!(dbg_exp_ & 0x40000)) launch_gemm(g, stream_);
     prof_end("gemm_rkv_lora", ev);
     // ---- WKV + LoRA-up + GroupNorm + bonus + gate
     WkvArgs k{};
@@ -403,7 +392,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     k.exp = dbg_exp_;
     k.tl = tl_next("wkv");
     prof_begin(&ev);
-    if (!(dbg_exp_ & 0x20000)) launch_wkv(k, n_seg, H_, ks());
+    if (!(dbg_exp_ & 0x20000)) launch_wkv(k, n_seg, H_, stream_);
     prof_end("wkv", ev);
     // ---- output projection (split-K partials)
     GemmArgs go{};
@@ -415,7 +404,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     prof_begin(&ev);
     go.exp = dbg_exp_ >> 8;
     go.tl = tl_next("gemm_wo");
-    if (!(dbg_exp_ & 0x40000)) launch_gemm(go, ks());
+    if (!(dbg_exp_ & 0x40000)) launch_gemm(go, stream_);
     prof_end("gemm_wo", ev);
     // ---- ffn: residual + Wo partials -> LN2 -> mix
     LnMixArgs f = m;
@@ -432,7 +421,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     f.shift = ffn_sh_;
     f.tl = tl_next("ln_ffn");
     prof_begin(&ev);
-    if (!(dbg_exp_ & 0x10000)) launch_ln_mix(f, R, ks());
+    if (!(dbg_exp_ & 0x10000)) launch_ln_mix(f, R, stream_);
     prof_end("ln_mix_ffn", ev);
     GemmArgs gk{};
     gk.f16 = f16_;
@@ -443,7 +432,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     prof_begin(&ev);
     gk.exp = dbg_exp_ >> 8;
     gk.tl = tl_next("gemm_key");
-    if (!(dbg_exp_ & 0x40000)) launch_gemm(gk, ks());
+    if (!(dbg_exp_ & 0x40000)) launch_gemm(gk, stream_);
     prof_end("gemm_ffn_key", ev);
     GemmArgs gv{};
     gv.f16 = f16_;
@@ -457,7 +446,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     gv.stamps = (l == 5 && dbg_gstamps_) ? dbg_gstamps_ + 4096 * 4 : nullptr;
     gv.exp = dbg_exp_ >> 8;
     gv.tl = tl_next("gemm_value");
-    if (!(dbg_exp_ & 0x40000)) launch_gemm(gv, ks());
+    if (!(dbg_exp_ & 0x40000)) launch_gemm(gv, stream_);
     prof_end("gemm_ffn_value", ev);
   }
   if (n_lg > 0) {
@@ -481,7 +470,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     o.row_map = d_lg_rows_;
     o.tl = tl_next("ln_out");
     prof_begin(&ev);
-    launch_ln_mix(o, n_lg, ks());
+    launch_ln_mix(o, n_lg, stream_);
     prof_end("ln_out", ev);
     GemmArgs gh{};
     gh.f16 = f16_;
@@ -492,7 +481,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     prof_begin(&ev);
     gh.exp = dbg_exp_ >> 8;
     gh.tl = tl_next("gemm_head");
-    if (!(dbg_exp_ & 0x40000)) launch_gemm(gh, ks());
+    if (!(dbg_exp_ & 0x40000)) launch_gemm(gh, stream_);
     prof_end("gemm_head", ev);
     if (advance) {
       AdvanceArgs a{};
@@ -505,15 +494,10 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
       a.sem_out = d_sem_;
       a.n_rows = n_lg;
       a.tl = tl_next("advance");
-      a.sanitize = pipe_ ? 1 : 0;
       prof_begin(&ev);
-      launch_advance(a, ks());
+      launch_advance(a, stream_);
       prof_end("sample_advance", ev);
     }
-  }
-  if (pipe) {
-    RT_HIP(hipEventRecord(ev_join_, stream2_));
-    RT_HIP(hipStreamWaitEvent(stream_, ev_join_, 0));
   }
   if (!inplace)
     hipLaunchKernelGGL(k_flip_parity, dim3((n_seg + 255) / 256), dim3(256), 0, stream_, d_segs_, slot_par_, n_seg);

@@ -99,9 +99,10 @@ struct WkvArgs {
 void launch_embed(const uint32_t* tokens, const int4* rows, const int* ctrl_tok, int ctrl_stride,
                   const bf16_t* emb, const float* w, const float* b, float* h, int R, int C, int f16, hipStream_t st,
                   unsigned long long* tl, int n_vocab);
-void launch_ln_mix(const LnMixArgs& a, int n_out_rows, hipStream_t st);
-void launch_gemm(const GemmArgs& a, hipStream_t st);
-void launch_wkv(const WkvArgs& a, int n_seg, int H, hipStream_t st);
+// Launchers return the workgroup count of the launch.
+int launch_ln_mix(const LnMixArgs& a, int n_out_rows, hipStream_t st);
+int launch_gemm(const GemmArgs& a, hipStream_t st);
+int launch_wkv(const WkvArgs& a, int n_seg, int H, hipStream_t st);
 // Repack a GEMM matrix W [N][K] (K % 32 == 0) into MFMA fragment blocks (k_gemm's layout):
 // out holds ceil(N/16)*16*K elements.
 void launch_pack_frag(const bf16_t* W, int N, int K, bf16_t* out, hipStream_t st);

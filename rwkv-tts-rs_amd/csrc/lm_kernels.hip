@@ -269,23 +269,22 @@ __global__ __launch_bounds__(256) void k_ln1024(LnMixArgs a) {
   const int out_row = blockIdx.x;
   const int row = a.row_map ? a.row_map[out_row] : out_row;
   const int c = 4 * threadIdx.x;
-  float4_ v = ld4(a.h_in + (int64_t)row * C + c);
-  float4_ t[NP > 0 ? NP : 1];
-#pragma unroll
-  for (int p = 0; p < NP; ++p) t[p] = ld4(a.part + p * a.part_stride + (int64_t)row * a.ldp + c);
+  // loads that do not depend on the previous launch: LN / mix vectors, row descriptor, shift state
   const float4_ w = ld4(a.ln_w + c), b = ld4(a.ln_b + c);
   float4_ mu[NMIX > 0 ? NMIX : 1];
 #pragma unroll
   for (int m = 0; m < NMIX; ++m) mu[m] = ld4(a.mu[m] + c);
   int slot = 0, flags = 0, prev_row = -1, par = 0;
   float4_ pv = {0.f, 0.f, 0.f, 0.f};
-  const float* sh = nullptr;
   if constexpr (MODE == 1) {
     const int4 info = a.rows[row];
     slot = info.x; flags = info.y; prev_row = info.z; par = info.w;
-    sh = a.shift + (((int64_t)par * a.S + slot) * a.L + a.layer) * C;
-    if (prev_row < 0) pv = ld4(sh + c);
+    if (prev_row < 0) pv = ld4(a.shift + (((int64_t)par * a.S + slot) * a.L + a.layer) * C + c);
   }
+  float4_ v = ld4(a.h_in + (int64_t)row * C + c);
+  float4_ t[NP > 0 ? NP : 1];
+#pragma unroll
+  for (int p = 0; p < NP; ++p) t[p] = ld4(a.part + p * a.part_stride + (int64_t)row * a.ldp + c);
 #pragma unroll
   for (int p = 0; p < NP; ++p) v += t[p];
   if (a.h_out) *(float4_*)(a.h_out + (int64_t)row * C + c) = v;
@@ -306,8 +305,6 @@ __global__ __launch_bounds__(256) void k_ln1024(LnMixArgs a) {
   };
   if constexpr (MODE == 0) {
     store(v, a.x_hi, a.x_lo, (int64_t)out_row * a.ldx + c);
-    tl_end(a.tl);
-    return;
   } else {
     if (prev_row >= 0) {  // prefill row: the previous token's LN output, recomputed identically
       pv = ld4(a.h_in + (int64_t)prev_row * C + c);
@@ -325,8 +322,8 @@ __global__ __launch_bounds__(256) void k_ln1024(LnMixArgs a) {
     }
     if (flags & kRowLast)
       *(float4_*)(a.shift + (((int64_t)(a.inplace ? par : par ^ 1) * a.S + slot) * a.L + a.layer) * C + c) = v;
-    tl_end(a.tl);
   }
+  tl_end(a.tl);
 }
 
 // ------------------------------------------------------------------------------------
@@ -514,12 +511,20 @@ __global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
   const int split = blockIdx.y;
   const int kbeg = split * KS;
   const int row0 = blockIdx.z * ROWS;
-  // 1) X slice requests
+  // X slice (activations of the previous launch, L2-resident) and weight stream (packed
+  // fragment blocks, 1 KB per wave instruction). X is requested first: staging waits only for X
+  // (vmcnt retires in order) while the weights are still in flight.
   constexpr int CH = KS / 8;
   constexpr int PERP = ROWS * CH / 256;        // kXPlanes: 16-byte chunks per thread per plane
   constexpr int PERR = ROWS * KS / 4 / 256;    // kXRelu2: float4 chunks per thread per slab
   short8 vh[XMODE == kXPlanes ? PERP : 1], vl[XMODE == kXPlanes ? PERP : 1];
   float4_ xr[XMODE == kXPlanes ? 1 : NX][XMODE == kXPlanes ? 1 : PERR];
+  int nb = col0 >> 4;
+  const int nblk = (Nn + 15) >> 4;
+  if (nb >= nblk) nb = nblk - 1;
+  const bf16_t* wp = Wm + (((int64_t)nb * (a.K >> 5) + (kbeg >> 5)) * 64 + lane) * 8;
+  short8 b[KSTEPS];
+  auto load_x = [&]() {
   if constexpr (XMODE == kXPlanes) {
 #pragma unroll
     for (int u = 0; u < PERP; ++u) {
@@ -541,14 +546,13 @@ __global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
         xr[p][u] = *(const float4_*)(a.x_part + p * a.x_part_stride + (int64_t)src * a.x_ld + kbeg + k4);
       }
   }
-  // 2) weight stream (packed fragment blocks, 1 KB per wave instruction)
-  int nb = col0 >> 4;
-  const int nblk = (Nn + 15) >> 4;
-  if (nb >= nblk) nb = nblk - 1;
-  const bf16_t* wp = Wm + (((int64_t)nb * (a.K >> 5) + (kbeg >> 5)) * 64 + lane) * 8;
-  short8 b[KSTEPS];
+  };
+  auto load_w = [&]() {
 #pragma unroll
   for (int t = 0; t < KSTEPS; ++t) b[t] = __builtin_nontemporal_load((const short8*)(wp + t * 512));
+  };
+  load_x();
+  load_w();
   // 3) X -> LDS (rows past M hold a copy of row M-1; their outputs are not stored)
   if constexpr (XMODE == kXPlanes) {
 #pragma unroll
@@ -825,7 +829,7 @@ void launch_embed(const uint32_t* tokens, const int4* rows, const int* ctrl_tok,
   hipLaunchKernelGGL(k_embed, dim3(R), dim3(256), 0, st, tokens, rows, ctrl_tok, ctrl_stride, emb, w, b, h, C, f16, tl,
                      n_vocab);
 }
-void launch_ln_mix(const LnMixArgs& a, int n_out_rows, hipStream_t st) {
+int launch_ln_mix(const LnMixArgs& a, int n_out_rows, hipStream_t st) {
   LnMixArgs b = a;
   b.n_rows = n_out_rows;
   const dim3 grid(n_out_rows);
@@ -844,7 +848,7 @@ void launch_ln_mix(const LnMixArgs& a, int n_out_rows, hipStream_t st) {
       if (!a.shift) { LN_CASE(false, 0, 0) } else if (a.n_mix == 6) { LN_CASE(false, 1, 6) } else { LN_CASE(false, 1, 1) }
     }
 #undef LN_CASE
-    return;
+    return n_out_rows;
   }
   if (a.C <= 1024) {
     switch (a.n_part) {  // slab counts of the 0.4B configuration: every load in flight at once
@@ -856,6 +860,7 @@ void launch_ln_mix(const LnMixArgs& a, int n_out_rows, hipStream_t st) {
   } else {
     hipLaunchKernelGGL((k_ln_mix<2, -1>), grid, dim3(256), 0, st, b);
   }
+  return n_out_rows;
 }
 
 template <int MT, int KSTEPS>
@@ -885,7 +890,7 @@ static void launch_gemm_t(const GemmArgs& a, dim3 grid, hipStream_t st) {
 
 int gemm_ksteps(int kslice) { return kslice / 32; }
 
-void launch_gemm(const GemmArgs& a, hipStream_t st) {
+int launch_gemm(const GemmArgs& a, hipStream_t st) {
   const int tiles = a.seg[a.nseg - 1].tile_start + (a.seg[a.nseg - 1].N + 63) / 64;
   const int mt = a.M <= 16 ? 1 : 2;
   const int mg = (a.M + mt * 16 - 1) / (mt * 16);
@@ -903,6 +908,7 @@ void launch_gemm(const GemmArgs& a, hipStream_t st) {
     default: break;  // rejected at engine init (kslice in {128, 256, 512})
   }
 #undef GEMM_CASE
+  return (int)(grid.x * grid.y * grid.z);
 }
 // W [N][K] -> MFMA B-fragment blocks: block (nb, kb) = 16 columns x 32 k = 1 KB, lane
 // l = 16 g + li holding W[16 nb + li][32 kb + 8 g .. + 8]; blocks ordered nb-major. Rows >= N are 0.
@@ -1558,7 +1564,7 @@ __global__ __launch_bounds__(128) void k_wkv4(WkvArgs a) {
   tl_end(a.tl);
 }
 
-void launch_wkv(const WkvArgs& a, int n_seg, int H, hipStream_t st) {
+int launch_wkv(const WkvArgs& a, int n_seg, int H, hipStream_t st) {
   const dim3 grid(n_seg, H);
   if (a.Dw == 64 && a.Da == 64 && a.Dv == 32 && a.Dg == 128 && a.n_part <= 4 && !getenv("RWKVTTS_WKV_OLD")) {
     static const int sgw = getenv("RWKVTTS_WKV_SG") ? atoi(getenv("RWKVTTS_WKV_SG")) : 0;
@@ -1572,20 +1578,21 @@ void launch_wkv(const WkvArgs& a, int n_seg, int H, hipStream_t st) {
     } else {
       hipLaunchKernelGGL((k_wkv2<64, 64, 32, 128, 4>), grid, dim3(128), 0, st, a);
     }
-    return;
+    return n_seg * H;
   }
   if (a.Dw == 16 && a.Da == 16 && a.Dv == 16 && a.Dg == 32 && a.n_part <= 1 && !getenv("RWKVTTS_WKV_OLD")) {
     hipLaunchKernelGGL((k_wkv2<16, 16, 16, 32, 1>), grid, dim3(128), 0, st, a);
-    return;
+    return n_seg * H;
   }
   if (a.Dw == 32 && a.Da == 32 && a.Dv == 16 && a.Dg == 64 && a.n_part <= 1 && !getenv("RWKVTTS_WKV_OLD")) {
     hipLaunchKernelGGL((k_wkv2<32, 32, 16, 64, 1>), grid, dim3(128), 0, st, a);
-    return;
+    return n_seg * H;
   }
   const int units = (a.Dw + a.Da + a.Dv + a.Dg + 15) / 16;
   if (units <= 8 && a.n_part <= 4) hipLaunchKernelGGL((k_wkv<8, 4>), grid, dim3(256), 0, st, a);
   else if (units <= 20 && a.n_part <= 4) hipLaunchKernelGGL((k_wkv<20, 4>), grid, dim3(256), 0, st, a);
   else hipLaunchKernelGGL((k_wkv<32, 8>), grid, dim3(256), 0, st, a);
+  return n_seg * H;
 }
 
 }  // namespace rwkvtts

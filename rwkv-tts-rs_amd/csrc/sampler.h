@@ -57,10 +57,9 @@ struct AdvanceArgs {
   int32_t* sem_out;      // [S][2048]
   int n_rows;
   unsigned long long* tl;  // debug timeline slot (null in production)
-  int sanitize;            // experiments with racy inputs: non-finite logits read as 0 (0 in production)
 };
 
 void launch_sample_rows(const SampleRowArgs& a, int rows, hipStream_t st);
-void launch_advance(const AdvanceArgs& a, hipStream_t st);
+int launch_advance(const AdvanceArgs& a, hipStream_t st);
 
 }  // namespace rwkvtts

@@ -772,13 +772,10 @@ void launch_sample_rows(const SampleRowArgs& a, int rows, hipStream_t st) {
 __device__ inline float load_logit(const AdvanceArgs& a, const float* lg, int i) {
   float v = lg[i];
   for (int p = 1; p < a.n_part; ++p) v += lg[p * a.part_stride + i];
-  if (a.sanitize && !(fabsf(v) < 1e30f)) v = 0.f;
   return v;
 }
 
-__global__ __launch_bounds__(256) void k_advance(AdvanceArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  tl_begin(a.tl);
+__device__ __attribute__((always_inline)) void advance_body(const AdvanceArgs& a, char* smem) {
   const int row = blockIdx.x;
   const int slot = a.row_slot[row];
   SlotCtrl* c = a.ctrl + slot;
@@ -855,11 +852,18 @@ __global__ __launch_bounds__(256) void k_advance(AdvanceArgs a) {
       if (c->n_sem >= c->sem_limit) c->phase = kPhDone;
     }
   }
+}
+
+__global__ __launch_bounds__(256) void k_advance(AdvanceArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  tl_begin(a.tl);
+  advance_body(a, smem);
   tl_end(a.tl);
 }
 
-void launch_advance(const AdvanceArgs& a, hipStream_t st) {
+int launch_advance(const AdvanceArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(k_advance, dim3(a.n_rows), dim3(256), smem_bytes(RWKVTTS_EOS_TOKEN + 1), st, a);
+  return a.n_rows;
 }
 
 }  // namespace rwkvtts
