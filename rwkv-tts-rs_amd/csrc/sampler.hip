@@ -156,12 +156,13 @@ __device__ float wave_exact_add(float s, const float* p, int b, int e) {
 // Sequential f32 sum s + p[b] + ... + p[e-1] by ONE lane from its own registers: each 128-
 // element piece is pulled in with 32 back-to-back 16-byte LDS reads, then added in order -- one
 // dependent v_add per element, no cross-lane traffic. b must be a multiple of 4.
-__device__ inline float add128(float s, const float* p) {
-  float4_ v[32];
+template <int NE>
+__device__ inline float addNE(float s, const float* p) {
+  float4_ v[NE / 4];
 #pragma unroll
-  for (int q = 0; q < 32; ++q) v[q] = *(const float4_*)(p + 4 * q);
+  for (int q = 0; q < NE / 4; ++q) v[q] = *(const float4_*)(p + 4 * q);
 #pragma unroll
-  for (int q = 0; q < 32; ++q) {
+  for (int q = 0; q < NE / 4; ++q) {
     s += v[q][0];
     s += v[q][1];
     s += v[q][2];
@@ -169,8 +170,9 @@ __device__ inline float add128(float s, const float* p) {
   }
   return s;
 }
+template <int NE>
 __device__ inline float lane_serial_add(float s, const float* p, int b, int e) {
-  for (; b + 128 <= e; b += 128) s = add128(s, p + b);
+  for (; b + NE <= e; b += NE) s = addNE<NE>(s, p + b);
   for (; b + 4 <= e; b += 4) {
     const float4_ v = *(const float4_*)(p + b);
     s += v[0];
@@ -194,20 +196,21 @@ __device__ inline float prefix64(float s, float v, float* total) {
   return out;
 }
 
-// Shared-memory layout of one sampling workgroup (256 threads).
+// Shared-memory layout of one sampling workgroup (NT threads, NW = NT / 64 waves).
+// fred[0..NW) / ired[8..8+2 NW): block reductions; fred[16..20) / ired[0..8): named results.
 struct SampleSmem {
   float* p;           // [n] logits -> e -> probabilities
   uint64_t* keys;     // [kSampleMaxSorted] sort keys (p bits << 32 | ~index)
   int* list;          // [kSampleMaxSorted] positive indices in index order
   int* scan;          // [8] block-scan wave totals
   double* dscan;      // [8]
-  uint32_t* sub_t;    // [256][2] sub-chunk parity maps of the exact-sum emulation
-  int* sub_ok;        // [256]
+  uint32_t* sub_t;    // [NT][2] sub-chunk parity maps of the exact-sum emulation
+  int* sub_ok;        // [NT]
   int* chunk_e;       // [64] predicted binade per chunk
   uint32_t* chunk_t;  // [64][2]
   int* chunk_ok;      // [64]
-  float* fred;        // [8]
-  int* ired;          // [16]
+  float* fred;        // [32]
+  int* ired;          // [48]
 };
 
 __device__ inline int wave_sum_i(int v) {
@@ -215,16 +218,20 @@ __device__ inline int wave_sum_i(int v) {
   return v;
 }
 
+template <int NT>
 __device__ inline float block_max(float v, float* fred) {
   for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
   __syncthreads();
   if ((threadIdx.x & 63) == 0) fred[threadIdx.x >> 6] = v;
   __syncthreads();
-  return fmaxf(fmaxf(fred[0], fred[1]), fmaxf(fred[2], fred[3]));
+  float m = fred[0];
+#pragma unroll
+  for (int w = 1; w < NT / 64; ++w) m = fmaxf(m, fred[w]);
+  return m;
 }
 
-// block-wide exclusive scans (256 threads): wave shuffles + 4 wave totals
-template <typename T>
+// block-wide exclusive scans (NT threads): wave shuffles + NT/64 wave totals
+template <int NT, typename T>
 __device__ inline T block_excl_scan_t(T v, T* scratch, T* tot) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   T x = v;
@@ -238,20 +245,25 @@ __device__ inline T block_excl_scan_t(T v, T* scratch, T* tot) {
   __syncthreads();
   T base = 0;
   for (int k = 0; k < w; ++k) base += scratch[k];
-  *tot = (scratch[0] + scratch[1]) + (scratch[2] + scratch[3]);
+  T t = scratch[0];
+#pragma unroll
+  for (int k = 1; k < NT / 64; ++k) t += scratch[k];
+  *tot = t;
   return base + x - v;
 }
-__device__ inline int block_excl_scan(int v, int* scratch, int* tot) { return block_excl_scan_t<int>(v, scratch, tot); }
+template <int NT>
+__device__ inline int block_excl_scan(int v, int* scratch, int* tot) { return block_excl_scan_t<NT, int>(v, scratch, tot); }
 
 // compact indices with p > 0 into list (index order); returns count (may exceed capacity:
 // then list is incomplete and callers fall back to a scan of p).
+template <int NT>
 __device__ int compact_positive(const SampleSmem& sm, int n) {
-  const int chunk = (n + 255) / 256;
+  const int chunk = (n + NT - 1) / NT;
   const int b = min(n, (int)threadIdx.x * chunk), e = min(n, b + chunk);
   int cnt = 0;
   for (int i = b; i < e; ++i) cnt += sm.p[i] > 0.0f;
   int tot;
-  int off = block_excl_scan(cnt, sm.scan, &tot);
+  int off = block_excl_scan<NT>(cnt, sm.scan, &tot);
   for (int i = b; i < e; ++i)
     if (sm.p[i] > 0.0f) {
       if (off < kSampleMaxSorted) sm.list[off] = i;
@@ -324,18 +336,21 @@ __device__ inline void sum_sim_elem(uint32_t b, int E, uint32_t& T0, uint32_t& T
   if (T0 >= 0x1000000u || T1 >= 0x1000000u) ok = false;
 }
 
+template <int NT>
 __device__ float exact_seq_sum(const SampleSmem& sm, int n, uint64_t* stamps = nullptr) {
+  constexpr int NS = NT / 64;  // sub-chunks per chunk (64 chunks, one per lane of wave 0)
+  constexpr int NE = NT >= 1024 ? 64 : 128;  // serial-add register batch
   const int tid = threadIdx.x;
-  const int CH = (((n + 63) / 64) + 3) & ~3, SUB = (CH + 3) / 4;  // chunks start 16-byte aligned
-  const int chunk = tid >> 2, sub = tid & 3;
+  const int CH = (((n + 63) / 64) + 3) & ~3, SUB = (CH + NS - 1) / NS;  // chunks start 16-byte aligned
+  const int chunk = tid / NS, sub = tid % NS;
   const int cb = min(n, chunk * CH), ce = min(n, cb + CH);
   const int sb = min(ce, cb + sub * SUB), se = min(ce, sb + SUB);
   double ds = 0.0;
   for (int i = sb; i < se; ++i) ds += (double)sm.p[i];
   double dtot;
-  const double pre = block_excl_scan_t<double>(ds, sm.dscan, &dtot);
+  const double pre = block_excl_scan_t<NT, double>(ds, sm.dscan, &dtot);
   STAMP(10);
-  const double pchunk = __shfl(pre, (tid & 63) & ~3);  // prefix at the chunk start
+  const double pchunk = __shfl(pre, (tid & 63) & ~(NS - 1));  // prefix at the chunk start
   const float pf = (float)pchunk;
   const uint32_t pb = __builtin_bit_cast(uint32_t, pf);
   const int E = (int)((pb >> 23) & 0xFFu) - 127;
@@ -349,14 +364,14 @@ __device__ float exact_seq_sum(const SampleSmem& sm, int n, uint64_t* stamps = n
   if (sub == 0) sm.chunk_e[chunk] = E;
   __syncthreads();
   STAMP(11);
-  if (tid < 64) {  // compose the 4 sub-chunk maps of chunk `tid`
+  if (tid < 64) {  // compose the NS sub-chunk maps of chunk `tid`
     bool cok = true;
-    for (int s = 0; s < 4; ++s) cok &= sm.sub_ok[4 * tid + s] != 0;
+    for (int s = 0; s < NS; ++s) cok &= sm.sub_ok[NS * tid + s] != 0;
     for (int pin = 0; pin < 2; ++pin) {
       int par = pin;
       uint32_t T = 0;
-      for (int s = 0; s < 4; ++s) {
-        const uint32_t t = sm.sub_t[2 * (4 * tid + s) + par];
+      for (int s = 0; s < NS; ++s) {
+        const uint32_t t = sm.sub_t[2 * (NS * tid + s) + par];
         T += t;
         par = (int)((par + t) & 1u);
       }
@@ -414,7 +429,7 @@ __device__ float exact_seq_sum(const SampleSmem& sm, int n, uint64_t* stamps = n
       // unusable chunk, or a run whose prediction failed: add chunk c in order on one lane
       const int b0 = c * CH, e0 = min(n, b0 + CH);
       float t = 0.0f;
-      if (lane == 0) t = lane_serial_add(s, sm.p, b0, e0);
+      if (lane == 0) t = lane_serial_add<NE>(s, sm.p, b0, e0);
       s = readlane_f(t, 0);
       ++c;
       // the chunks after c (if inside a run) are no longer run heads; step them one at a time
@@ -434,27 +449,28 @@ __device__ float exact_seq_sum(const SampleSmem& sm, int n, uint64_t* stamps = n
         if (!fast) {
           const int b1 = c * CH, e1 = min(n, b1 + CH);
           float t1 = 0.0f;
-          if (lane == 0) t1 = lane_serial_add(s, sm.p, b1, e1);
+          if (lane == 0) t1 = lane_serial_add<NE>(s, sm.p, b1, e1);
           s = readlane_f(t1, 0);
         }
         ++c;
       }
     }
     if (tid == 0) {
-      sm.fred[4] = s;
+      sm.fred[16] = s;
       if (stamps) stamps[14] = nfast;
     }
   }
   __syncthreads();
   STAMP(13);
-  return sm.fred[4];
+  return sm.fred[16];
 }
 
 // bitonic sort (descending) of M (power of two) keys in LDS by the whole workgroup
+template <int NT>
 __device__ void bitonic_desc(uint64_t* keys, int M) {
   for (int k = 2; k <= M; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int q = threadIdx.x; q < M; q += 256) {
+      for (int q = threadIdx.x; q < M; q += NT) {
         const int ixj = q ^ j;
         if (ixj > q) {
           const uint64_t A = keys[q], B = keys[ixj];
@@ -473,6 +489,7 @@ __device__ inline uint64_t pkey(float p, int i) {
 
 // The sampler. p holds the (masked) logits on entry. Returns the index in every thread.
 // status: 0 ok, RWKVTTS_EUNSUPPORTED for the documented limitation.
+template <int NT>
 __device__ __attribute__((always_inline)) int sample_block(const SampleSmem& sm, int n, float temperature, float top_p,
                             int top_k, const uint32_t* key, uint64_t draw, bool fixed42,
                             float* dbg, int* status, uint64_t* stamps = nullptr) {
@@ -482,15 +499,15 @@ __device__ __attribute__((always_inline)) int sample_block(const SampleSmem& sm,
   STAMP(1);
   // (2) softmax: max, exp, sequential sum (exact emulation), divide
   float mx = -__builtin_inff();
-  for (int i = tid; i < n; i += 256) mx = fmaxf(mx, sm.p[i]);
-  mx = block_max(mx, sm.fred);
-  for (int i = tid; i < n; i += 256) sm.p[i] = glibc_expf(sm.p[i] - mx);
+  for (int i = tid; i < n; i += NT) mx = fmaxf(mx, sm.p[i]);
+  mx = block_max<NT>(mx, sm.fred);
+  for (int i = tid; i < n; i += NT) sm.p[i] = glibc_expf(sm.p[i] - mx);
   __syncthreads();
   STAMP(2);
-  const float sum = exact_seq_sum(sm, n, stamps);
+  const float sum = exact_seq_sum<NT>(sm, n, stamps);
   STAMP(3);
   if (sum > 0.0f)
-    for (int i = tid; i < n; i += 256) sm.p[i] = sm.p[i] / sum;
+    for (int i = tid; i < n; i += NT) sm.p[i] = sm.p[i] / sum;
   __syncthreads();
   STAMP(4);
   // sorted (p desc, index asc) candidate keys; valid for the first n_sorted entries
@@ -498,9 +515,10 @@ __device__ __attribute__((always_inline)) int sample_block(const SampleSmem& sm,
   // (3) top-k (:95-105): candidates above a lower bound of the k-th largest, sorted
   if (top_k > 0 && top_k < n) {
     bool done = false;
-    if (top_k <= 256) {
-      // lower bound L: min over waves of the ceil(k/4)-th largest thread-local maximum
-      const int chunk = (n + 255) / 256;
+    if (top_k <= 64 * (NT / 64)) {
+      // lower bound L: min over waves of the ceil(k/NW)-th largest thread-local maximum (each of
+      // the NW waves holds that many disjoint elements >= L, so at least k elements are >= L)
+      const int chunk = (n + NT - 1) / NT;
       const int b = min(n, tid * chunk), e = min(n, b + chunk);
       float lm = -1.0f;  // every p >= 0
       for (int i = b; i < e; ++i) lm = fmaxf(lm, sm.p[i]);
@@ -513,27 +531,30 @@ __device__ __attribute__((always_inline)) int sample_block(const SampleSmem& sm,
           const bool up = ((lane & k) == 0) == ((lane & j) == 0);
           v = up ? fmaxf(v, o) : fminf(v, o);
         }
-      const int kw = (top_k + 3) / 4;
+      const int kw = (top_k + NT / 64 - 1) / (NT / 64);
       const float vw = __shfl(v, kw - 1);
       if (lane == 0) sm.fred[tid >> 6] = vw;
       __syncthreads();
-      const float L = fmaxf(fminf(fminf(sm.fred[0], sm.fred[1]), fminf(sm.fred[2], sm.fred[3])), 0.0f);
+      float Lm = sm.fred[0];
+#pragma unroll
+      for (int w = 1; w < NT / 64; ++w) Lm = fminf(Lm, sm.fred[w]);
+      const float L = fmaxf(Lm, 0.0f);
       int cnt = 0;
       for (int i = b; i < e; ++i) cnt += sm.p[i] >= L;
       int tot;
-      int off = block_excl_scan(cnt, sm.scan, &tot);
+      int off = block_excl_scan<NT>(cnt, sm.scan, &tot);
       if (tot <= kSampleMaxSorted) {
         for (int i = b; i < e; ++i)
           if (sm.p[i] >= L) sm.keys[off++] = pkey(sm.p[i], i);
         int M = 1;
         while (M < tot) M <<= 1;
-        for (int q = tot + tid; q < M; q += 256) sm.keys[q] = 0ull;
+        for (int q = tot + tid; q < M; q += NT) sm.keys[q] = 0ull;
         __syncthreads();
-        bitonic_desc(sm.keys, M);
+        bitonic_desc<NT>(sm.keys, M);
         // zero everything, then restore the k survivors
-        for (int i = tid; i < n; i += 256) sm.p[i] = 0.0f;
+        for (int i = tid; i < n; i += NT) sm.p[i] = 0.0f;
         __syncthreads();
-        for (int q = tid; q < top_k; q += 256) {
+        for (int q = tid; q < top_k; q += NT) {
           const uint64_t kk = sm.keys[q];
           sm.p[0xFFFFFFFFu - (uint32_t)kk] = __builtin_bit_cast(float, (uint32_t)(kk >> 32));
         }
@@ -548,24 +569,26 @@ __device__ __attribute__((always_inline)) int sample_block(const SampleSmem& sm,
       while (hi - lo > 1) {
         const uint32_t mid = lo + ((hi - lo) >> 1);
         int c = 0;
-        for (int i = tid; i < n; i += 256) c += __builtin_bit_cast(uint32_t, sm.p[i]) >= mid;
+        for (int i = tid; i < n; i += NT) c += __builtin_bit_cast(uint32_t, sm.p[i]) >= mid;
         c = wave_sum_i(c);
-        if ((tid & 63) == 0) sm.ired[8 + (it & 1) * 4 + (tid >> 6)] = c;
+        if ((tid & 63) == 0) sm.ired[8 + (it & 1) * (NT / 64) + (tid >> 6)] = c;
         __syncthreads();
-        const int* r4 = sm.ired + 8 + (it & 1) * 4;
-        const int t4 = (r4[0] + r4[1]) + (r4[2] + r4[3]);
+        const int* r4 = sm.ired + 8 + (it & 1) * (NT / 64);
+        int t4 = 0;
+#pragma unroll
+        for (int w = 0; w < NT / 64; ++w) t4 += r4[w];
         if (t4 >= top_k) lo = mid;
         else { hi = mid; cnt_hi = t4; }
         ++it;
       }
       const float t = __builtin_bit_cast(float, lo);
       const int need_eq = top_k - cnt_hi;
-      const int chunk = (n + 255) / 256;
+      const int chunk = (n + NT - 1) / NT;
       const int b = min(n, tid * chunk), e = min(n, b + chunk);
       int cnt = 0;
       for (int i = b; i < e; ++i) cnt += (sm.p[i] == t);
       int tot;
-      int rank = block_excl_scan(cnt, sm.scan, &tot);
+      int rank = block_excl_scan<NT>(cnt, sm.scan, &tot);
       for (int i = b; i < e; ++i) {
         const float v = sm.p[i];
         if (v < t) sm.p[i] = 0.0f;
@@ -578,7 +601,7 @@ __device__ __attribute__((always_inline)) int sample_block(const SampleSmem& sm,
     }
   }
   STAMP(5);
-  int npos = compact_positive(sm, n);
+  int npos = compact_positive<NT>(sm, n);
   STAMP(6);
   // (4) top-p (:108-153)
   if (top_p < 1.0f) {
@@ -590,9 +613,9 @@ __device__ __attribute__((always_inline)) int sample_block(const SampleSmem& sm,
       }
       int M = 1;
       while (M < npos) M <<= 1;
-      for (int q = tid; q < M; q += 256) sm.keys[q] = q < npos ? pkey(sm.p[sm.list[q]], sm.list[q]) : 0ull;
+      for (int q = tid; q < M; q += NT) sm.keys[q] = q < npos ? pkey(sm.p[sm.list[q]], sm.list[q]) : 0ull;
       __syncthreads();
-      bitonic_desc(sm.keys, M);
+      bitonic_desc<NT>(sm.keys, M);
     }
     if (tid < 64) {  // sequential cumulative in sorted order (wave-uniform, keys staged in lanes)
       float cum = 0.0f, cutoff = 0.0f;
@@ -612,22 +635,22 @@ __device__ __attribute__((always_inline)) int sample_block(const SampleSmem& sm,
       }
       if (!found && 0.0f >= top_p && npos < n) { found = 1; cutoff = 0.0f; }  // top_p <= 0 with zeros
       if (tid == 0) {
-        sm.fred[5] = cutoff;
+        sm.fred[17] = cutoff;
         sm.ired[2] = found;
       }
     }
     __syncthreads();
     if (sm.ired[2]) {
-      const float cutoff = sm.fred[5];
-      for (int i = tid; i < n; i += 256)
+      const float cutoff = sm.fred[17];
+      for (int i = tid; i < n; i += NT)
         if (sm.p[i] < cutoff) sm.p[i] = 0.0f;
       __syncthreads();
       if (top_p > 0.0f) {
-        npos = compact_positive(sm, n);
+        npos = compact_positive<NT>(sm, n);
         if (tid == 0) sm.ired[3] = 0;
         __syncthreads();
         int c = 0;
-        for (int i = tid; i < n; i += 256) c += (sm.p[i] == cutoff);
+        for (int i = tid; i < n; i += NT) c += (sm.p[i] == cutoff);
         c = wave_sum_i(c);
         if ((tid & 63) == 0) atomicAdd(&sm.ired[3], c);
         __syncthreads();
@@ -636,40 +659,40 @@ __device__ __attribute__((always_inline)) int sample_block(const SampleSmem& sm,
           if (tid == 0) {
             sm.ired[4] = 0;
             if (cur < top_p && sm.ired[3] > 0) {
-              sm.fred[6] = (top_p - cur) / (float)sm.ired[3];
+              sm.fred[18] = (top_p - cur) / (float)sm.ired[3];
               sm.ired[4] = 1;
             }
           }
         }
         __syncthreads();
         if (sm.ired[4]) {
-          const float adj = sm.fred[6];
-          for (int i = tid; i < n; i += 256)
+          const float adj = sm.fred[18];
+          for (int i = tid; i < n; i += NT)
             if (sm.p[i] == cutoff) sm.p[i] = cutoff + adj;
           __syncthreads();
         }
       }
     }
-    npos = compact_positive(sm, n);
+    npos = compact_positive<NT>(sm, n);
   }
   STAMP(7);
   // (5) temperature (:156-171)
   if (temperature != 1.0f && temperature > 0.0f) {
     const float tinv = 1.0f / temperature;
-    for (int i = tid; i < n; i += 256) {
+    for (int i = tid; i < n; i += NT) {
       const float v = sm.p[i];
       if (v > 0.0f) sm.p[i] = (float)exp2(log2((double)v) * (double)tinv);
     }
     __syncthreads();
-    npos = compact_positive(sm, n);
+    npos = compact_positive<NT>(sm, n);
     if (tid < 64) {
       const float s2 = wave_sum_positive(sm, n, npos);
-      if (tid == 0) sm.fred[7] = s2;
+      if (tid == 0) sm.fred[19] = s2;
     }
     __syncthreads();
-    const float s2 = sm.fred[7];
+    const float s2 = sm.fred[19];
     if (s2 > 0.0f)
-      for (int i = tid; i < n; i += 256) sm.p[i] = sm.p[i] / s2;
+      for (int i = tid; i < n; i += NT) sm.p[i] = sm.p[i] / s2;
     __syncthreads();
   }
   STAMP(8);
@@ -720,50 +743,54 @@ __device__ __attribute__((always_inline)) int sample_block(const SampleSmem& sm,
   return sm.ired[5];
 }
 
+template <int NT>
 __device__ SampleSmem carve(char* base, int n) {
   SampleSmem sm;
   const int npad = (n + 3) & ~3;
   char* q = base;
   sm.p = (float*)q; q += (size_t)npad * 4;
   sm.keys = (uint64_t*)q; q += kSampleMaxSorted * 8;
-  sm.dscan = (double*)q; q += 8 * 8;
+  sm.dscan = (double*)q; q += 16 * 8;
   sm.list = (int*)q; q += kSampleMaxSorted * 4;
-  sm.scan = (int*)q; q += 8 * 4;
-  sm.sub_t = (uint32_t*)q; q += 512 * 4;
-  sm.sub_ok = (int*)q; q += 256 * 4;
+  sm.scan = (int*)q; q += 16 * 4;
+  sm.sub_t = (uint32_t*)q; q += 2 * NT * 4;
+  sm.sub_ok = (int*)q; q += NT * 4;
   sm.chunk_e = (int*)q; q += 64 * 4;
   sm.chunk_t = (uint32_t*)q; q += 128 * 4;
   sm.chunk_ok = (int*)q; q += 64 * 4;
-  sm.fred = (float*)q; q += 8 * 4;
+  sm.fred = (float*)q; q += 32 * 4;
   sm.ired = (int*)q;
   return sm;
 }
+template <int NT>
 inline size_t smem_bytes(int n) {
   const int npad = (n + 3) & ~3;
-  return (size_t)npad * 4 + kSampleMaxSorted * 8 + 64 + kSampleMaxSorted * 4 + 32 + 2048 + 1024 + 256 +
-         512 + 256 + 32 + 64;
+  return (size_t)npad * 4 + kSampleMaxSorted * 8 + 16 * 8 + kSampleMaxSorted * 4 + 16 * 4 + 2 * NT * 4 + NT * 4 +
+         256 + 512 + 256 + 32 * 4 + 48 * 4;
 }
+constexpr int kSampleThreads = 512;  // one workgroup per sampled row
 
-__global__ __launch_bounds__(256) void k_sample_rows(SampleRowArgs a) {
+__global__ __launch_bounds__(kSampleThreads) void k_sample_rows(SampleRowArgs a) {
+  constexpr int NT = kSampleThreads;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const SampleSmem sm = carve(smem, a.n);
+  const SampleSmem sm = carve<NT>(smem, a.n);
   const int row = blockIdx.x;
   uint64_t* stamps = a.stamps ? a.stamps + row * 16 : nullptr;
   STAMP(0);
   const float* lg = a.logits + (int64_t)row * a.ld;
-  for (int i = threadIdx.x; i < a.n; i += 256) sm.p[i] = lg[i];
+  for (int i = threadIdx.x; i < a.n; i += NT) sm.p[i] = lg[i];
   __syncthreads();
   if (threadIdx.x == 0 && a.forbid >= 0 && a.forbid < a.n) sm.p[a.forbid] = -__builtin_inff();
   __syncthreads();
   int status;
-  const int id = sample_block(sm, a.n, a.temperature, a.top_p, a.top_k,
+  const int id = sample_block<NT>(sm, a.n, a.temperature, a.top_p, a.top_k,
                               a.keys ? a.keys + row * 8 : nullptr, a.draws ? a.draws[row] : 0,
                               a.keys == nullptr, a.dbg ? a.dbg + row * 2 : nullptr, &status, stamps);
   if (threadIdx.x == 0) a.out[row] = status ? status : id;
 }
 
 void launch_sample_rows(const SampleRowArgs& a, int rows, hipStream_t st) {
-  hipLaunchKernelGGL(k_sample_rows, dim3(rows), dim3(256), smem_bytes(a.n), st, a);
+  hipLaunchKernelGGL(k_sample_rows, dim3(rows), dim3(kSampleThreads), smem_bytes<kSampleThreads>(a.n), st, a);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -776,6 +803,7 @@ __device__ inline float load_logit(const AdvanceArgs& a, const float* lg, int i)
 }
 
 __device__ __attribute__((always_inline)) void advance_body(const AdvanceArgs& a, char* smem) {
+  constexpr int NT = kSampleThreads;
   const int row = blockIdx.x;
   const int slot = a.row_slot[row];
   SlotCtrl* c = a.ctrl + slot;
@@ -791,11 +819,11 @@ __device__ __attribute__((always_inline)) void advance_body(const AdvanceArgs& a
   }
   const float* lg = a.logits + (int64_t)row * a.ld;
   if (phase == kPhGlobal) {
-    const SampleSmem sm = carve(smem, 4096);
-    for (int i = threadIdx.x; i < 4096; i += 256) sm.p[i] = load_logit(a, lg, i);
+    const SampleSmem sm = carve<NT>(smem, 4096);
+    for (int i = threadIdx.x; i < 4096; i += NT) sm.p[i] = load_logit(a, lg, i);
     __syncthreads();
     int status;
-    const int id = sample_block(sm, 4096, 1.0f, 0.95f, c->top_k_g, c->gkey, c->gdraw, false,
+    const int id = sample_block<NT>(sm, 4096, 1.0f, 0.95f, c->top_k_g, c->gkey, c->gdraw, false,
                                 nullptr, &status);
     if (threadIdx.x == 0) {
       c->gdraw += 1;
@@ -807,14 +835,14 @@ __device__ __attribute__((always_inline)) void advance_body(const AdvanceArgs& a
   }
   // semantic: rows [0, 8192] (j > 8192 and the tags are -inf in the reference)
   constexpr int NS = RWKVTTS_EOS_TOKEN + 1;
-  const SampleSmem sm = carve(smem, NS);
+  const SampleSmem sm = carve<NT>(smem, NS);
   const bool eos_masked = c->fixed || (c->mode == 1 && c->n_sem < c->hard_min);
-  for (int i = threadIdx.x; i < NS; i += 256) sm.p[i] = load_logit(a, lg, i);
+  for (int i = threadIdx.x; i < NS; i += NT) sm.p[i] = load_logit(a, lg, i);
   __syncthreads();
   if (threadIdx.x == 0 && eos_masked) sm.p[RWKVTTS_EOS_TOKEN] = -__builtin_inff();
   __syncthreads();
   int status;
-  int id = sample_block(sm, NS, 1.0f, 0.95f, c->top_k_s, c->skey, c->sdraw, false, nullptr, &status);
+  int id = sample_block<NT>(sm, NS, 1.0f, 0.95f, c->top_k_s, c->skey, c->sdraw, false, nullptr, &status);
   uint64_t used = 1;
   bool stop = false;
   if (id == RWKVTTS_EOS_TOKEN) {
@@ -827,11 +855,11 @@ __device__ __attribute__((always_inline)) void advance_body(const AdvanceArgs& a
       if (wl >= 12 && ratio >= 0.7f) {
         stop = true;
       } else {  // re-draw with EOS masked from the same logits (zero_shot_inference.rs:287-297)
-        for (int i = threadIdx.x; i < NS; i += 256) sm.p[i] = load_logit(a, lg, i);
+        for (int i = threadIdx.x; i < NS; i += NT) sm.p[i] = load_logit(a, lg, i);
         __syncthreads();
         if (threadIdx.x == 0) sm.p[RWKVTTS_EOS_TOKEN] = -__builtin_inff();
         __syncthreads();
-        id = sample_block(sm, NS, 1.0f, 0.95f, c->top_k_s, c->skey, c->sdraw + 1, false, nullptr,
+        id = sample_block<NT>(sm, NS, 1.0f, 0.95f, c->top_k_s, c->skey, c->sdraw + 1, false, nullptr,
                           &status);
         used = 2;
       }
@@ -854,7 +882,7 @@ __device__ __attribute__((always_inline)) void advance_body(const AdvanceArgs& a
   }
 }
 
-__global__ __launch_bounds__(256) void k_advance(AdvanceArgs a) {
+__global__ __launch_bounds__(kSampleThreads) void k_advance(AdvanceArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   tl_begin(a.tl);
   advance_body(a, smem);
@@ -862,7 +890,8 @@ __global__ __launch_bounds__(256) void k_advance(AdvanceArgs a) {
 }
 
 int launch_advance(const AdvanceArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(k_advance, dim3(a.n_rows), dim3(256), smem_bytes(RWKVTTS_EOS_TOKEN + 1), st, a);
+  hipLaunchKernelGGL(k_advance, dim3(a.n_rows), dim3(kSampleThreads), smem_bytes<kSampleThreads>(RWKVTTS_EOS_TOKEN + 1),
+                     st, a);
   return a.n_rows;
 }
 
