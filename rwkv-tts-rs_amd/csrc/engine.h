@@ -70,6 +70,9 @@ class Engine {
   int flush_prof();
   int dump_stamps();
 
+  void state_permute(const float* std_block, float* dev_block);
+  void state_unpermute(const float* dev_block, float* std_block);
+  bool state_perm_ = false;  // WKV state blocks in k_wkv4's coalesced layout (see engine.hip)
   int device_ = 0;
   int f16_ = 0;  // fp16 matrices (else bf16): MFMA f16 and f16 activation planes
   hipStream_t stream_ = nullptr;

@@ -83,6 +83,7 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
   splitH_ = pick(C, 512);   // head: 129 col tiles x 2
   RT_CHECK(C % 128 == 0 && F % 128 == 0, RWKVTTS_EUNSUPPORTED, "K dims must be multiples of 128");
   RT_CHECK(splitA_ <= kMaxParts, RWKVTTS_EUNSUPPORTED, "n_embd too large for the WKV partial sum (raise kMaxParts)");
+  state_perm_ = wkv_perm_layout(dims.d_decay, dims.d_aaa, dims.d_mv, dims.d_gate, splitA_);
   if (const char* ex = getenv("RWKVTTS_DEBUG_EXP")) dbg_exp_ = atoi(ex);
   if (const char* gp = getenv("RWKVTTS_GEMM_STAMPS")) {
     dbg_gstamp_path_ = gp;
@@ -220,6 +221,22 @@ int Engine::slot_reset(int slot) {
   return RWKVTTS_OK;
 }
 
+// k_wkv4's state layout of one (slot, layer, head) block: thread t = 2 i + (j >= 32) of the
+// workgroup owns row i, half j >= 32; its q-th float4 (columns 32 hf + 4 q .. + 3) lives at float4
+// index q * 128 + t, so each wave-wide load / store of the state is 1 KB contiguous.
+static inline int64_t perm_index(int i, int j) {
+  const int t = 2 * i + (j >> 5), q = (j & 31) >> 2, e = j & 3;
+  return ((int64_t)q * 128 + t) * 4 + e;
+}
+void Engine::state_permute(const float* std_block, float* dev_block) {
+  for (int i = 0; i < 64; ++i)
+    for (int j = 0; j < 64; ++j) dev_block[perm_index(i, j)] = std_block[i * 64 + j];
+}
+void Engine::state_unpermute(const float* dev_block, float* std_block) {
+  for (int i = 0; i < 64; ++i)
+    for (int j = 0; j < 64; ++j) std_block[i * 64 + j] = dev_block[perm_index(i, j)];
+}
+
 int Engine::slot_read(int slot, float* out) {
   RT_CHECK(slot >= 0 && slot < S_, RWKVTTS_EINVAL, "slot out of range");
   RT_HIP(hipSetDevice(device_));
@@ -231,6 +248,10 @@ int Engine::slot_read(int slot, float* out) {
     float* o = out + l * (2 * C + HNN);
     RT_HIP(hipMemcpy(o, att_sh_ + (((int64_t)par * S_ + slot) * Lc + l) * C, C * 4, hipMemcpyDeviceToHost));
     RT_HIP(hipMemcpy(o + C, wkv_ + ((int64_t)slot * Lc + l) * HNN, HNN * 4, hipMemcpyDeviceToHost));
+    if (state_perm_) {  // device layout -> S[i][j] per head
+      std::vector<float> tmp(o + C, o + C + HNN);
+      for (int h = 0; h < H_; ++h) state_unpermute(tmp.data() + (int64_t)h * 4096, o + C + (int64_t)h * 4096);
+    }
     RT_HIP(hipMemcpy(o + C + HNN, ffn_sh_ + (((int64_t)par * S_ + slot) * Lc + l) * C, C * 4, hipMemcpyDeviceToHost));
   }
   return RWKVTTS_OK;
@@ -246,7 +267,13 @@ int Engine::slot_write(int slot, const float* in) {
   for (int64_t l = 0; l < Lc; ++l) {
     const float* o = in + l * (2 * C + HNN);
     RT_HIP(hipMemcpy(att_sh_ + (((int64_t)0 * S_ + slot) * Lc + l) * C, o, C * 4, hipMemcpyHostToDevice));
-    RT_HIP(hipMemcpy(wkv_ + ((int64_t)slot * Lc + l) * HNN, o + C, HNN * 4, hipMemcpyHostToDevice));
+    if (state_perm_) {  // S[i][j] per head -> device layout
+      std::vector<float> tmp(HNN);
+      for (int h = 0; h < H_; ++h) state_permute(o + C + (int64_t)h * 4096, tmp.data() + (int64_t)h * 4096);
+      RT_HIP(hipMemcpy(wkv_ + ((int64_t)slot * Lc + l) * HNN, tmp.data(), HNN * 4, hipMemcpyHostToDevice));
+    } else {
+      RT_HIP(hipMemcpy(wkv_ + ((int64_t)slot * Lc + l) * HNN, o + C, HNN * 4, hipMemcpyHostToDevice));
+    }
     RT_HIP(hipMemcpy(ffn_sh_ + (((int64_t)0 * S_ + slot) * Lc + l) * C, o + C + HNN, C * 4, hipMemcpyHostToDevice));
   }
   return RWKVTTS_OK;
@@ -387,6 +414,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     k.state = wkv_; k.slot_stride = (int64_t)Lc * H_ * 64 * 64; k.layer_off = (int64_t)l * H_ * 64 * 64;
     k.v_first = vfirst_; k.ldv = C; k.z_hi = z_hi_; k.z_lo = z_lo_; k.ldz = C;
     k.segs = d_segs_; k.layer = l; k.C = C; k.n_slots = S_; k.n_seg = n_seg;
+    k.perm = state_perm_ ? 1 : 0;
     k.Dw = dims.d_decay; k.Da = dims.d_aaa; k.Dv = dims.d_mv; k.Dg = dims.d_gate;
     k.stamps = (l == 5) ? dbg_stamps_ : nullptr;
     k.exp = dbg_exp_;

@@ -89,6 +89,7 @@ struct WkvArgs {
   int layer, C, Dw, Da, Dv, Dg;
   int n_slots;         // state slots (bounds the speculative slot = segment index)
   int n_seg;           // segments in this step (k_wkv3 groups SG segments per workgroup)
+  int perm;            // state blocks in k_wkv4's coalesced layout (must match wkv_perm_layout)
   int f16;             // fp16 model: LoRA-up rows and the z planes are f16
   uint64_t* stamps;    // debug: 8 s_memtime stamps per workgroup (null in production)
   int exp;             // debug experiment bits (0 in production)
@@ -103,6 +104,9 @@ void launch_embed(const uint32_t* tokens, const int4* rows, const int* ctrl_tok,
 int launch_ln_mix(const LnMixArgs& a, int n_out_rows, hipStream_t st);
 int launch_gemm(const GemmArgs& a, hipStream_t st);
 int launch_wkv(const WkvArgs& a, int n_seg, int H, hipStream_t st);
+// True when launch_wkv runs k_wkv4 for these LoRA ranks / slab count: the engine then keeps the
+// WKV state in k_wkv4's coalesced block layout.
+bool wkv_perm_layout(int Dw, int Da, int Dv, int Dg, int n_part);
 // Repack a GEMM matrix W [N][K] (K % 32 == 0) into MFMA fragment blocks (k_gemm's layout):
 // out holds ceil(N/16)*16*K elements.
 void launch_pack_frag(const bf16_t* W, int N, int K, bf16_t* out, hipStream_t st);

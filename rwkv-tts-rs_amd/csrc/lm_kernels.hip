@@ -1410,12 +1410,13 @@ __global__ __launch_bounds__(128) void k_wkv4(WkvArgs a) {
   const float rkc = a.r_k[c], lnw = a.lnx_w[c], lnb = a.lnx_b[c];
   // ---- segment-dependent loads, speculated for slot = row = segment index (decode layout)
   const int spec = blockIdx.x < a.n_slots ? blockIdx.x : 0;
-  const int64_t soff = a.layer_off + (int64_t)h * N * N + i * N + hf * 32;
+  // state block layout (engine.hip perm_index): this thread's q-th float4 at index q * 128 + t
+  const int64_t soff = a.layer_off + (int64_t)h * N * N + (int64_t)t * 4;
   float4_ S4[8];
   auto load_state = [&](int slot) {
     const float4_* Sp = (const float4_*)(a.state + (int64_t)slot * a.slot_stride + soff);
 #pragma unroll
-    for (int q = 0; q < 8; ++q) S4[q] = Sp[q];
+    for (int q = 0; q < 8; ++q) S4[q] = Sp[q * 128];
   };
   load_state(spec);
   const bool hid_thread = t < DALL / 4;
@@ -1543,7 +1544,7 @@ __global__ __launch_bounds__(128) void k_wkv4(WkvArgs a) {
     }
     if (rr + 1 == n_rows) {  // the segment's final state: stored before the GroupNorm tail
 #pragma unroll
-      for (int q = 0; q < 8; ++q) Srow[q] = S4[q];
+      for (int q = 0; q < 8; ++q) Srow[q * 128] = S4[q];
     }
     float y = y2[0] + y2[1];
     y += __shfl_xor(y, 1);
@@ -1564,11 +1565,16 @@ __global__ __launch_bounds__(128) void k_wkv4(WkvArgs a) {
   tl_end(a.tl);
 }
 
+bool wkv_perm_layout(int Dw, int Da, int Dv, int Dg, int n_part) {
+  const char* sg = getenv("RWKVTTS_WKV_SG");
+  return Dw == 64 && Da == 64 && Dv == 32 && Dg == 128 && n_part == 4 && !getenv("RWKVTTS_WKV_OLD") &&
+         !(sg && atoi(sg) != 0);
+}
 int launch_wkv(const WkvArgs& a, int n_seg, int H, hipStream_t st) {
   const dim3 grid(n_seg, H);
   if (a.Dw == 64 && a.Da == 64 && a.Dv == 32 && a.Dg == 128 && a.n_part <= 4 && !getenv("RWKVTTS_WKV_OLD")) {
     static const int sgw = getenv("RWKVTTS_WKV_SG") ? atoi(getenv("RWKVTTS_WKV_SG")) : 0;
-    if (sgw == 0 && a.n_part == 4) {
+    if (a.perm) {
       if (a.f16) hipLaunchKernelGGL((k_wkv4<true>), grid, dim3(128), 0, st, a);
       else hipLaunchKernelGGL((k_wkv4<false>), grid, dim3(128), 0, st, a);
     } else if (sgw == 2) {
