@@ -132,7 +132,10 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
   for (int l = 0; l < dims.n_layer; ++l) {
     LayerW& w = L_[l];
     bf16_t* dst = lora_pack_ + (size_t)l * C * Dtot_;
-    launch_pack_lora(w.w2t, w.a2t, w.v2t, w.g2t, C, dims.d_decay, dims.d_aaa, dims.d_mv, dims.d_gate, dst, stream_);
+    if (state_perm_)  // k_wkv4 (0.4B LoRA ranks): its coalesced register order
+      launch_pack_lora4(w.w2t, w.a2t, w.v2t, w.g2t, C, dst, stream_);
+    else
+      launch_pack_lora(w.w2t, w.a2t, w.v2t, w.g2t, C, dims.d_decay, dims.d_aaa, dims.d_mv, dims.d_gate, dst, stream_);
     RT_HIP(hipGetLastError());
     w.lup = dst;
   }

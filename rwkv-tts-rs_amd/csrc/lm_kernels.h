@@ -75,7 +75,7 @@ struct WkvArgs {
   int ldp;
   int64_t part_stride;
   const bf16_t *w2t, *a2t, *v2t, *g2t;  // LoRA-up rows [C][D] (k_wkv1)
-  const bf16_t* lup;   // LoRA-up rows packed [C][4 quarters][(Dw+Da+Dv+Dg)/4] (launch_pack_lora)
+  const bf16_t* lup;   // LoRA-up rows packed for k_wkv (launch_pack_lora) or k_wkv4 (launch_pack_lora4)
   const float *w0, *a0, *v0, *k_k, *k_a, *r_k, *lnx_w, *lnx_b;
   float* state;
   int64_t slot_stride;
@@ -110,6 +110,9 @@ bool wkv_perm_layout(int Dw, int Da, int Dv, int Dg, int n_part);
 // Repack a GEMM matrix W [N][K] (K % 32 == 0) into MFMA fragment blocks (k_gemm's layout):
 // out holds ceil(N/16)*16*K elements.
 void launch_pack_frag(const bf16_t* W, int N, int K, bf16_t* out, hipStream_t st);
+// Repack one layer's LoRA-up rows (0.4B ranks 64/64/32/128) into k_wkv4's coalesced order.
+void launch_pack_lora4(const bf16_t* w2t, const bf16_t* a2t, const bf16_t* v2t, const bf16_t* g2t, int C,
+                       bf16_t* out, hipStream_t st);
 // Repack one layer's w2t | a2t | v2t | g2t ([C][D] each) into the per-thread order of k_wkv.
 void launch_pack_lora(const bf16_t* w2t, const bf16_t* a2t, const bf16_t* v2t, const bf16_t* g2t, int C,
                       int Dw, int Da, int Dv, int Dg, bf16_t* out, hipStream_t st);

@@ -944,6 +944,31 @@ __global__ void k_pack_lora(const bf16_t* w2t, const bf16_t* a2t, const bf16_t* 
   }
 }
 
+// LoRA-up rows in k_wkv4's register order: per head h, entry u (w 0..3 | a 4..7 | v 8..9 |
+// g 10..17, 8 bf16 each) of thread t = 2 i + hf (channel 64 h + i, half hf) at uint4 index
+// (h * 18 + u) * 128 + t, so each wave-wide load is 1 KB contiguous.
+__global__ void k_pack_lora4(const bf16_t* w2t, const bf16_t* a2t, const bf16_t* v2t, const bf16_t* g2t, int C,
+                             bf16_t* out) {
+  const int64_t total = (int64_t)(C / 64) * 18 * 128;
+  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int t = (int)(idx % 128), u = (int)((idx / 128) % 18), h = (int)(idx / (128 * 18));
+    const int c = h * 64 + (t >> 1), hf = t & 1;
+    const bf16_t* src;
+    if (u < 4) src = w2t + (int64_t)c * 64 + hf * 32 + u * 8;
+    else if (u < 8) src = a2t + (int64_t)c * 64 + hf * 32 + (u - 4) * 8;
+    else if (u < 10) src = v2t + (int64_t)c * 32 + hf * 16 + (u - 8) * 8;
+    else src = g2t + (int64_t)c * 128 + hf * 64 + (u - 10) * 8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) out[idx * 8 + e] = src[e];
+  }
+}
+
+void launch_pack_lora4(const bf16_t* w2t, const bf16_t* a2t, const bf16_t* v2t, const bf16_t* g2t, int C,
+                       bf16_t* out, hipStream_t st) {
+  hipLaunchKernelGGL(k_pack_lora4, dim3(256), dim3(256), 0, st, w2t, a2t, v2t, g2t, C, out);
+}
+
 void launch_pack_lora(const bf16_t* w2t, const bf16_t* a2t, const bf16_t* v2t, const bf16_t* g2t, int C,
                       int Dw, int Da, int Dv, int Dg, bf16_t* out, hipStream_t st) {
   hipLaunchKernelGGL(k_pack_lora, dim3(1024), dim3(256), 0, st, w2t, a2t, v2t, g2t, C, Dw, Da, Dv, Dg, out);
@@ -1392,19 +1417,10 @@ __global__ __launch_bounds__(128) void k_wkv4(WkvArgs a) {
   const int4 sg = a.segs[blockIdx.x];
   // ---- head-only loads: half of channel c's LoRA-up rows + parameters
   uint4 lw[18];  // 8 bf16 per entry: w 0..3 | a 4..7 | v 8..9 | g 10..17
-  {
-    const uint4* pw = (const uint4*)(a.w2t + (int64_t)c * DW + hf * (DW / 2));
-    const uint4* pa = (const uint4*)(a.a2t + (int64_t)c * DA + hf * (DA / 2));
-    const uint4* pv = (const uint4*)(a.v2t + (int64_t)c * DV + hf * (DV / 2));
-    const uint4* pg = (const uint4*)(a.g2t + (int64_t)c * DG + hf * (DG / 2));
+  {  // packed per head by launch_pack_lora4: entry u of thread t at uint4 index u * 128 + t
+    const uint4* pl = (const uint4*)(a.lup + (int64_t)h * 18 * 128 * 8);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) lw[u] = pw[u];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) lw[4 + u] = pa[u];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) lw[8 + u] = pv[u];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) lw[10 + u] = pg[u];
+    for (int u = 0; u < 18; ++u) lw[u] = pl[u * 128 + t];
   }
   const float w0 = a.w0[c], a0 = a.a0[c], v0 = a.v0[c], kkc = a.k_k[c], kac = a.k_a[c];
   const float rkc = a.r_k[c], lnw = a.lnx_w[c], lnb = a.lnx_b[c];
