@@ -411,6 +411,10 @@ __device__ float exact_seq_sum(const SampleSmem& sm, int n, uint64_t* stamps = n
     float s = 0.0f;
     int c = 0;
     while (c < nch) {
+      // s and c are wave-uniform; say so, so that the walk runs on scalar registers and scalar
+      // branches (readlane with an SGPR lane select) instead of divergent-looking VGPR code
+      s = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, s)));
+      c = __builtin_amdgcn_readfirstlane(c);
       const uint32_t sb2 = __builtin_bit_cast(uint32_t, s);
       const int ef = (int)((sb2 >> 23) & 0xFFu);
       const bool is_head = (heads >> c) & 1ull;
@@ -429,11 +433,15 @@ __device__ float exact_seq_sum(const SampleSmem& sm, int n, uint64_t* stamps = n
       // unusable chunk, or a run whose prediction failed: add chunk c in order on one lane
       const int b0 = c * CH, e0 = min(n, b0 + CH);
       float t = 0.0f;
+      const uint64_t fb0 = stamps ? __builtin_amdgcn_s_memtime() : 0;
       if (lane == 0) t = lane_serial_add<NE>(s, sm.p, b0, e0);
       s = readlane_f(t, 0);
+      if (stamps && tid == 0) stamps[15] += __builtin_amdgcn_s_memtime() + (uint64_t)(s != s) - fb0;
       ++c;
       // the chunks after c (if inside a run) are no longer run heads; step them one at a time
       while (c < nch && !((heads >> c) & 1ull)) {
+        s = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, s)));
+        c = __builtin_amdgcn_readfirstlane(c);
         const uint32_t sb3 = __builtin_bit_cast(uint32_t, s);
         const int ef3 = (int)((sb3 >> 23) & 0xFFu);
         bool fast = false;
@@ -449,8 +457,10 @@ __device__ float exact_seq_sum(const SampleSmem& sm, int n, uint64_t* stamps = n
         if (!fast) {
           const int b1 = c * CH, e1 = min(n, b1 + CH);
           float t1 = 0.0f;
+          const uint64_t fb1 = stamps ? __builtin_amdgcn_s_memtime() : 0;
           if (lane == 0) t1 = lane_serial_add<NE>(s, sm.p, b1, e1);
           s = readlane_f(t1, 0);
+          if (stamps && tid == 0) stamps[15] += __builtin_amdgcn_s_memtime() + (uint64_t)(s != s) - fb1;
         }
         ++c;
       }
