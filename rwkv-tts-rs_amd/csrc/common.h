@@ -1,6 +1,7 @@
 // common.h -- shared host/device helpers for the MI355X (gfx950) RWKV-TTS hot path.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 #include <string>
 
@@ -111,5 +112,31 @@ __device__ inline void tl_end(unsigned long long* tl) {
   if (tl && threadIdx.x == 0) atomicMax(&tl[2 + (tl_block() & 63)], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 #endif
 }
+
+// Kernel launches of the LM / sampler path go through RT_LAUNCH. While the engine has a
+// profiling window open (Engine::prof_begin .. prof_end) the launch carries the window's HIP
+// events (hipExtLaunchKernelGGL): they are stamped by the kernel's own dispatch packet, so the
+// elapsed time is the kernel's execution interval (what rocprofv3 --kernel-trace reports), not
+// the queue gap an event marker before it would add. The first launch of a window stamps the
+// start, every launch the stop. Outside a window this is a plain hipLaunchKernelGGL.
+struct LaunchTiming {
+  hipEvent_t start = nullptr, stop = nullptr;
+  int launches = 0;
+};
+inline LaunchTiming& launch_timing() {
+  static thread_local LaunchTiming t;
+  return t;
+}
+#define RT_LAUNCH(K, G, B, SH, ST, ...)                                                              \
+  do {                                                                                               \
+    ::rwkvtts::LaunchTiming& lt_ = ::rwkvtts::launch_timing();                                       \
+    if (lt_.stop) {                                                                                  \
+      hipExtLaunchKernelGGL(K, G, B, SH, ST, lt_.launches == 0 ? lt_.start : nullptr, lt_.stop, 0u, \
+                            __VA_ARGS__);                                                            \
+      ++lt_.launches;                                                                                \
+    } else {                                                                                         \
+      hipLaunchKernelGGL(K, G, B, SH, ST, __VA_ARGS__);                                              \
+    }                                                                                                \
+  } while (0)
 
 }  // namespace rwkvtts

@@ -302,19 +302,27 @@ __global__ void k_flip_parity(const int4* segs, int* slot_par, int n_seg) {
   if (s < n_seg) slot_par[segs[s].x] ^= 1;
 }
 
+// Profiling window around one launcher call: the launches inside stamp the two events with
+// their own start / end (RT_LAUNCH, common.h). A window whose launcher issued nothing (an
+// ablated kernel) gets plain markers.
 void Engine::prof_begin(hipEvent_t* ev) {
   *ev = nullptr;
   if (!profiling) return;
+  hipEvent_t e2;
   hipEventCreate(ev);
-  hipEventRecord(*ev, stream_);
+  hipEventCreate(&e2);
+  launch_timing() = LaunchTiming{*ev, e2, 0};
 }
 void Engine::prof_end(const char* name, hipEvent_t ev) {
   if (!profiling || !ev) return;
-  hipEvent_t e2;
-  hipEventCreate(&e2);
-  hipEventRecord(e2, stream_);
-  pending_prof_.push_back({std::string(name) + "#begin", ev});
-  pending_prof_.push_back({name, e2});
+  LaunchTiming& lt = launch_timing();
+  if (lt.launches == 0) {
+    hipEventRecord(lt.start, stream_);
+    hipEventRecord(lt.stop, stream_);
+  }
+  pending_prof_.push_back({std::string(name) + "#begin", lt.start});
+  pending_prof_.push_back({name, lt.stop});
+  lt = LaunchTiming{};
 }
 int Engine::flush_prof() {
   if (pending_prof_.empty()) return RWKVTTS_OK;

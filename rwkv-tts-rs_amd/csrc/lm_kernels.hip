@@ -826,7 +826,7 @@ __global__ __launch_bounds__(256, 2) void k_wkv(WkvArgs a) {
 void launch_embed(const uint32_t* tokens, const int4* rows, const int* ctrl_tok, int ctrl_stride,
                   const bf16_t* emb, const float* w, const float* b, float* h, int R, int C, int f16, hipStream_t st,
                   unsigned long long* tl, int n_vocab) {
-  hipLaunchKernelGGL(k_embed, dim3(R), dim3(256), 0, st, tokens, rows, ctrl_tok, ctrl_stride, emb, w, b, h, C, f16, tl,
+  RT_LAUNCH(k_embed, dim3(R), dim3(256), 0, st, tokens, rows, ctrl_tok, ctrl_stride, emb, w, b, h, C, f16, tl,
                      n_vocab);
 }
 int launch_ln_mix(const LnMixArgs& a, int n_out_rows, hipStream_t st) {
@@ -838,9 +838,9 @@ int launch_ln_mix(const LnMixArgs& a, int n_out_rows, hipStream_t st) {
       (a.n_part == 0 || a.n_part == 8 || a.n_part == 16)) {
 #define LN_CASE(F, MO, NM)                                                                                  \
   switch (a.n_part) {                                                                                      \
-    case 0: hipLaunchKernelGGL((k_ln1024<F, MO, NM, 0>), grid, dim3(256), 0, st, b); break;                \
-    case 8: hipLaunchKernelGGL((k_ln1024<F, MO, NM, 8>), grid, dim3(256), 0, st, b); break;                \
-    default: hipLaunchKernelGGL((k_ln1024<F, MO, NM, 16>), grid, dim3(256), 0, st, b); break;              \
+    case 0: RT_LAUNCH((k_ln1024<F, MO, NM, 0>), grid, dim3(256), 0, st, b); break;                \
+    case 8: RT_LAUNCH((k_ln1024<F, MO, NM, 8>), grid, dim3(256), 0, st, b); break;                \
+    default: RT_LAUNCH((k_ln1024<F, MO, NM, 16>), grid, dim3(256), 0, st, b); break;              \
   }
     if (a.f16) {
       if (!a.shift) { LN_CASE(true, 0, 0) } else if (a.n_mix == 6) { LN_CASE(true, 1, 6) } else { LN_CASE(true, 1, 1) }
@@ -852,13 +852,13 @@ int launch_ln_mix(const LnMixArgs& a, int n_out_rows, hipStream_t st) {
   }
   if (a.C <= 1024) {
     switch (a.n_part) {  // slab counts of the 0.4B configuration: every load in flight at once
-      case 0: hipLaunchKernelGGL((k_ln_mix<1, 0>), grid, dim3(256), 0, st, b); break;
-      case 8: hipLaunchKernelGGL((k_ln_mix<1, 8>), grid, dim3(256), 0, st, b); break;
-      case 16: hipLaunchKernelGGL((k_ln_mix<1, 16>), grid, dim3(256), 0, st, b); break;
-      default: hipLaunchKernelGGL((k_ln_mix<1, -1>), grid, dim3(256), 0, st, b); break;
+      case 0: RT_LAUNCH((k_ln_mix<1, 0>), grid, dim3(256), 0, st, b); break;
+      case 8: RT_LAUNCH((k_ln_mix<1, 8>), grid, dim3(256), 0, st, b); break;
+      case 16: RT_LAUNCH((k_ln_mix<1, 16>), grid, dim3(256), 0, st, b); break;
+      default: RT_LAUNCH((k_ln_mix<1, -1>), grid, dim3(256), 0, st, b); break;
     }
   } else {
-    hipLaunchKernelGGL((k_ln_mix<2, -1>), grid, dim3(256), 0, st, b);
+    RT_LAUNCH((k_ln_mix<2, -1>), grid, dim3(256), 0, st, b);
   }
   return n_out_rows;
 }
@@ -869,22 +869,22 @@ static void launch_gemm_t(const GemmArgs& a, dim3 grid, hipStream_t st) {
   static const bool v2 = !getenv("RWKVTTS_GEMM_OLD");
   if (v2 && (a.xmode == kXPlanes || a.x_nsplit == 4 || a.x_nsplit == 2) && a.stamps == nullptr && a.exp == 0) {
     if (a.f16) {
-      if (a.xmode == kXPlanes) hipLaunchKernelGGL((k_gemm2<MT, KSTEPS, kXPlanes, true, 1>), grid, dim3(256), lds, st, a);
-      else if (a.x_nsplit == 4) hipLaunchKernelGGL((k_gemm2<MT, KSTEPS, kXRelu2, true, 4>), grid, dim3(256), lds, st, a);
-      else hipLaunchKernelGGL((k_gemm2<MT, KSTEPS, kXRelu2, true, 2>), grid, dim3(256), lds, st, a);
+      if (a.xmode == kXPlanes) RT_LAUNCH((k_gemm2<MT, KSTEPS, kXPlanes, true, 1>), grid, dim3(256), lds, st, a);
+      else if (a.x_nsplit == 4) RT_LAUNCH((k_gemm2<MT, KSTEPS, kXRelu2, true, 4>), grid, dim3(256), lds, st, a);
+      else RT_LAUNCH((k_gemm2<MT, KSTEPS, kXRelu2, true, 2>), grid, dim3(256), lds, st, a);
     } else {
-      if (a.xmode == kXPlanes) hipLaunchKernelGGL((k_gemm2<MT, KSTEPS, kXPlanes, false, 1>), grid, dim3(256), lds, st, a);
-      else if (a.x_nsplit == 4) hipLaunchKernelGGL((k_gemm2<MT, KSTEPS, kXRelu2, false, 4>), grid, dim3(256), lds, st, a);
-      else hipLaunchKernelGGL((k_gemm2<MT, KSTEPS, kXRelu2, false, 2>), grid, dim3(256), lds, st, a);
+      if (a.xmode == kXPlanes) RT_LAUNCH((k_gemm2<MT, KSTEPS, kXPlanes, false, 1>), grid, dim3(256), lds, st, a);
+      else if (a.x_nsplit == 4) RT_LAUNCH((k_gemm2<MT, KSTEPS, kXRelu2, false, 4>), grid, dim3(256), lds, st, a);
+      else RT_LAUNCH((k_gemm2<MT, KSTEPS, kXRelu2, false, 2>), grid, dim3(256), lds, st, a);
     }
     return;
   }
   if (a.f16) {
-    if (a.xmode == kXPlanes) hipLaunchKernelGGL((k_gemm<MT, KSTEPS, kXPlanes, true>), grid, dim3(256), lds, st, a);
-    else hipLaunchKernelGGL((k_gemm<MT, KSTEPS, kXRelu2, true>), grid, dim3(256), lds, st, a);
+    if (a.xmode == kXPlanes) RT_LAUNCH((k_gemm<MT, KSTEPS, kXPlanes, true>), grid, dim3(256), lds, st, a);
+    else RT_LAUNCH((k_gemm<MT, KSTEPS, kXRelu2, true>), grid, dim3(256), lds, st, a);
   } else {
-    if (a.xmode == kXPlanes) hipLaunchKernelGGL((k_gemm<MT, KSTEPS, kXPlanes, false>), grid, dim3(256), lds, st, a);
-    else hipLaunchKernelGGL((k_gemm<MT, KSTEPS, kXRelu2, false>), grid, dim3(256), lds, st, a);
+    if (a.xmode == kXPlanes) RT_LAUNCH((k_gemm<MT, KSTEPS, kXPlanes, false>), grid, dim3(256), lds, st, a);
+    else RT_LAUNCH((k_gemm<MT, KSTEPS, kXRelu2, false>), grid, dim3(256), lds, st, a);
   }
 }
 
@@ -925,7 +925,7 @@ __global__ void k_pack_frag(const bf16_t* W, int N, int K, bf16_t* out) {
 }
 
 void launch_pack_frag(const bf16_t* W, int N, int K, bf16_t* out, hipStream_t st) {
-  hipLaunchKernelGGL(k_pack_frag, dim3(4096), dim3(256), 0, st, W, N, K, out);
+  RT_LAUNCH(k_pack_frag, dim3(4096), dim3(256), 0, st, W, N, K, out);
 }
 
 __global__ void k_pack_lora(const bf16_t* w2t, const bf16_t* a2t, const bf16_t* v2t, const bf16_t* g2t, int C,
@@ -966,12 +966,12 @@ __global__ void k_pack_lora4(const bf16_t* w2t, const bf16_t* a2t, const bf16_t*
 
 void launch_pack_lora4(const bf16_t* w2t, const bf16_t* a2t, const bf16_t* v2t, const bf16_t* g2t, int C,
                        bf16_t* out, hipStream_t st) {
-  hipLaunchKernelGGL(k_pack_lora4, dim3(256), dim3(256), 0, st, w2t, a2t, v2t, g2t, C, out);
+  RT_LAUNCH(k_pack_lora4, dim3(256), dim3(256), 0, st, w2t, a2t, v2t, g2t, C, out);
 }
 
 void launch_pack_lora(const bf16_t* w2t, const bf16_t* a2t, const bf16_t* v2t, const bf16_t* g2t, int C,
                       int Dw, int Da, int Dv, int Dg, bf16_t* out, hipStream_t st) {
-  hipLaunchKernelGGL(k_pack_lora, dim3(1024), dim3(256), 0, st, w2t, a2t, v2t, g2t, C, Dw, Da, Dv, Dg, out);
+  RT_LAUNCH(k_pack_lora, dim3(1024), dim3(256), 0, st, w2t, a2t, v2t, g2t, C, Dw, Da, Dv, Dg, out);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1591,29 +1591,29 @@ int launch_wkv(const WkvArgs& a, int n_seg, int H, hipStream_t st) {
   if (a.Dw == 64 && a.Da == 64 && a.Dv == 32 && a.Dg == 128 && a.n_part <= 4 && !getenv("RWKVTTS_WKV_OLD")) {
     static const int sgw = getenv("RWKVTTS_WKV_SG") ? atoi(getenv("RWKVTTS_WKV_SG")) : 0;
     if (a.perm) {
-      if (a.f16) hipLaunchKernelGGL((k_wkv4<true>), grid, dim3(128), 0, st, a);
-      else hipLaunchKernelGGL((k_wkv4<false>), grid, dim3(128), 0, st, a);
+      if (a.f16) RT_LAUNCH((k_wkv4<true>), grid, dim3(128), 0, st, a);
+      else RT_LAUNCH((k_wkv4<false>), grid, dim3(128), 0, st, a);
     } else if (sgw == 2) {
-      hipLaunchKernelGGL((k_wkv3<64, 64, 32, 128, 4, 2>), dim3((n_seg + 1) / 2, H), dim3(256), 0, st, a);
+      RT_LAUNCH((k_wkv3<64, 64, 32, 128, 4, 2>), dim3((n_seg + 1) / 2, H), dim3(256), 0, st, a);
     } else if (sgw == 4) {
-      hipLaunchKernelGGL((k_wkv3<64, 64, 32, 128, 4, 4>), dim3((n_seg + 3) / 4, H), dim3(512), 0, st, a);
+      RT_LAUNCH((k_wkv3<64, 64, 32, 128, 4, 4>), dim3((n_seg + 3) / 4, H), dim3(512), 0, st, a);
     } else {
-      hipLaunchKernelGGL((k_wkv2<64, 64, 32, 128, 4>), grid, dim3(128), 0, st, a);
+      RT_LAUNCH((k_wkv2<64, 64, 32, 128, 4>), grid, dim3(128), 0, st, a);
     }
     return n_seg * H;
   }
   if (a.Dw == 16 && a.Da == 16 && a.Dv == 16 && a.Dg == 32 && a.n_part <= 1 && !getenv("RWKVTTS_WKV_OLD")) {
-    hipLaunchKernelGGL((k_wkv2<16, 16, 16, 32, 1>), grid, dim3(128), 0, st, a);
+    RT_LAUNCH((k_wkv2<16, 16, 16, 32, 1>), grid, dim3(128), 0, st, a);
     return n_seg * H;
   }
   if (a.Dw == 32 && a.Da == 32 && a.Dv == 16 && a.Dg == 64 && a.n_part <= 1 && !getenv("RWKVTTS_WKV_OLD")) {
-    hipLaunchKernelGGL((k_wkv2<32, 32, 16, 64, 1>), grid, dim3(128), 0, st, a);
+    RT_LAUNCH((k_wkv2<32, 32, 16, 64, 1>), grid, dim3(128), 0, st, a);
     return n_seg * H;
   }
   const int units = (a.Dw + a.Da + a.Dv + a.Dg + 15) / 16;
-  if (units <= 8 && a.n_part <= 4) hipLaunchKernelGGL((k_wkv<8, 4>), grid, dim3(256), 0, st, a);
-  else if (units <= 20 && a.n_part <= 4) hipLaunchKernelGGL((k_wkv<20, 4>), grid, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((k_wkv<32, 8>), grid, dim3(256), 0, st, a);
+  if (units <= 8 && a.n_part <= 4) RT_LAUNCH((k_wkv<8, 4>), grid, dim3(256), 0, st, a);
+  else if (units <= 20 && a.n_part <= 4) RT_LAUNCH((k_wkv<20, 4>), grid, dim3(256), 0, st, a);
+  else RT_LAUNCH((k_wkv<32, 8>), grid, dim3(256), 0, st, a);
   return n_seg * H;
 }
 

@@ -800,7 +800,7 @@ __global__ __launch_bounds__(kSampleThreads) void k_sample_rows(SampleRowArgs a)
 }
 
 void launch_sample_rows(const SampleRowArgs& a, int rows, hipStream_t st) {
-  hipLaunchKernelGGL(k_sample_rows, dim3(rows), dim3(kSampleThreads), smem_bytes<kSampleThreads>(a.n), st, a);
+  RT_LAUNCH(k_sample_rows, dim3(rows), dim3(kSampleThreads), smem_bytes<kSampleThreads>(a.n), st, a);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -900,7 +900,7 @@ __global__ __launch_bounds__(kSampleThreads) void k_advance(AdvanceArgs a) {
 }
 
 int launch_advance(const AdvanceArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(k_advance, dim3(a.n_rows), dim3(kSampleThreads), smem_bytes<kSampleThreads>(RWKVTTS_EOS_TOKEN + 1),
+  RT_LAUNCH(k_advance, dim3(a.n_rows), dim3(kSampleThreads), smem_bytes<kSampleThreads>(RWKVTTS_EOS_TOKEN + 1),
                      st, a);
   return a.n_rows;
 }
