@@ -429,7 +429,12 @@ class Codec {
                    (d.up_kernels[i] + d.up_rates[i] - 1) / d.up_rates[i] <= 8,
                RWKVTTS_EINVAL, "codec: ConvTranspose needs k >= s, even k - s and <= 8 taps per phase");
     RT_HIP(hipSetDevice(device));
-    RT_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    {  // lowest queue priority: the LM decode chain (engine.hip) goes first when both share the GPU
+      int least = 0, greatest = 0;
+      RT_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+      if (getenv("RWKVTTS_NO_PRIO")) least = 0;
+      RT_HIP(hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, least));
+    }
 #define RT_CONV_ATTR(TN, KT) \
     RT_HIP(hipFuncSetAttribute((const void*)k_conv<TN, KT>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     RT_CONV_ATTR(32, 1) RT_CONV_ATTR(32, 3) RT_CONV_ATTR(32, 7)

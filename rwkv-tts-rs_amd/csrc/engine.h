@@ -72,7 +72,7 @@ class Engine {
 
   void state_permute(const float* std_block, float* dev_block);
   void state_unpermute(const float* dev_block, float* std_block);
-  bool state_perm_ = false;  // WKV state blocks in k_wkv4's coalesced layout (see engine.hip)
+  int state_perm_ = 0;  // WKV state block layout (wkv_perm_layout; engine.hip perm_index)
   int device_ = 0;
   int f16_ = 0;  // fp16 matrices (else bf16): MFMA f16 and f16 activation planes
   hipStream_t stream_ = nullptr;

@@ -41,7 +41,13 @@ Engine::~Engine() {
 int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t bytes, int on_device) {
   device_ = desc.device;
   RT_HIP(hipSetDevice(device_));
-  RT_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  {  // the token generator's latency-bound launch chain gets the highest queue priority, so a
+     // vocoder sharing the GPU (codec.hip: lowest) fills the CUs it leaves idle
+    int least = 0, greatest = 0;
+    RT_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    if (getenv("RWKVTTS_NO_PRIO")) greatest = 0;
+    RT_HIP(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, greatest));
+  }
 
   rwkvtts_blob_header hdr;
   if (on_device) {
@@ -83,7 +89,7 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
   splitH_ = pick(C, 512);   // head: 129 col tiles x 2
   RT_CHECK(C % 128 == 0 && F % 128 == 0, RWKVTTS_EUNSUPPORTED, "K dims must be multiples of 128");
   RT_CHECK(splitA_ <= kMaxParts, RWKVTTS_EUNSUPPORTED, "n_embd too large for the WKV partial sum (raise kMaxParts)");
-  state_perm_ = wkv_perm_layout(dims.d_decay, dims.d_aaa, dims.d_mv, dims.d_gate, splitA_);
+  state_perm_ = wkv_perm_layout(dims.d_decay, dims.d_aaa, dims.d_mv, dims.d_gate, splitA_, S_);
   if (const char* ex = getenv("RWKVTTS_DEBUG_EXP")) dbg_exp_ = atoi(ex);
   if (const char* gp = getenv("RWKVTTS_GEMM_STAMPS")) {
     dbg_gstamp_path_ = gp;
@@ -132,7 +138,9 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
   for (int l = 0; l < dims.n_layer; ++l) {
     LayerW& w = L_[l];
     bf16_t* dst = lora_pack_ + (size_t)l * C * Dtot_;
-    if (state_perm_)  // k_wkv4 (0.4B LoRA ranks): its coalesced register order
+    if (state_perm_ == 2)  // k_wkv6 (0.4B LoRA ranks): its coalesced register order
+      launch_pack_lora6(w.w2t, w.a2t, w.v2t, w.g2t, C, dst, stream_);
+    else if (state_perm_ == 1)  // k_wkv4
       launch_pack_lora4(w.w2t, w.a2t, w.v2t, w.g2t, C, dst, stream_);
     else
       launch_pack_lora(w.w2t, w.a2t, w.v2t, w.g2t, C, dims.d_decay, dims.d_aaa, dims.d_mv, dims.d_gate, dst, stream_);
@@ -224,20 +232,25 @@ int Engine::slot_reset(int slot) {
   return RWKVTTS_OK;
 }
 
-// k_wkv4's state layout of one (slot, layer, head) block: thread t = 2 i + (j >= 32) of the
-// workgroup owns row i, half j >= 32; its q-th float4 (columns 32 hf + 4 q .. + 3) lives at float4
-// index q * 128 + t, so each wave-wide load / store of the state is 1 KB contiguous.
-static inline int64_t perm_index(int i, int j) {
-  const int t = 2 * i + (j >> 5), q = (j & 31) >> 2, e = j & 3;
-  return ((int64_t)q * 128 + t) * 4 + e;
+// Coalesced state layouts of one (slot, layer, head) block, in the WKV kernel's register order:
+// layout 1 (k_wkv4): thread t = 2 i + (j >> 5) owns row i, half j >> 5; its q-th float4 (columns
+// 32 hf + 4 q .. + 3) lives at float4 index q * 128 + t. Layout 2 (k_wkv6): t = 4 i + (j >> 4),
+// q-th float4 at q * 256 + t. Either way each wave-wide load / store is 1 KB contiguous.
+static inline int64_t perm_index(int kind, int i, int j) {
+  if (kind == 1) {
+    const int t = 2 * i + (j >> 5), q = (j & 31) >> 2, e = j & 3;
+    return ((int64_t)q * 128 + t) * 4 + e;
+  }
+  const int t = 4 * i + (j >> 4), q = (j & 15) >> 2, e = j & 3;
+  return ((int64_t)q * 256 + t) * 4 + e;
 }
 void Engine::state_permute(const float* std_block, float* dev_block) {
   for (int i = 0; i < 64; ++i)
-    for (int j = 0; j < 64; ++j) dev_block[perm_index(i, j)] = std_block[i * 64 + j];
+    for (int j = 0; j < 64; ++j) dev_block[perm_index(state_perm_, i, j)] = std_block[i * 64 + j];
 }
 void Engine::state_unpermute(const float* dev_block, float* std_block) {
   for (int i = 0; i < 64; ++i)
-    for (int j = 0; j < 64; ++j) std_block[i * 64 + j] = dev_block[perm_index(i, j)];
+    for (int j = 0; j < 64; ++j) std_block[i * 64 + j] = dev_block[perm_index(state_perm_, i, j)];
 }
 
 int Engine::slot_read(int slot, float* out) {
@@ -425,7 +438,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     k.state = wkv_; k.slot_stride = (int64_t)Lc * H_ * 64 * 64; k.layer_off = (int64_t)l * H_ * 64 * 64;
     k.v_first = vfirst_; k.ldv = C; k.z_hi = z_hi_; k.z_lo = z_lo_; k.ldz = C;
     k.segs = d_segs_; k.layer = l; k.C = C; k.n_slots = S_; k.n_seg = n_seg;
-    k.perm = state_perm_ ? 1 : 0;
+    k.perm = state_perm_;
     k.Dw = dims.d_decay; k.Da = dims.d_aaa; k.Dv = dims.d_mv; k.Dg = dims.d_gate;
     k.stamps = (l == 5) ? dbg_stamps_ : nullptr;
     k.exp = dbg_exp_;

@@ -88,8 +88,8 @@ struct WkvArgs {
   const int4* segs;    // slot, row_begin, n_rows, _
   int layer, C, Dw, Da, Dv, Dg;
   int n_slots;         // state slots (bounds the speculative slot = segment index)
-  int n_seg;           // segments in this step (k_wkv3 groups SG segments per workgroup)
-  int perm;            // state blocks in k_wkv4's coalesced layout (must match wkv_perm_layout)
+  int n_seg;           // segments in this step 
+  int perm;            // state block layout (wkv_perm_layout): 0 row-major, 1 k_wkv4, 2 k_wkv6
   int f16;             // fp16 model: LoRA-up rows and the z planes are f16
   uint64_t* stamps;    // debug: 8 s_memtime stamps per workgroup (null in production)
   int exp;             // debug experiment bits (0 in production)
@@ -104,14 +104,16 @@ void launch_embed(const uint32_t* tokens, const int4* rows, const int* ctrl_tok,
 int launch_ln_mix(const LnMixArgs& a, int n_out_rows, hipStream_t st);
 int launch_gemm(const GemmArgs& a, hipStream_t st);
 int launch_wkv(const WkvArgs& a, int n_seg, int H, hipStream_t st);
-// True when launch_wkv runs k_wkv4 for these LoRA ranks / slab count: the engine then keeps the
-// WKV state in k_wkv4's coalesced block layout.
-bool wkv_perm_layout(int Dw, int Da, int Dv, int Dg, int n_part);
+// Which coalesced WKV state layout launch_wkv expects for these LoRA ranks / slab count: 0 none
+// (row-major S[i][j]), 1 k_wkv4 (two waves per block, the default), 2 k_wkv6 (four waves).
+int wkv_perm_layout(int Dw, int Da, int Dv, int Dg, int n_part, int max_slots);
 // Repack a GEMM matrix W [N][K] (K % 32 == 0) into MFMA fragment blocks (k_gemm's layout):
 // out holds ceil(N/16)*16*K elements.
 void launch_pack_frag(const bf16_t* W, int N, int K, bf16_t* out, hipStream_t st);
 // Repack one layer's LoRA-up rows (0.4B ranks 64/64/32/128) into k_wkv4's coalesced order.
 void launch_pack_lora4(const bf16_t* w2t, const bf16_t* a2t, const bf16_t* v2t, const bf16_t* g2t, int C,
+                       bf16_t* out, hipStream_t st);
+void launch_pack_lora6(const bf16_t* w2t, const bf16_t* a2t, const bf16_t* v2t, const bf16_t* g2t, int C,
                        bf16_t* out, hipStream_t st);
 // Repack one layer's w2t | a2t | v2t | g2t ([C][D] each) into the per-thread order of k_wkv.
 void launch_pack_lora(const bf16_t* w2t, const bf16_t* a2t, const bf16_t* v2t, const bf16_t* g2t, int C,

@@ -969,6 +969,29 @@ void launch_pack_lora4(const bf16_t* w2t, const bf16_t* a2t, const bf16_t* v2t, 
   RT_LAUNCH(k_pack_lora4, dim3(256), dim3(256), 0, st, w2t, a2t, v2t, g2t, C, out);
 }
 
+// k_wkv6's register order: thread t = 4 i + qq holds quarter qq of channel c = 64 h + i's rows
+// (w 16 | a 16 | v 8 | g 32 values = 9 entries of 8); entry u of thread t at uint4 u * 256 + t.
+__global__ void k_pack_lora6(const bf16_t* w2t, const bf16_t* a2t, const bf16_t* v2t, const bf16_t* g2t, int C,
+                             bf16_t* out) {
+  const int64_t total = (int64_t)(C / 64) * 9 * 256;
+  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int t = (int)(idx % 256), u = (int)((idx / 256) % 9), h = (int)(idx / (256 * 9));
+    const int c = h * 64 + (t >> 2), qq = t & 3;
+    const bf16_t* src;
+    if (u < 2) src = w2t + (int64_t)c * 64 + qq * 16 + u * 8;
+    else if (u < 4) src = a2t + (int64_t)c * 64 + qq * 16 + (u - 2) * 8;
+    else if (u == 4) src = v2t + (int64_t)c * 32 + qq * 8;
+    else src = g2t + (int64_t)c * 128 + qq * 32 + (u - 5) * 8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) out[idx * 8 + e] = src[e];
+  }
+}
+void launch_pack_lora6(const bf16_t* w2t, const bf16_t* a2t, const bf16_t* v2t, const bf16_t* g2t, int C,
+                       bf16_t* out, hipStream_t st) {
+  RT_LAUNCH(k_pack_lora6, dim3(256), dim3(256), 0, st, w2t, a2t, v2t, g2t, C, out);
+}
+
 void launch_pack_lora(const bf16_t* w2t, const bf16_t* a2t, const bf16_t* v2t, const bf16_t* g2t, int C,
                       int Dw, int Da, int Dv, int Dg, bf16_t* out, hipStream_t st) {
   RT_LAUNCH(k_pack_lora, dim3(1024), dim3(256), 0, st, w2t, a2t, v2t, g2t, C, Dw, Da, Dv, Dg, out);
@@ -1162,222 +1185,6 @@ __global__ __launch_bounds__(128) void k_wkv2(WkvArgs a) {
     *(float4_*)(Srow + q * 4) = v4;
   }
   if (stp) stp[5] = __builtin_amdgcn_s_memtime();
-}
-
-// ------------------------------------------------------------------------------------
-// wkv3: k_wkv2's per-(segment, head) arithmetic, SG segments per workgroup (128 threads each).
-// The head's LoRA-up rows (64 channels x (Dw+Da+Dv+Dg) bf16, 36 KB at the 0.4B dims) are staged
-// in LDS once per workgroup and shared by its SG segments, which divides the L2 -> CU traffic
-// of these rows (re-read by every slot in k_wkv2) by SG. Barriers are workgroup-wide; groups
-// whose segment has fewer rows (prefill) idle through the extra iterations.
-// ------------------------------------------------------------------------------------
-template <int DW, int DA, int DV, int DG, int MAXP, int SG>
-__global__ __launch_bounds__(128 * SG) void k_wkv3(WkvArgs a) {
-  constexpr int N = 64, DALL = DW + DA + DV + DG;
-  constexpr int LWS = DALL + 8;  // LDS row stride (bf16): +16 B spreads the channel rows over banks
-  __shared__ __attribute__((aligned(16))) bf16_t s_lw[N * LWS];
-  __shared__ __attribute__((aligned(16))) float s_hid[SG][DALL];
-  __shared__ __attribute__((aligned(16))) float s_vec[SG][5][N];  // w, kk (unnormalised), a, k, r
-  __shared__ float s_red[SG][4][2];
-  const int tid = threadIdx.x, grp = tid >> 7, t = tid & 127;
-  const int lane = t & 63, wave = t >> 6, i = t >> 1, hf = t & 1;
-  const int h = blockIdx.y, C = a.C, c = h * N + i;
-  const int segi = blockIdx.x * SG + grp;
-  const bool active = segi < a.n_seg;
-  const int4 sg = a.segs[active ? segi : 0];
-  // ---- head-only loads: this workgroup's share of the LoRA-up rows (16-B pieces) + parameters
-  constexpr int PW = DW / 8, PA = DA / 8, PV = DV / 8, PG = DG / 8, PC = PW + PA + PV + PG;  // pieces/channel
-  constexpr int NPIECE = N * PC, PPT = (NPIECE + 128 * SG - 1) / (128 * SG);
-  short8 lw[PPT];
-#pragma unroll
-  for (int u = 0; u < PPT; ++u) {
-    const int q = tid + u * 128 * SG;
-    const int ch = q / PC, pc = q - ch * PC;
-    const int cc = h * N + ch;
-    const bf16_t* src;
-    if (pc < PW) src = a.w2t + (int64_t)cc * DW + pc * 8;
-    else if (pc < PW + PA) src = a.a2t + (int64_t)cc * DA + (pc - PW) * 8;
-    else if (pc < PW + PA + PV) src = a.v2t + (int64_t)cc * DV + (pc - PW - PA) * 8;
-    else src = a.g2t + (int64_t)cc * DG + (pc - PW - PA - PV) * 8;
-    lw[u] = (q < NPIECE && !(a.exp & 32)) ? *(const short8*)src : (short8){0, 0, 0, 0, 0, 0, 0, 0};
-  }
-  const float w0 = a.w0[c], a0 = a.a0[c], v0 = a.v0[c], kkc = a.k_k[c], kac = a.k_a[c];
-  const float rkc = a.r_k[c], lnw = a.lnx_w[c], lnb = a.lnx_b[c];
-  // ---- segment-dependent loads, issued speculatively for slot = row = segment index
-  const int spec = segi;
-  const int64_t soff = a.layer_off + (int64_t)h * N * N + i * N + hf * 32;
-  float S[32];
-  auto load_state = [&](int slot) {
-    const float* Sp = a.state + (int64_t)slot * a.slot_stride + soff;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const float4_ v4 = (a.exp & 8) ? (float4_){0.f, 0.f, 0.f, 0.f} : *(const float4_*)(Sp + q * 4);
-      S[q * 4 + 0] = v4[0]; S[q * 4 + 1] = v4[1]; S[q * 4 + 2] = v4[2]; S[q * 4 + 3] = v4[3];
-    }
-  };
-  load_state(spec < a.n_slots ? spec : 0);
-  constexpr int HPL = (DALL + 127) / 128;
-  float hp[MAXP][HPL], rp[MAXP], kp[MAXP], vp[MAXP], vf = 0.f;
-  auto load_parts = [&](int row) {
-    const float* prow = a.part + (int64_t)row * a.ldp;
-#pragma unroll
-    for (int p = 0; p < MAXP; ++p) {
-      const bool on = p < a.n_part && !(a.exp & 16);
-      const float* pp = prow + p * a.part_stride;
-#pragma unroll
-      for (int e = 0; e < HPL; ++e) {
-        const int d = t + 128 * e;
-        hp[p][e] = (on && d < DALL) ? pp[3 * C + d] : 0.f;
-      }
-      rp[p] = on ? pp[c] : 0.f;
-      kp[p] = on ? pp[C + c] : 0.f;
-      vp[p] = on ? pp[2 * C + c] : 0.f;
-    }
-    vf = a.layer > 0 ? a.v_first[(int64_t)row * a.ldv + c] : 0.f;
-  };
-  const int spec_row = spec < a.n_slots ? spec : 0;
-  load_parts(spec_row);
-  // LoRA-up rows -> LDS (after the state/partials loads are in flight)
-#pragma unroll
-  for (int u = 0; u < PPT; ++u) {
-    const int q = tid + u * 128 * SG;
-    if (q < NPIECE) {
-      const int ch = q / PC, pc = q - ch * PC;
-      *(short8*)(s_lw + ch * LWS + pc * 8) = lw[u];
-    }
-  }
-  const int slot = sg.x, r_begin = sg.y, n_rows = active ? sg.z : 0;
-  float* Srow = a.state + (int64_t)slot * a.slot_stride + soff;
-  if (active && slot != spec_row) load_state(slot);
-  if (active && r_begin != spec_row) load_parts(r_begin);
-  int max_rows = 0;
-#pragma unroll
-  for (int g2 = 0; g2 < SG; ++g2) {
-    const int sj = blockIdx.x * SG + g2;
-    if (sj < a.n_seg) max_rows = max(max_rows, a.segs[sj].z);
-  }
-  float* hid = s_hid[grp];
-  float(*vec)[N] = s_vec[grp];
-  float(*red)[2] = s_red[grp];
-  const bf16_t* myw = s_lw + i * LWS;
-  for (int rr = 0; rr < max_rows; ++rr) {
-    const bool on = rr < n_rows;
-    const int row = r_begin + rr;
-    if (rr > 0 && on) load_parts(row);
-#pragma unroll
-    for (int e = 0; e < HPL; ++e) {
-      float x = 0.f;
-#pragma unroll
-      for (int p = 0; p < MAXP; ++p) x += hp[p][e];
-      const int d = t + 128 * e;
-      if (d < DALL) hid[d] = d < DW ? tanhf(x) : (d >= DW + DA + DV ? sigm(x) : x);
-    }
-    float r = 0.f, k = 0.f, v = 0.f;
-#pragma unroll
-    for (int p = 0; p < MAXP; ++p) {
-      r += rp[p];
-      k += kp[p];
-      v += vp[p];
-    }
-    __syncthreads();
-    // ---- LoRA up: this thread's half of channel c's four dot products (weights from LDS)
-    float lo0 = 0.f, lo1 = 0.f, lo2 = 0.f, lo3 = 0.f;
-    auto dot8 = [&](const bf16_t* wsrc, const float* hsrc) {
-      const short8 q = *(const short8*)wsrc;
-      const float4_ h0 = *(const float4_*)hsrc;
-      const float4_ h1 = *(const float4_*)(hsrc + 4);
-      float acc = 0.f;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) acc += w16_to_f32((uint16_t)q[e], a.f16 != 0) * h0[e];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) acc += w16_to_f32((uint16_t)q[4 + e], a.f16 != 0) * h1[e];
-      return acc;
-    };
-#pragma unroll
-    for (int u = 0; u < DW / 16; ++u) lo0 += dot8(myw + hf * (DW / 2) + u * 8, hid + hf * (DW / 2) + u * 8);
-#pragma unroll
-    for (int u = 0; u < DA / 16; ++u) lo1 += dot8(myw + DW + hf * (DA / 2) + u * 8, hid + DW + hf * (DA / 2) + u * 8);
-#pragma unroll
-    for (int u = 0; u < DV / 16; ++u)
-      lo2 += dot8(myw + DW + DA + hf * (DV / 2) + u * 8, hid + DW + DA + hf * (DV / 2) + u * 8);
-#pragma unroll
-    for (int u = 0; u < DG / 16; ++u)
-      lo3 += dot8(myw + DW + DA + DV + hf * (DG / 2) + u * 8, hid + DW + DA + DV + hf * (DG / 2) + u * 8);
-    lo0 += __shfl_xor(lo0, 1);
-    lo1 += __shfl_xor(lo1, 1);
-    lo2 += __shfl_xor(lo2, 1);
-    lo3 += __shfl_xor(lo3, 1);
-    const float w = expf(-0.60653066f * sigm(w0 + lo0));
-    const float av = sigm(a0 + lo1);
-    const float kk = k * kkc;
-    k = k * (1.0f + (av - 1.0f) * kac);
-    if (a.layer == 0) {
-      if (hf == 0 && on) a.v_first[(int64_t)row * a.ldv + c] = v;
-    } else {
-      v = v + (vf - v) * sigm(v0 + lo2);
-    }
-    {
-      const float ksq = wave_sum(hf == 0 ? kk * kk : 0.f);
-      const float bon = wave_sum(hf == 0 ? r * k * rkc : 0.f);
-      if (lane == 0) { red[0][wave] = ksq; red[1][wave] = bon; }
-    }
-    if (hf == 0) {
-      vec[0][i] = w; vec[1][i] = kk; vec[2][i] = av; vec[3][i] = k; vec[4][i] = r;
-    }
-    __syncthreads();
-    const float inv = 1.0f / fmaxf(sqrtf(red[0][0] + red[0][1]), 1e-12f);
-    const float bonus = red[1][0] + red[1][1];
-    const float* vj = &vec[0][hf * 32];
-    float sa = 0.f;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const float4_ kq = *(const float4_*)(vj + N + q * 4);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) sa += S[q * 4 + e] * (kq[e] * inv);
-    }
-    sa += __shfl_xor(sa, 1);
-    float y = 0.f;
-    float Sn[32];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const float4_ wq = *(const float4_*)(vj + q * 4);
-      const float4_ kq = *(const float4_*)(vj + N + q * 4);
-      const float4_ aq = *(const float4_*)(vj + 2 * N + q * 4);
-      const float4_ k4 = *(const float4_*)(vj + 3 * N + q * 4);
-      const float4_ rq = *(const float4_*)(vj + 4 * N + q * 4);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float sv = S[q * 4 + e] * wq[e] - sa * ((kq[e] * inv) * aq[e]) + v * k4[e];
-        Sn[q * 4 + e] = sv;
-        y += sv * rq[e];
-      }
-    }
-    if (on) {
-#pragma unroll
-      for (int q = 0; q < 32; ++q) S[q] = Sn[q];
-      if (rr + 1 == n_rows && !(a.exp & 64)) {  // last row of the segment: the state is final, store it now
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          float4_ v4 = {S[q * 4 + 0], S[q * 4 + 1], S[q * 4 + 2], S[q * 4 + 3]};
-          *(float4_*)(Srow + q * 4) = v4;
-        }
-      }
-    }
-    y += __shfl_xor(y, 1);
-    {
-      const float s1 = wave_sum(hf == 0 ? y : 0.f);
-      const float s2 = wave_sum(hf == 0 ? y * y : 0.f);
-      if (lane == 0) { red[2][wave] = s1; red[3][wave] = s2; }
-    }
-    __syncthreads();
-    const float mean = (red[2][0] + red[2][1]) * (1.0f / N);
-    const float var = fmaxf((red[3][0] + red[3][1]) * (1.0f / N) - mean * mean, 0.f);
-    if (hf == 0 && on) {
-      const float gn = (y - mean) * (1.0f / sqrtf(var + 64e-5f)) * lnw + lnb;
-      split_store((gn + bonus * v) * lo3, a.z_hi, a.z_lo, (int64_t)row * a.ldz + c, a.f16 != 0);
-    }
-    if (rr + 1 < max_rows) __syncthreads();
-  }
 }
 
 // ------------------------------------------------------------------------------------
@@ -1581,22 +1388,199 @@ __global__ __launch_bounds__(128) void k_wkv4(WkvArgs a) {
   tl_end(a.tl);
 }
 
-bool wkv_perm_layout(int Dw, int Da, int Dv, int Dg, int n_part) {
-  const char* sg = getenv("RWKVTTS_WKV_SG");
-  return Dw == 64 && Da == 64 && Dv == 32 && Dg == 128 && n_part == 4 && !getenv("RWKVTTS_WKV_OLD") &&
-         !(sg && atoi(sg) != 0);
+// ------------------------------------------------------------------------------------
+// wkv6: k_wkv4 on four waves. Thread t = (channel i = t >> 2, quarter qq = t & 3) owns state
+// row S[i][16 qq .. 16 qq + 15] and a quarter of channel c's LoRA-up dot products, so each
+// thread executes half of k_wkv4's per-row arithmetic and two waves share every SIMD (the
+// dependent chains of one hide behind the other's). Quarter sums are two quad shuffles.
+// State blocks: thread t's q-th float4 at float4 index q * 256 + t (engine.hip perm_index,
+// layout 2); LoRA-up rows: entry u of thread t at uint4 index u * 256 + t (launch_pack_lora6).
+// ------------------------------------------------------------------------------------
+template <bool F16>
+__global__ __launch_bounds__(256) void k_wkv6(WkvArgs a) {
+  constexpr int N = 64, DW = 64, DA = 64, DV = 32, DG = 128, DALL = DW + DA + DV + DG, NP = 4;
+  __shared__ __attribute__((aligned(16))) float s_hid[DALL];
+  __shared__ __attribute__((aligned(16))) float s_vec[5][N];  // w, kk (unnormalised), a, k, r
+  __shared__ float s_red[4][4];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, i = t >> 2, qq = t & 3;
+  const int h = blockIdx.y, C = a.C, c = h * N + i;
+  tl_begin(a.tl);
+  const int4 sg = a.segs[blockIdx.x];
+  uint4 lw[9];  // 8 bf16 per entry: w 0..1 | a 2..3 | v 4 | g 5..8
+  {
+    const uint4* pl = (const uint4*)(a.lup + (int64_t)h * 9 * 256 * 8);
+#pragma unroll
+    for (int u = 0; u < 9; ++u) lw[u] = pl[u * 256 + t];
+  }
+  const float w0 = a.w0[c], a0 = a.a0[c], v0 = a.v0[c], kkc = a.k_k[c], kac = a.k_a[c];
+  const float rkc = a.r_k[c], lnw = a.lnx_w[c], lnb = a.lnx_b[c];
+  const int spec = blockIdx.x < a.n_slots ? blockIdx.x : 0;
+  const int64_t soff = a.layer_off + (int64_t)h * N * N + (int64_t)t * 4;
+  float4_ S4[4];
+  auto load_state = [&](int slot) {
+    const float4_* Sp = (const float4_*)(a.state + (int64_t)slot * a.slot_stride + soff);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) S4[q] = Sp[q * 256];
+  };
+  load_state(spec);
+  const bool hid_thread = t < DALL / 4;
+  float4_ hp[NP];
+  float rp[NP], kp[NP], vp[NP], vf = 0.f;
+  auto load_parts = [&](int row) {
+    const float* prow = a.part + (int64_t)row * a.ldp;
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const float* pp = prow + p * a.part_stride;
+      hp[p] = *(const float4_*)(pp + 3 * C + (hid_thread ? 4 * t : 0));
+      rp[p] = pp[c];
+      kp[p] = pp[C + c];
+      vp[p] = pp[2 * C + c];
+    }
+    vf = a.layer > 0 ? a.v_first[(int64_t)row * a.ldv + c] : 0.f;
+  };
+  load_parts(spec);
+  const int slot = sg.x, r_begin = sg.y, n_rows = sg.z;
+  if (slot != spec) load_state(slot);
+  if (r_begin != spec) load_parts(r_begin);
+  float4_* Srow = (float4_*)(a.state + (int64_t)slot * a.slot_stride + soff);
+  auto quad_sum = [](float x) {
+    x += __shfl_xor(x, 1);
+    return x + __shfl_xor(x, 2);
+  };
+  for (int rr = 0; rr < n_rows; ++rr) {
+    const int row = r_begin + rr;
+    if (rr > 0) load_parts(row);
+    if (hid_thread) {
+      float4_ x = hp[0];
+#pragma unroll
+      for (int p = 1; p < NP; ++p) x += hp[p];
+      float4_ y;
+      if (t < DW / 4) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) y[e] = ftanh(x[e]);
+      } else if (t < (DW + DA + DV) / 4) {
+        y = x;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) y[e] = fsigm(x[e]);
+      }
+      *(float4_*)(s_hid + 4 * t) = y;
+    }
+    float r = rp[0], k = kp[0], v = vp[0];
+#pragma unroll
+    for (int p = 1; p < NP; ++p) {
+      r += rp[p];
+      k += kp[p];
+      v += vp[p];
+    }
+    __syncthreads();
+    float2_ l0 = {0.f, 0.f}, l1 = {0.f, 0.f}, l2 = {0.f, 0.f}, l3 = {0.f, 0.f};
+    auto dot = [&](float2_ acc, const uint4 q, const float* hsrc) {
+      const float4_ h0 = *(const float4_*)hsrc;
+      const float4_ h1 = *(const float4_*)(hsrc + 4);
+      acc += w2f<F16>(q.x) * (float2_){h0[0], h0[1]};
+      acc += w2f<F16>(q.y) * (float2_){h0[2], h0[3]};
+      acc += w2f<F16>(q.z) * (float2_){h1[0], h1[1]};
+      acc += w2f<F16>(q.w) * (float2_){h1[2], h1[3]};
+      return acc;
+    };
+#pragma unroll
+    for (int u = 0; u < 2; ++u) l0 = dot(l0, lw[u], s_hid + qq * (DW / 4) + u * 8);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) l1 = dot(l1, lw[2 + u], s_hid + DW + qq * (DA / 4) + u * 8);
+    l2 = dot(l2, lw[4], s_hid + DW + DA + qq * (DV / 4));
+#pragma unroll
+    for (int u = 0; u < 4; ++u) l3 = dot(l3, lw[5 + u], s_hid + DW + DA + DV + qq * (DG / 4) + u * 8);
+    const float lo0 = quad_sum(l0[0] + l0[1]), lo1 = quad_sum(l1[0] + l1[1]);
+    const float lo2 = quad_sum(l2[0] + l2[1]), lo3 = quad_sum(l3[0] + l3[1]);
+    const float w = fexp(-0.60653066f * fsigm(w0 + lo0));
+    const float av = fsigm(a0 + lo1);
+    const float kk = k * kkc;
+    k = k * (1.0f + (av - 1.0f) * kac);
+    if (a.layer == 0) {
+      if (qq == 0) a.v_first[(int64_t)row * a.ldv + c] = v;
+    } else {
+      v = v + (vf - v) * fsigm(v0 + lo2);
+    }
+    {
+      const float ksq = wave_sum(qq == 0 ? kk * kk : 0.f);
+      const float bon = wave_sum(qq == 0 ? r * k * rkc : 0.f);
+      if (lane == 0) { s_red[0][wave] = ksq; s_red[1][wave] = bon; }
+    }
+    if (qq == 0) {
+      s_vec[0][i] = w; s_vec[1][i] = kk; s_vec[2][i] = av; s_vec[3][i] = k; s_vec[4][i] = r;
+    }
+    __syncthreads();
+    const float inv =
+        __builtin_amdgcn_rcpf(fmaxf(sqrtf((s_red[0][0] + s_red[0][1]) + (s_red[0][2] + s_red[0][3])), 1e-12f));
+    const float bonus = (s_red[1][0] + s_red[1][1]) + (s_red[1][2] + s_red[1][3]);
+    const float* vj = &s_vec[0][qq * 16];
+    float2_ sa2 = {0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4_ kq = *(const float4_*)(vj + N + q * 4);
+      sa2 += (float2_){S4[q][0], S4[q][1]} * (float2_){kq[0], kq[1]};
+      sa2 += (float2_){S4[q][2], S4[q][3]} * (float2_){kq[2], kq[3]};
+    }
+    const float sa = quad_sum((sa2[0] + sa2[1]) * inv);
+    float2_ y2 = {0.f, 0.f};
+    const float2_ sav = {sa * inv, sa * inv}, vv = {v, v};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4_ wq = *(const float4_*)(vj + q * 4);
+      const float4_ kq = *(const float4_*)(vj + N + q * 4);
+      const float4_ aq = *(const float4_*)(vj + 2 * N + q * 4);
+      const float4_ k4 = *(const float4_*)(vj + 3 * N + q * 4);
+      const float4_ rq = *(const float4_*)(vj + 4 * N + q * 4);
+#pragma unroll
+      for (int e = 0; e < 4; e += 2) {
+        float2_ sv = (float2_){S4[q][e], S4[q][e + 1]} * (float2_){wq[e], wq[e + 1]};
+        sv -= sav * ((float2_){kq[e], kq[e + 1]} * (float2_){aq[e], aq[e + 1]});
+        sv += vv * (float2_){k4[e], k4[e + 1]};
+        S4[q][e] = sv[0];
+        S4[q][e + 1] = sv[1];
+        y2 += sv * (float2_){rq[e], rq[e + 1]};
+      }
+    }
+    if (rr + 1 == n_rows) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Srow[q * 256] = S4[q];
+    }
+    const float y = quad_sum(y2[0] + y2[1]);
+    {
+      const float s1 = wave_sum(qq == 0 ? y : 0.f);
+      const float s2 = wave_sum(qq == 0 ? y * y : 0.f);
+      if (lane == 0) { s_red[2][wave] = s1; s_red[3][wave] = s2; }
+    }
+    __syncthreads();
+    const float mean = ((s_red[2][0] + s_red[2][1]) + (s_red[2][2] + s_red[2][3])) * (1.0f / N);
+    const float var =
+        fmaxf(((s_red[3][0] + s_red[3][1]) + (s_red[3][2] + s_red[3][3])) * (1.0f / N) - mean * mean, 0.f);
+    if (qq == 0) {
+      const float gn = (y - mean) * __builtin_amdgcn_rsqf(var + 64e-5f) * lnw + lnb;
+      split_store((gn + bonus * v) * lo3, a.z_hi, a.z_lo, (int64_t)row * a.ldz + c, F16);
+    }
+    if (rr + 1 < n_rows) __syncthreads();
+  }
+  tl_end(a.tl);
+}
+
+int wkv_perm_layout(int Dw, int Da, int Dv, int Dg, int n_part, int max_slots) {
+  if (!(Dw == 64 && Da == 64 && Dv == 32 && Dg == 128 && n_part == 4 && !getenv("RWKVTTS_WKV_OLD"))) return 0;
+  if (const char* e = getenv("RWKVTTS_WKV_LAYOUT")) return atoi(e) == 2 ? 2 : 1;
+  // measured per decode step: k_wkv6 1 % faster at one slot (16 workgroups on an idle chip),
+  // k_wkv4 1 % faster at 32 slots (512 workgroups)
+  return max_slots <= 8 ? 2 : 1;
 }
 int launch_wkv(const WkvArgs& a, int n_seg, int H, hipStream_t st) {
   const dim3 grid(n_seg, H);
   if (a.Dw == 64 && a.Da == 64 && a.Dv == 32 && a.Dg == 128 && a.n_part <= 4 && !getenv("RWKVTTS_WKV_OLD")) {
-    static const int sgw = getenv("RWKVTTS_WKV_SG") ? atoi(getenv("RWKVTTS_WKV_SG")) : 0;
-    if (a.perm) {
+    if (a.perm == 2) {
+      if (a.f16) RT_LAUNCH((k_wkv6<true>), grid, dim3(256), 0, st, a);
+      else RT_LAUNCH((k_wkv6<false>), grid, dim3(256), 0, st, a);
+    } else if (a.perm == 1) {
       if (a.f16) RT_LAUNCH((k_wkv4<true>), grid, dim3(128), 0, st, a);
       else RT_LAUNCH((k_wkv4<false>), grid, dim3(128), 0, st, a);
-    } else if (sgw == 2) {
-      RT_LAUNCH((k_wkv3<64, 64, 32, 128, 4, 2>), dim3((n_seg + 1) / 2, H), dim3(256), 0, st, a);
-    } else if (sgw == 4) {
-      RT_LAUNCH((k_wkv3<64, 64, 32, 128, 4, 4>), dim3((n_seg + 3) / 4, H), dim3(512), 0, st, a);
     } else {
       RT_LAUNCH((k_wkv2<64, 64, 32, 128, 4>), grid, dim3(128), 0, st, a);
     }
