@@ -20,10 +20,25 @@ namespace rwkvtts {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
-__device__ inline float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-  return v;
+// Cross-lane sums on DPP moves (no LDS round trip, unlike __shfl_xor's ds_bpermute). Each step
+// pairs every lane with a partner holding the other half of its group and both add in the same
+// order, so every lane of a group ends with the identical sum.
+template <int CTRL>
+__device__ inline float dpp_mov(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+__device__ inline float sum16(float v) {  // aligned groups of 16 lanes
+  v += dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_mov<0x141>(v);  // row_half_mirror: the two quads of each half-row
+  return v + dpp_mov<0x140>(v);  // row_mirror: the two halves of each row
+}
+__device__ inline float readlane_f32(float v, int l) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+__device__ inline float wave_sum(float v) {  // whole wave (all lanes active); uniform result
+  v = sum16(v);
+  return (readlane_f32(v, 0) + readlane_f32(v, 16)) + (readlane_f32(v, 32) + readlane_f32(v, 48));
 }
 
 // deterministic block (256 threads) sum; every thread gets the result
@@ -748,10 +763,10 @@ __global__ __launch_bounds__(256, 2) void k_wkv(WkvArgs a) {
           lo3 += e >= e3 ? d : 0.f;
         }
       }
-      lo0 += __shfl_xor(lo0, 1); lo0 += __shfl_xor(lo0, 2);
-      lo1 += __shfl_xor(lo1, 1); lo1 += __shfl_xor(lo1, 2);
-      lo2 += __shfl_xor(lo2, 1); lo2 += __shfl_xor(lo2, 2);
-      lo3 += __shfl_xor(lo3, 1); lo3 += __shfl_xor(lo3, 2);
+      lo0 += dpp_mov<0xB1>(lo0); lo0 += dpp_mov<0x4E>(lo0);
+      lo1 += dpp_mov<0xB1>(lo1); lo1 += dpp_mov<0x4E>(lo1);
+      lo2 += dpp_mov<0xB1>(lo2); lo2 += dpp_mov<0x4E>(lo2);
+      lo3 += dpp_mov<0xB1>(lo3); lo3 += dpp_mov<0x4E>(lo3);
     }
     {
       const float w = expf(-0.60653066f * sigm(w0 + lo0));
@@ -783,8 +798,8 @@ __global__ __launch_bounds__(256, 2) void k_wkv(WkvArgs a) {
     float sa = 0.f;
 #pragma unroll
     for (int q = 0; q < 16; ++q) sa += S[q] * kkn[q];
-    sa += __shfl_xor(sa, 1);
-    sa += __shfl_xor(sa, 2);
+    sa += dpp_mov<0xB1>(sa);
+    sa += dpp_mov<0x4E>(sa);
     const float vi = s_v[i];
     float y = 0.f;
 #pragma unroll
@@ -793,8 +808,8 @@ __global__ __launch_bounds__(256, 2) void k_wkv(WkvArgs a) {
       S[q] = S[q] * s_w[jj] - sa * (kkn[q] * s_b[jj]) + vi * s_k[jj];
       y += S[q] * s_r[jj];
     }
-    y += __shfl_xor(y, 1);
-    y += __shfl_xor(y, 2);
+    y += dpp_mov<0xB1>(y);
+    y += dpp_mov<0x4E>(y);
     if ((tid & 3) == 0) s_y[i] = y;
     __syncthreads();
     if (rr == 0) { WKV_STAMP(4) }
@@ -1109,10 +1124,10 @@ __global__ __launch_bounds__(128) void k_wkv2(WkvArgs a) {
     for (int u = 0; u < UV; ++u) lo2 += dot8(lw[UW + UA + u], s_hid + DW + DA + hf * (DV / 2) + u * 8);
 #pragma unroll
     for (int u = 0; u < UG; ++u) lo3 += dot8(lw[UW + UA + UV + u], s_hid + DW + DA + DV + hf * (DG / 2) + u * 8);
-    lo0 += __shfl_xor(lo0, 1);
-    lo1 += __shfl_xor(lo1, 1);
-    lo2 += __shfl_xor(lo2, 1);
-    lo3 += __shfl_xor(lo3, 1);
+    lo0 += dpp_mov<0xB1>(lo0);
+    lo1 += dpp_mov<0xB1>(lo1);
+    lo2 += dpp_mov<0xB1>(lo2);
+    lo3 += dpp_mov<0xB1>(lo3);
     // ---- channel mixing terms (both threads of the pair compute channel c)
     const float w = expf(-0.60653066f * sigm(w0 + lo0));
     const float av = sigm(a0 + lo1);
@@ -1144,7 +1159,7 @@ __global__ __launch_bounds__(128) void k_wkv2(WkvArgs a) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) sa += S[q * 4 + e] * (kq[e] * inv);
     }
-    sa += __shfl_xor(sa, 1);
+    sa += dpp_mov<0xB1>(sa);
     float y = 0.f;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
@@ -1160,7 +1175,7 @@ __global__ __launch_bounds__(128) void k_wkv2(WkvArgs a) {
         y += sv * rq[e];
       }
     }
-    y += __shfl_xor(y, 1);
+    y += dpp_mov<0xB1>(y);
     // ---- GroupNorm over the head's 64 rows (eps 64e-5): one-barrier moments
     {
       const float s1 = wave_sum(hf == 0 ? y : 0.f);
@@ -1310,10 +1325,10 @@ __global__ __launch_bounds__(128) void k_wkv4(WkvArgs a) {
 #pragma unroll
     for (int u = 0; u < 8; ++u) l3 = dot(l3, lw[10 + u], s_hid + DW + DA + DV + hf * (DG / 2) + u * 8);
     float lo0 = l0[0] + l0[1], lo1 = l1[0] + l1[1], lo2 = l2[0] + l2[1], lo3 = l3[0] + l3[1];
-    lo0 += __shfl_xor(lo0, 1);
-    lo1 += __shfl_xor(lo1, 1);
-    lo2 += __shfl_xor(lo2, 1);
-    lo3 += __shfl_xor(lo3, 1);
+    lo0 += dpp_mov<0xB1>(lo0);
+    lo1 += dpp_mov<0xB1>(lo1);
+    lo2 += dpp_mov<0xB1>(lo2);
+    lo3 += dpp_mov<0xB1>(lo3);
     // ---- channel mixing terms (both threads of the pair compute channel c)
     const float w = fexp(-0.60653066f * fsigm(w0 + lo0));
     const float av = fsigm(a0 + lo1);
@@ -1345,7 +1360,7 @@ __global__ __launch_bounds__(128) void k_wkv4(WkvArgs a) {
       sa2 += (float2_){S4[q][2], S4[q][3]} * (float2_){kq[2], kq[3]};
     }
     float sa = (sa2[0] + sa2[1]) * inv;
-    sa += __shfl_xor(sa, 1);
+    sa += dpp_mov<0xB1>(sa);
     float2_ y2 = {0.f, 0.f};
     const float2_ sav = {sa * inv, sa * inv}, vv = {v, v};
 #pragma unroll
@@ -1370,7 +1385,7 @@ __global__ __launch_bounds__(128) void k_wkv4(WkvArgs a) {
       for (int q = 0; q < 8; ++q) Srow[q * 128] = S4[q];
     }
     float y = y2[0] + y2[1];
-    y += __shfl_xor(y, 1);
+    y += dpp_mov<0xB1>(y);
     {
       const float s1 = wave_sum(hf == 0 ? y : 0.f);
       const float s2 = wave_sum(hf == 0 ? y * y : 0.f);
@@ -1444,8 +1459,8 @@ __global__ __launch_bounds__(256) void k_wkv6(WkvArgs a) {
   if (r_begin != spec) load_parts(r_begin);
   float4_* Srow = (float4_*)(a.state + (int64_t)slot * a.slot_stride + soff);
   auto quad_sum = [](float x) {
-    x += __shfl_xor(x, 1);
-    return x + __shfl_xor(x, 2);
+    x += dpp_mov<0xB1>(x);
+    return x + dpp_mov<0x4E>(x);
   };
   for (int rr = 0; rr < n_rows; ++rr) {
     const int row = r_begin + rr;
