@@ -497,7 +497,7 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
 //    latency; in kXRelu2 mode all NX key slabs are in flight at once;
 //  * hi and lo products accumulate in separate MFMA chains (2*MT independent accumulators).
 // ------------------------------------------------------------------------------------
-template <int MT, int KSTEPS, int XMODE, bool F16, int NX>
+template <int MT, int KSTEPS, int XMODE, bool F16, int NX, bool MS>
 __global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int KS = KSTEPS * 32;
@@ -507,15 +507,19 @@ __global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
   bf16_t* xl = xh + ROWS * LD;
   tl_begin(a.tl);
   const int tile = blockIdx.x;
+  // MS: several segments (the rkv + LoRA-down launch); single-segment launches read seg[0]
+  // directly, which saves the dependent kernel-argument round trip of the segment lookup
   int s = 0;
+  if constexpr (MS) {
 #pragma unroll
-  for (int j = 1; j < 8; ++j) s += (j < a.nseg && tile >= a.seg[j].tile_start) ? 1 : 0;
+    for (int j = 1; j < 8; ++j) s += (j < a.nseg && tile >= a.seg[j].tile_start) ? 1 : 0;
+  }
   const bf16_t* Wm = a.seg[0].W;
   const bf16_t* Xhi = a.seg[0].Xhi;
   const bf16_t* Xlo = a.seg[0].Xlo;
   int ldx = a.seg[0].ldx, Nn = a.seg[0].N, col_off = a.seg[0].col_off, tstart = a.seg[0].tile_start;
 #pragma unroll
-  for (int j = 1; j < 8; ++j)
+  for (int j = 1; j < (MS ? 8 : 1); ++j)
     if (s == j) {
       Wm = a.seg[j].W; Xhi = a.seg[j].Xhi; Xlo = a.seg[j].Xlo;
       ldx = a.seg[j].ldx; Nn = a.seg[j].N; col_off = a.seg[j].col_off; tstart = a.seg[j].tile_start;
@@ -883,14 +887,17 @@ static void launch_gemm_t(const GemmArgs& a, dim3 grid, hipStream_t st) {
   const size_t lds = (size_t)MT * 16 * (KSTEPS * 32 + 8) * 2 * 2;
   static const bool v2 = !getenv("RWKVTTS_GEMM_OLD");
   if (v2 && (a.xmode == kXPlanes || a.x_nsplit == 4 || a.x_nsplit == 2) && a.stamps == nullptr && a.exp == 0) {
+    const bool ms = a.nseg > 1;
     if (a.f16) {
-      if (a.xmode == kXPlanes) RT_LAUNCH((k_gemm2<MT, KSTEPS, kXPlanes, true, 1>), grid, dim3(256), lds, st, a);
-      else if (a.x_nsplit == 4) RT_LAUNCH((k_gemm2<MT, KSTEPS, kXRelu2, true, 4>), grid, dim3(256), lds, st, a);
-      else RT_LAUNCH((k_gemm2<MT, KSTEPS, kXRelu2, true, 2>), grid, dim3(256), lds, st, a);
+      if (a.xmode == kXPlanes && ms) RT_LAUNCH((k_gemm2<MT, KSTEPS, kXPlanes, true, 1, true>), grid, dim3(256), lds, st, a);
+      else if (a.xmode == kXPlanes) RT_LAUNCH((k_gemm2<MT, KSTEPS, kXPlanes, true, 1, false>), grid, dim3(256), lds, st, a);
+      else if (a.x_nsplit == 4) RT_LAUNCH((k_gemm2<MT, KSTEPS, kXRelu2, true, 4, false>), grid, dim3(256), lds, st, a);
+      else RT_LAUNCH((k_gemm2<MT, KSTEPS, kXRelu2, true, 2, false>), grid, dim3(256), lds, st, a);
     } else {
-      if (a.xmode == kXPlanes) RT_LAUNCH((k_gemm2<MT, KSTEPS, kXPlanes, false, 1>), grid, dim3(256), lds, st, a);
-      else if (a.x_nsplit == 4) RT_LAUNCH((k_gemm2<MT, KSTEPS, kXRelu2, false, 4>), grid, dim3(256), lds, st, a);
-      else RT_LAUNCH((k_gemm2<MT, KSTEPS, kXRelu2, false, 2>), grid, dim3(256), lds, st, a);
+      if (a.xmode == kXPlanes && ms) RT_LAUNCH((k_gemm2<MT, KSTEPS, kXPlanes, false, 1, true>), grid, dim3(256), lds, st, a);
+      else if (a.xmode == kXPlanes) RT_LAUNCH((k_gemm2<MT, KSTEPS, kXPlanes, false, 1, false>), grid, dim3(256), lds, st, a);
+      else if (a.x_nsplit == 4) RT_LAUNCH((k_gemm2<MT, KSTEPS, kXRelu2, false, 4, false>), grid, dim3(256), lds, st, a);
+      else RT_LAUNCH((k_gemm2<MT, KSTEPS, kXRelu2, false, 2, false>), grid, dim3(256), lds, st, a);
     }
     return;
   }
