@@ -282,7 +282,8 @@ __global__ __launch_bounds__(256) void k_ln1024(LnMixArgs a) {
   __shared__ float red[16];
   tl_begin(a.tl);
   const int out_row = blockIdx.x;
-  const int row = a.row_map ? a.row_map[out_row] : out_row;
+  // MODE 1 (LN + mixes) never remaps rows: no dependent row_map load
+  const int row = (MODE == 0 && a.row_map) ? a.row_map[out_row] : out_row;
   const int c = 4 * threadIdx.x;
   // loads that do not depend on the previous launch: LN / mix vectors, row descriptor, shift state
   const float4_ w = ld4(a.ln_w + c), b = ld4(a.ln_b + c);
