@@ -152,21 +152,24 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
   {
     auto packed_elems = [](int N, int K) { return (size_t)((N + 15) / 16) * 16 * K; };
     const int Dw = dims.d_decay, Da = dims.d_aaa, Dv = dims.d_mv, Dg = dims.d_gate;
-    size_t per_layer = 3 * packed_elems(C, C) + packed_elems(Dw, C) + packed_elems(Da, C) + packed_elems(Dv, C) +
-                       packed_elems(Dg, C) + packed_elems(C, C) + packed_elems(F, C) + packed_elems(C, F);
+    // the r, k, v and LoRA-down matrices are padded to 64-column tiles, back to back, so the
+    // rkv launch finds tile t's weights at a fixed stride (gemm_tile_table)
+    auto packed64 = [](int N, int K) { return (size_t)((N + 63) / 64) * 64 * K; };
+    size_t per_layer = 3 * packed64(C, C) + packed64(Dw, C) + packed64(Da, C) + packed64(Dv, C) +
+                       packed64(Dg, C) + packed_elems(C, C) + packed_elems(F, C) + packed_elems(C, F);
     size_t total = per_layer * dims.n_layer + packed_elems(dims.n_vocab, C);
     RT_OK(alloc(&wpack_, total));
     RT_HIP(hipDeviceSynchronize());  // alloc's memset runs on the null stream; stream_ is non-blocking
     bf16_t* dst = wpack_;
-    auto pack = [&](const bf16_t*& Wm, int N, int K) {
+    auto pack = [&](const bf16_t*& Wm, int N, int K, bool tile64 = false) {
       launch_pack_frag(Wm, N, K, dst, stream_);
       Wm = dst;
-      dst += packed_elems(N, K);
+      dst += tile64 ? packed64(N, K) : packed_elems(N, K);
     };
     for (int l = 0; l < dims.n_layer; ++l) {
       LayerW& w = L_[l];
-      pack(w.wr, C, C); pack(w.wk, C, C); pack(w.wv, C, C);
-      pack(w.w1t, Dw, C); pack(w.a1t, Da, C); pack(w.v1t, Dv, C); pack(w.g1t, Dg, C);
+      pack(w.wr, C, C, true); pack(w.wk, C, C, true); pack(w.wv, C, C, true);
+      pack(w.w1t, Dw, C, true); pack(w.a1t, Da, C, true); pack(w.v1t, Dv, C, true); pack(w.g1t, Dg, C, true);
       pack(w.wo, C, C); pack(w.ffn_k, F, C); pack(w.ffn_v, C, F);
     }
     pack(head_, dims.n_vocab, C);
@@ -420,6 +423,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     seg(5, w.v1t, 3, dims.d_mv, 3 * C + dims.d_decay + dims.d_aaa);
     seg(6, w.g1t, 5, dims.d_gate, 3 * C + dims.d_decay + dims.d_aaa + dims.d_mv);
     g.K = C; g.M = R; g.k_split = splitA_; g.kslice = C / splitA_;
+    gemm_tile_table(g, RC);
     g.xmode = kXPlanes; g.out = partA_; g.split_stride = (int64_t)Rmax_ * ldA_; g.ldo = ldA_;
     prof_begin(&ev);
     g.stamps = (l == 5 && dbg_gstamps_) ? dbg_gstamps_ : nullptr;

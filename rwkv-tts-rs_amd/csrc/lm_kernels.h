@@ -67,6 +67,15 @@ struct GemmArgs {
   int f16;             // weights and activation planes in f16 (fp16 model)
   int exp;             // debug experiment bits (0 in production): 1 skip X loads, 2 skip W loads
   unsigned long long* tl;  // debug timeline slot (null in production)
+  // Multi-segment launches whose segments are packed back to back in 64-column tiles (set by
+  // gemm_tile_table): tile t's weights at tw + t * 64 * K and one descriptor word per tile,
+  // mix plane (bits 0-2) | valid columns (bits 3-9) | first output column (bits 10-31); X of
+  // mix plane m at seg[0].Xhi / Xlo + m * x_mix_stride. Read by blockIdx alone, so the kernel
+  // needs no dependent kernel-argument load to find its segment.
+  int n_tinfo;         // 0: per-segment lookup
+  const bf16_t* tw;
+  int64_t x_mix_stride;
+  uint32_t tinfo[128];
 };
 
 struct WkvArgs {
@@ -103,6 +112,10 @@ void launch_embed(const uint32_t* tokens, const int4* rows, const int* ctrl_tok,
 // Launchers return the workgroup count of the launch.
 int launch_ln_mix(const LnMixArgs& a, int n_out_rows, hipStream_t st);
 int launch_gemm(const GemmArgs& a, hipStream_t st);
+// Fills a.tw / a.tinfo / a.n_tinfo when the segments' packed weights are contiguous in 64-column
+// tiles and every segment's X is seg[0]'s planes plus a multiple of x_mix_stride; returns whether
+// the table applies (otherwise the kernel looks the segment up).
+bool gemm_tile_table(GemmArgs& a, int64_t x_mix_stride);
 int launch_wkv(const WkvArgs& a, int n_seg, int H, hipStream_t st);
 // Which coalesced WKV state layout launch_wkv expects for these LoRA ranks / slab count: 0 none
 // (row-major S[i][j]), 1 k_wkv4 (two waves per block, the default), 2 k_wkv6 (four waves).

@@ -15,6 +15,8 @@
 
 #include <stdlib.h>
 
+#include <algorithm>
+
 namespace rwkvtts {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -498,7 +500,7 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
 //    latency; in kXRelu2 mode all NX key slabs are in flight at once;
 //  * hi and lo products accumulate in separate MFMA chains (2*MT independent accumulators).
 // ------------------------------------------------------------------------------------
-template <int MT, int KSTEPS, int XMODE, bool F16, int NX, bool MS>
+template <int MT, int KSTEPS, int XMODE, bool F16, int NX, int MS>
 __global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int KS = KSTEPS * 32;
@@ -508,10 +510,11 @@ __global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
   bf16_t* xl = xh + ROWS * LD;
   tl_begin(a.tl);
   const int tile = blockIdx.x;
-  // MS: several segments (the rkv + LoRA-down launch); single-segment launches read seg[0]
-  // directly, which saves the dependent kernel-argument round trip of the segment lookup
+  // MS 0: one segment, read from seg[0] directly. MS 1: several segments, looked up from the
+  // tile starts (a second, dependent kernel-argument round trip). MS 2: several segments
+  // through the per-tile descriptor table (one round trip, addressed by blockIdx alone).
   int s = 0;
-  if constexpr (MS) {
+  if constexpr (MS == 1) {
 #pragma unroll
     for (int j = 1; j < 8; ++j) s += (j < a.nseg && tile >= a.seg[j].tile_start) ? 1 : 0;
   }
@@ -519,12 +522,24 @@ __global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
   const bf16_t* Xhi = a.seg[0].Xhi;
   const bf16_t* Xlo = a.seg[0].Xlo;
   int ldx = a.seg[0].ldx, Nn = a.seg[0].N, col_off = a.seg[0].col_off, tstart = a.seg[0].tile_start;
+  if constexpr (MS == 1) {
 #pragma unroll
-  for (int j = 1; j < (MS ? 8 : 1); ++j)
-    if (s == j) {
-      Wm = a.seg[j].W; Xhi = a.seg[j].Xhi; Xlo = a.seg[j].Xlo;
-      ldx = a.seg[j].ldx; Nn = a.seg[j].N; col_off = a.seg[j].col_off; tstart = a.seg[j].tile_start;
-    }
+    for (int j = 1; j < 8; ++j)
+      if (s == j) {
+        Wm = a.seg[j].W; Xhi = a.seg[j].Xhi; Xlo = a.seg[j].Xlo;
+        ldx = a.seg[j].ldx; Nn = a.seg[j].N; col_off = a.seg[j].col_off; tstart = a.seg[j].tile_start;
+      }
+  }
+  if constexpr (MS == 2) {
+    const uint32_t ti = a.tinfo[tile];
+    const int mix = ti & 7;
+    Wm = a.tw + (int64_t)tile * 64 * a.K;
+    Xhi += mix * a.x_mix_stride;
+    Xlo += mix * a.x_mix_stride;
+    Nn = (ti >> 3) & 127;      // valid columns of this tile (the tile is its own segment)
+    col_off = (int)(ti >> 10);
+    tstart = tile;
+  }
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int g = lane >> 4, li = lane & 15;
   const int col0 = (tile - tstart) * 64 + wave * 16;
@@ -888,18 +903,18 @@ static void launch_gemm_t(const GemmArgs& a, dim3 grid, hipStream_t st) {
   const size_t lds = (size_t)MT * 16 * (KSTEPS * 32 + 8) * 2 * 2;
   static const bool v2 = !getenv("RWKVTTS_GEMM_OLD");
   if (v2 && (a.xmode == kXPlanes || a.x_nsplit == 4 || a.x_nsplit == 2) && a.stamps == nullptr && a.exp == 0) {
-    const bool ms = a.nseg > 1;
+    const int ms = a.nseg > 1 ? (a.n_tinfo > 0 ? 2 : 1) : 0;
+#define G2(F, XM, NX_, MS_) RT_LAUNCH((k_gemm2<MT, KSTEPS, XM, F, NX_, MS_>), grid, dim3(256), lds, st, a)
     if (a.f16) {
-      if (a.xmode == kXPlanes && ms) RT_LAUNCH((k_gemm2<MT, KSTEPS, kXPlanes, true, 1, true>), grid, dim3(256), lds, st, a);
-      else if (a.xmode == kXPlanes) RT_LAUNCH((k_gemm2<MT, KSTEPS, kXPlanes, true, 1, false>), grid, dim3(256), lds, st, a);
-      else if (a.x_nsplit == 4) RT_LAUNCH((k_gemm2<MT, KSTEPS, kXRelu2, true, 4, false>), grid, dim3(256), lds, st, a);
-      else RT_LAUNCH((k_gemm2<MT, KSTEPS, kXRelu2, true, 2, false>), grid, dim3(256), lds, st, a);
+      if (a.xmode == kXPlanes) { if (ms == 2) G2(true, kXPlanes, 1, 2); else if (ms == 1) G2(true, kXPlanes, 1, 1); else G2(true, kXPlanes, 1, 0); }
+      else if (a.x_nsplit == 4) G2(true, kXRelu2, 4, 0);
+      else G2(true, kXRelu2, 2, 0);
     } else {
-      if (a.xmode == kXPlanes && ms) RT_LAUNCH((k_gemm2<MT, KSTEPS, kXPlanes, false, 1, true>), grid, dim3(256), lds, st, a);
-      else if (a.xmode == kXPlanes) RT_LAUNCH((k_gemm2<MT, KSTEPS, kXPlanes, false, 1, false>), grid, dim3(256), lds, st, a);
-      else if (a.x_nsplit == 4) RT_LAUNCH((k_gemm2<MT, KSTEPS, kXRelu2, false, 4, false>), grid, dim3(256), lds, st, a);
-      else RT_LAUNCH((k_gemm2<MT, KSTEPS, kXRelu2, false, 2, false>), grid, dim3(256), lds, st, a);
+      if (a.xmode == kXPlanes) { if (ms == 2) G2(false, kXPlanes, 1, 2); else if (ms == 1) G2(false, kXPlanes, 1, 1); else G2(false, kXPlanes, 1, 0); }
+      else if (a.x_nsplit == 4) G2(false, kXRelu2, 4, 0);
+      else G2(false, kXRelu2, 2, 0);
     }
+#undef G2
     return;
   }
   if (a.f16) {
@@ -912,6 +927,29 @@ static void launch_gemm_t(const GemmArgs& a, dim3 grid, hipStream_t st) {
 }
 
 int gemm_ksteps(int kslice) { return kslice / 32; }
+
+bool gemm_tile_table(GemmArgs& a, int64_t x_mix_stride) {
+  a.n_tinfo = 0;
+  if (a.nseg < 2 || x_mix_stride <= 0) return false;
+  const int tiles = a.seg[a.nseg - 1].tile_start + (a.seg[a.nseg - 1].N + 63) / 64;
+  if (tiles > 128) return false;
+  const bf16_t* base = a.seg[0].W;
+  for (int j = 0; j < a.nseg; ++j) {
+    const GemmSeg& g = a.seg[j];
+    const int64_t dx = g.Xhi - a.seg[0].Xhi;
+    if (g.W != base + (int64_t)g.tile_start * 64 * a.K || g.ldx != a.seg[0].ldx || dx % x_mix_stride != 0 ||
+        g.Xlo - a.seg[0].Xlo != dx || dx / x_mix_stride < 0 || dx / x_mix_stride > 7 || g.col_off > (1 << 21))
+      return false;
+    for (int t = 0; t < (g.N + 63) / 64; ++t) {
+      const int nv = std::min(64, g.N - t * 64);
+      a.tinfo[g.tile_start + t] = (uint32_t)(dx / x_mix_stride) | ((uint32_t)nv << 3) | ((uint32_t)(g.col_off + t * 64) << 10);
+    }
+  }
+  a.tw = base;
+  a.x_mix_stride = x_mix_stride;
+  a.n_tinfo = tiles;
+  return true;
+}
 
 int launch_gemm(const GemmArgs& a, hipStream_t st) {
   const int tiles = a.seg[a.nseg - 1].tile_start + (a.seg[a.nseg - 1].N + 63) / 64;
