@@ -283,29 +283,43 @@ __global__ __launch_bounds__(256) void k_ln1024(LnMixArgs a) {
   constexpr int C = 1024;
   __shared__ float red[16];
   tl_begin(a.tl);
+  bf16_t* e_xhi = a.x_hi;
+  bf16_t* e_xlo = a.x_lo;
+  int64_t e_mix = a.mix_stride;
+  int e_ldx = a.ldx;
+  float* e_hout = a.h_out;
+  const float* e_hin = a.h_in;
+  const float* e_part = a.part;
+  int64_t e_pstride = a.part_stride;
+  int e_ldp = a.ldp;
+  float* e_shift = a.shift;
+  int e_S = a.S, e_L = a.L, e_layer = a.layer, e_inpl = a.inplace;
+
   const int out_row = blockIdx.x;
   // MODE 1 (LN + mixes) never remaps rows: no dependent row_map load
   const int row = (MODE == 0 && a.row_map) ? a.row_map[out_row] : out_row;
   const int c = 4 * threadIdx.x;
-  // loads that do not depend on the previous launch: LN / mix vectors, row descriptor, shift state
+  // loads that do not depend on the previous launch: LN / mix vectors
   const float4_ w = ld4(a.ln_w + c), b = ld4(a.ln_b + c);
   float4_ mu[NMIX > 0 ? NMIX : 1];
 #pragma unroll
   for (int m = 0; m < NMIX; ++m) mu[m] = ld4(a.mu[m] + c);
+  // the residual and the partial slabs (the previous launch's output) go out before the row
+  // descriptor, whose dependent round trip only addresses the shift state
+  float4_ v = ld4(e_hin + (int64_t)row * C + c);
+  float4_ t[NP > 0 ? NP : 1];
+#pragma unroll
+  for (int p = 0; p < NP; ++p) t[p] = ld4(e_part + p * e_pstride + (int64_t)row * e_ldp + c);
   int slot = 0, flags = 0, prev_row = -1, par = 0;
   float4_ pv = {0.f, 0.f, 0.f, 0.f};
   if constexpr (MODE == 1) {
     const int4 info = a.rows[row];
     slot = info.x; flags = info.y; prev_row = info.z; par = info.w;
-    if (prev_row < 0) pv = ld4(a.shift + (((int64_t)par * a.S + slot) * a.L + a.layer) * C + c);
+    if (prev_row < 0) pv = ld4(e_shift + (((int64_t)par * e_S + slot) * e_L + e_layer) * C + c);
   }
-  float4_ v = ld4(a.h_in + (int64_t)row * C + c);
-  float4_ t[NP > 0 ? NP : 1];
-#pragma unroll
-  for (int p = 0; p < NP; ++p) t[p] = ld4(a.part + p * a.part_stride + (int64_t)row * a.ldp + c);
 #pragma unroll
   for (int p = 0; p < NP; ++p) v += t[p];
-  if (a.h_out) *(float4_*)(a.h_out + (int64_t)row * C + c) = v;
+  if (e_hout) *(float4_*)(e_hout + (int64_t)row * C + c) = v;
   auto ln = [&](float4_& x, int slot_base) {
     const float mean = block_sum_1b((x[0] + x[1]) + (x[2] + x[3]), red, slot_base) * (1.0f / C);
     const float4_ d = x - mean;
@@ -322,13 +336,13 @@ __global__ __launch_bounds__(256) void k_ln1024(LnMixArgs a) {
     *(uint2*)(lo + idx) = make_uint2(l0, l1);
   };
   if constexpr (MODE == 0) {
-    store(v, a.x_hi, a.x_lo, (int64_t)out_row * a.ldx + c);
+    store(v, e_xhi, e_xlo, (int64_t)out_row * e_ldx + c);
   } else {
     if (prev_row >= 0) {  // prefill row: the previous token's LN output, recomputed identically
-      pv = ld4(a.h_in + (int64_t)prev_row * C + c);
+      pv = ld4(e_hin + (int64_t)prev_row * C + c);
       float4_ tp[NP > 0 ? NP : 1];
 #pragma unroll
-      for (int p = 0; p < NP; ++p) tp[p] = ld4(a.part + p * a.part_stride + (int64_t)prev_row * a.ldp + c);
+      for (int p = 0; p < NP; ++p) tp[p] = ld4(e_part + p * e_pstride + (int64_t)prev_row * e_ldp + c);
 #pragma unroll
       for (int p = 0; p < NP; ++p) pv += tp[p];
       ln(pv, 2);
@@ -336,10 +350,10 @@ __global__ __launch_bounds__(256) void k_ln1024(LnMixArgs a) {
 #pragma unroll
     for (int m = 0; m < NMIX; ++m) {
       const float4_ x = v + (pv - v) * mu[m];
-      store(x, a.x_hi + m * a.mix_stride, a.x_lo + m * a.mix_stride, (int64_t)out_row * a.ldx + c);
+      store(x, e_xhi + m * e_mix, e_xlo + m * e_mix, (int64_t)out_row * e_ldx + c);
     }
     if (flags & kRowLast)
-      *(float4_*)(a.shift + (((int64_t)(a.inplace ? par : par ^ 1) * a.S + slot) * a.L + a.layer) * C + c) = v;
+      *(float4_*)(e_shift + (((int64_t)(e_inpl ? par : par ^ 1) * e_S + slot) * e_L + e_layer) * C + c) = v;
   }
   tl_end(a.tl);
 }
@@ -509,6 +523,9 @@ __global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
   bf16_t* xh = (bf16_t*)smem;
   bf16_t* xl = xh + ROWS * LD;
   tl_begin(a.tl);
+  float* e_out = a.out;
+  int64_t e_sstride = a.split_stride;
+  int e_ldo = a.ldo, e_M = a.M;
   const int tile = blockIdx.x;
   // MS 0: one segment, read from seg[0] directly. MS 1: several segments, looked up from the
   // tile starts (a second, dependent kernel-argument round trip). MS 2: several segments
@@ -643,13 +660,13 @@ __global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
   // 5) store (D layout: col = lane&15, row = 4*(lane>>4) + j)
   const int col = col0 + li;
   if (col < Nn) {
-    float* out = a.out + split * a.split_stride + col_off + col;
+    float* out = e_out + split * e_sstride + col_off + col;
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int row = row0 + m * 16 + 4 * g + j;
-        if (row < a.M) out[(int64_t)row * a.ldo] = acc_h[m][j] + acc_l[m][j];
+        if (row < e_M) out[(int64_t)row * e_ldo] = acc_h[m][j] + acc_l[m][j];
       }
   }
   tl_end(a.tl);
@@ -1282,6 +1299,9 @@ __global__ __launch_bounds__(128) void k_wkv4(WkvArgs a) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, i = t >> 1, hf = t & 1;
   const int h = blockIdx.y, C = a.C, c = h * N + i;
   tl_begin(a.tl);
+  bf16_t* e_zhi = a.z_hi;
+  bf16_t* e_zlo = a.z_lo;
+  int e_ldz = a.ldz;
   const int4 sg = a.segs[blockIdx.x];
   // ---- head-only loads: half of channel c's LoRA-up rows + parameters
   uint4 lw[18];  // 8 bf16 per entry: w 0..3 | a 4..7 | v 8..9 | g 10..17
@@ -1442,7 +1462,7 @@ __global__ __launch_bounds__(128) void k_wkv4(WkvArgs a) {
     const float var = fmaxf((s_red[3][0] + s_red[3][1]) * (1.0f / N) - mean * mean, 0.f);
     if (hf == 0) {
       const float gn = (y - mean) * __builtin_amdgcn_rsqf(var + 64e-5f) * lnw + lnb;
-      split_store((gn + bonus * v) * lo3, a.z_hi, a.z_lo, (int64_t)row * a.ldz + c, F16);
+      split_store((gn + bonus * v) * lo3, e_zhi, e_zlo, (int64_t)row * e_ldz + c, F16);
     }
     if (rr + 1 < n_rows) __syncthreads();
   }
