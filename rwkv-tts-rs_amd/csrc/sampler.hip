@@ -230,15 +230,42 @@ __device__ inline float block_max(float v, float* fred) {
   return m;
 }
 
-// block-wide exclusive scans (NT threads): wave shuffles + NT/64 wave totals
+// DPP row shift: lane l of each 16-lane row receives lane l - N of the same row, lanes with no
+// source receive 0 (the update's old value)
+template <int N>
+__device__ inline int dpp_shr(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, 0x110 + N, 0xF, 0xF, false);
+}
+template <int N>
+__device__ inline double dpp_shr(double v) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)dpp_shr<N>((int)(uint32_t)u), hi = (uint32_t)dpp_shr<N>((int)(uint32_t)(u >> 32));
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+__device__ inline double readlane_d(double v, int l) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+__device__ inline int readlane_t(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ inline double readlane_t(double v, int l) { return readlane_d(v, l); }
+
+// block-wide exclusive scans (NT threads): per wave an inclusive scan of each 16-lane row on DPP
+// row shifts, row offsets from the row totals (readlane), then the NT/64 wave totals
 template <int NT, typename T>
 __device__ inline T block_excl_scan_t(T v, T* scratch, T* tot) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   T x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const T y = __shfl_up(x, o);
-    if (lane >= o) x += y;
+  x += dpp_shr<1>(x);
+  x += dpp_shr<2>(x);
+  x += dpp_shr<4>(x);
+  x += dpp_shr<8>(x);
+  {
+    const T r0 = readlane_t(x, 15), r1 = readlane_t(x, 31), r2 = readlane_t(x, 47);
+    const int row = lane >> 4;
+    const T off = row == 0 ? (T)0 : (row == 1 ? r0 : (row == 2 ? r0 + r1 : (r0 + r1) + r2));
+    x += off;
   }
   __syncthreads();
   if (lane == 63) scratch[w] = x;
@@ -532,17 +559,19 @@ __device__ __attribute__((always_inline)) int sample_block(const SampleSmem& sm,
       const int b = min(n, tid * chunk), e = min(n, b + chunk);
       float lm = -1.0f;  // every p >= 0
       for (int i = b; i < e; ++i) lm = fmaxf(lm, sm.p[i]);
-      // wave bitonic sort (descending) of the 64 local maxima
+      // the kw-th largest of the wave's 64 local maxima: the value v with #{> v} < kw <= #{>= v}
+      // (every lane counts against all 64 values read back through readlane; ties give the same v)
       const int lane = tid & 63;
-      float v = lm;
-      for (int k = 2; k <= 64; k <<= 1)
-        for (int j = k >> 1; j > 0; j >>= 1) {
-          const float o = __shfl_xor(v, j);
-          const bool up = ((lane & k) == 0) == ((lane & j) == 0);
-          v = up ? fmaxf(v, o) : fminf(v, o);
-        }
       const int kw = (top_k + NT / 64 - 1) / (NT / 64);
-      const float vw = __shfl(v, kw - 1);
+      int gt = 0, ge = 0;
+#pragma unroll 16
+      for (int j = 0; j < 64; ++j) {
+        const float o = readlane_f(lm, j);
+        gt += o > lm ? 1 : 0;
+        ge += o >= lm ? 1 : 0;
+      }
+      const uint64_t selm = __ballot(gt < kw && kw <= ge);
+      const float vw = readlane_f(lm, __builtin_ctzll(selm));
       if (lane == 0) sm.fred[tid >> 6] = vw;
       __syncthreads();
       float Lm = sm.fred[0];
@@ -556,11 +585,25 @@ __device__ __attribute__((always_inline)) int sample_block(const SampleSmem& sm,
       if (tot <= kSampleMaxSorted) {
         for (int i = b; i < e; ++i)
           if (sm.p[i] >= L) sm.keys[off++] = pkey(sm.p[i], i);
-        int M = 1;
-        while (M < tot) M <<= 1;
-        for (int q = tot + tid; q < M; q += NT) sm.keys[q] = 0ull;
-        __syncthreads();
-        bitonic_desc<NT>(sm.keys, M);
+        if (tot <= NT) {
+          // rank sort (keys are unique): candidate tid's place = number of larger keys; every
+          // thread reads the same key per iteration (LDS broadcast) and one barrier replaces the
+          // bitonic network's log2(M)(log2(M)+1)/2 barrier stages
+          __syncthreads();
+          const uint64_t kq = tid < tot ? sm.keys[tid] : 0ull;
+          int rank = 0;
+          if (tid < tot)
+            for (int j = 0; j < tot; ++j) rank += sm.keys[j] > kq ? 1 : 0;
+          __syncthreads();
+          if (tid < tot) sm.keys[rank] = kq;
+          __syncthreads();
+        } else {
+          int M = 1;
+          while (M < tot) M <<= 1;
+          for (int q = tot + tid; q < M; q += NT) sm.keys[q] = 0ull;
+          __syncthreads();
+          bitonic_desc<NT>(sm.keys, M);
+        }
         // zero everything, then restore the k survivors
         for (int i = tid; i < n; i += NT) sm.p[i] = 0.0f;
         __syncthreads();
