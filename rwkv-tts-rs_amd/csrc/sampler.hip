@@ -205,7 +205,7 @@ struct SampleSmem {
   int* scan;          // [8] block-scan wave totals
   double* dscan;      // [8]
   uint32_t* sub_t;    // [NT][2] sub-chunk parity maps of the exact-sum emulation
-  int* sub_ok;        // [NT]
+  int* sub_e;         // [NT] binade each sub-chunk map was simulated for (kNoBinade: unusable)
   int* chunk_e;       // [64] predicted binade per chunk
   uint32_t* chunk_t;  // [64][2]
   int* chunk_ok;      // [64]
@@ -363,12 +363,15 @@ __device__ inline void sum_sim_elem(uint32_t b, int E, uint32_t& T0, uint32_t& T
   if (T0 >= 0x1000000u || T1 >= 0x1000000u) ok = false;
 }
 
+constexpr int kNoBinade = 1 << 20;  // sub_e of a sub-chunk whose simulation failed
+
 template <int NT>
 __device__ float exact_seq_sum(const SampleSmem& sm, int n, uint64_t* stamps = nullptr) {
   constexpr int NS = NT / 64;  // sub-chunks per chunk (64 chunks, one per lane of wave 0)
   constexpr int NE = NT >= 1024 ? 64 : 128;  // serial-add register batch
   const int tid = threadIdx.x;
-  const int CH = (((n + 63) / 64) + 3) & ~3, SUB = (CH + NS - 1) / NS;  // chunks start 16-byte aligned
+  // chunks and sub-chunks start 16-byte aligned (the serial adds read float4)
+  const int CH = (((n + 63) / 64) + 3) & ~3, SUB = (((CH + NS - 1) / NS) + 3) & ~3;
   const int chunk = tid / NS, sub = tid % NS;
   const int cb = min(n, chunk * CH), ce = min(n, cb + CH);
   const int sb = min(ce, cb + sub * SUB), se = min(ce, sb + SUB);
@@ -377,8 +380,9 @@ __device__ float exact_seq_sum(const SampleSmem& sm, int n, uint64_t* stamps = n
   double dtot;
   const double pre = block_excl_scan_t<NT, double>(ds, sm.dscan, &dtot);
   STAMP(10);
-  const double pchunk = __shfl(pre, (tid & 63) & ~(NS - 1));  // prefix at the chunk start
-  const float pf = (float)pchunk;
+  // every sub-chunk is simulated for the binade predicted from the prefix at its OWN start, so a
+  // chunk that crosses a binade still has usable sub-chunk maps on either side of the crossing
+  const float pf = (float)pre;
   const uint32_t pb = __builtin_bit_cast(uint32_t, pf);
   const int E = (int)((pb >> 23) & 0xFFu) - 127;
   bool ok = pf >= 0x1p-100f && pf < 0x1p+100f;
@@ -387,13 +391,14 @@ __device__ float exact_seq_sum(const SampleSmem& sm, int n, uint64_t* stamps = n
   for (int i = sb; i < se && ok; ++i) sum_sim_elem(__builtin_bit_cast(uint32_t, sm.p[i]), E, T0, T1, q0, q1, ok);
   sm.sub_t[2 * tid] = T0;
   sm.sub_t[2 * tid + 1] = T1;
-  sm.sub_ok[tid] = ok;
-  if (sub == 0) sm.chunk_e[chunk] = E;
+  sm.sub_e[tid] = ok ? E : kNoBinade;
   __syncthreads();
   STAMP(11);
-  if (tid < 64) {  // compose the NS sub-chunk maps of chunk `tid`
-    bool cok = true;
-    for (int s = 0; s < NS; ++s) cok &= sm.sub_ok[NS * tid + s] != 0;
+  if (tid < 64) {  // compose the NS sub-chunk maps of chunk `tid` (all predicted in one binade)
+    const int clen = min(n, tid * CH + CH) - min(n, tid * CH);
+    const int E0 = sm.sub_e[NS * tid];
+    bool cok = E0 != kNoBinade;
+    for (int s = 1; s < NS; ++s) cok &= s * SUB >= clen || sm.sub_e[NS * tid + s] == E0;
     for (int pin = 0; pin < 2; ++pin) {
       int par = pin;
       uint32_t T = 0;
@@ -406,6 +411,7 @@ __device__ float exact_seq_sum(const SampleSmem& sm, int n, uint64_t* stamps = n
       sm.chunk_t[2 * tid + pin] = T;
     }
     sm.chunk_ok[tid] = cok;
+    sm.chunk_e[tid] = E0;
   }
   __syncthreads();
   STAMP(12);
@@ -435,6 +441,47 @@ __device__ float exact_seq_sum(const SampleSmem& sm, int n, uint64_t* stamps = n
       }
     }
     const uint64_t heads = __ballot(head) & (nch >= 64 ? ~0ull : ((1ull << nch) - 1ull));
+    // chunk `lane`'s sub-chunk maps, for chunks that cannot be applied whole
+    uint32_t sT0[NS], sT1[NS];
+    int sE[NS];
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+      sT0[j] = sm.sub_t[2 * (NS * lane + j)];
+      sT1[j] = sm.sub_t[2 * (NS * lane + j) + 1];
+      sE[j] = sm.sub_e[NS * lane + j];
+    }
+    // chunk c in order: each sub-chunk by its map when s is in the binade it was simulated for
+    // and stays there, otherwise element by element on one lane
+    auto add_chunk = [&](float s, int c) -> float {
+      const int cb0 = c * CH, ce0 = min(n, cb0 + CH);
+#pragma unroll
+      for (int j = 0; j < NS; ++j) {
+        const int b1 = cb0 + j * SUB;
+        if (b1 < ce0) {
+          s = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, s)));
+          const uint32_t sb4 = __builtin_bit_cast(uint32_t, s);
+          const int ef4 = (int)((sb4 >> 23) & 0xFFu);
+          bool fast = false;
+          if (ef4 != 0 && ef4 - 127 == readlane_i(sE[j], c)) {
+            const uint32_t m = (sb4 & 0x7FFFFFu) | 0x800000u;
+            const uint32_t T = (uint32_t)((m & 1u) ? readlane_i((int)sT1[j], c) : readlane_i((int)sT0[j], c));
+            if (m + T < 0x1000000u) {
+              s = __builtin_bit_cast(float, (sb4 & 0xFF800000u) | ((m + T) & 0x7FFFFFu));
+              fast = true;
+            }
+          }
+          if (!fast) {
+            const int e1 = min(ce0, b1 + SUB);
+            float t = 0.0f;
+            const uint64_t fb = stamps ? __builtin_amdgcn_s_memtime() : 0;
+            if (lane == 0) t = lane_serial_add<NE>(s, sm.p, b1, e1);
+            s = readlane_f(t, 0);
+            if (stamps && tid == 0) stamps[15] += __builtin_amdgcn_s_memtime() + (uint64_t)(s != s) - fb;
+          }
+        }
+      }
+      return s;
+    };
     float s = 0.0f;
     int c = 0;
     while (c < nch) {
@@ -457,13 +504,8 @@ __device__ float exact_seq_sum(const SampleSmem& sm, int n, uint64_t* stamps = n
           continue;
         }
       }
-      // unusable chunk, or a run whose prediction failed: add chunk c in order on one lane
-      const int b0 = c * CH, e0 = min(n, b0 + CH);
-      float t = 0.0f;
-      const uint64_t fb0 = stamps ? __builtin_amdgcn_s_memtime() : 0;
-      if (lane == 0) t = lane_serial_add<NE>(s, sm.p, b0, e0);
-      s = readlane_f(t, 0);
-      if (stamps && tid == 0) stamps[15] += __builtin_amdgcn_s_memtime() + (uint64_t)(s != s) - fb0;
+      // unusable chunk, or a run whose prediction failed: add chunk c sub-chunk by sub-chunk
+      s = add_chunk(s, c);
       ++c;
       // the chunks after c (if inside a run) are no longer run heads; step them one at a time
       while (c < nch && !((heads >> c) & 1ull)) {
@@ -481,14 +523,7 @@ __device__ float exact_seq_sum(const SampleSmem& sm, int n, uint64_t* stamps = n
             ++nfast;
           }
         }
-        if (!fast) {
-          const int b1 = c * CH, e1 = min(n, b1 + CH);
-          float t1 = 0.0f;
-          const uint64_t fb1 = stamps ? __builtin_amdgcn_s_memtime() : 0;
-          if (lane == 0) t1 = lane_serial_add<NE>(s, sm.p, b1, e1);
-          s = readlane_f(t1, 0);
-          if (stamps && tid == 0) stamps[15] += __builtin_amdgcn_s_memtime() + (uint64_t)(s != s) - fb1;
-        }
+        if (!fast) s = add_chunk(s, c);
         ++c;
       }
     }
@@ -807,7 +842,7 @@ __device__ SampleSmem carve(char* base, int n) {
   sm.list = (int*)q; q += kSampleMaxSorted * 4;
   sm.scan = (int*)q; q += 16 * 4;
   sm.sub_t = (uint32_t*)q; q += 2 * NT * 4;
-  sm.sub_ok = (int*)q; q += NT * 4;
+  sm.sub_e = (int*)q; q += NT * 4;
   sm.chunk_e = (int*)q; q += 64 * 4;
   sm.chunk_t = (uint32_t*)q; q += 128 * 4;
   sm.chunk_ok = (int*)q; q += 64 * 4;
