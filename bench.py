@@ -10,7 +10,9 @@ audio samples (320 per semantic token @16 kHz) / max-over-ranks wall time. Each 
 BiCodec decoder (HIP MFMA conv stack, assumed SparkTTS dims, random-init weights) turning every
 request's 32 global + 512 semantic tokens into PCM, so the timed region is tokens -> waveform.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]; N>1 under torch.distributed.run.
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]. N > 1 runs one process per GPU:
+under torch.distributed.run (RANK / WORLD_SIZE set by the launcher), or, when WORLD_SIZE is unset,
+bench.py starts the N ranks itself (before anything touches a GPU) and relays rank 0's line.
 """
 import argparse
 import json
@@ -96,12 +98,18 @@ def main():
                     help="run the vocoder of each batch after its LM decode instead of overlapped")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
+
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a "
+                         "different GPU count than asked for")
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -276,18 +284,56 @@ def main():
         dist.destroy_process_group()
 
 
+def spawn_ranks(n):
+    """--gpus N without a launcher: start ranks 0..N-1 as child processes (this process never
+    touches a GPU), rendezvous on 127.0.0.1, and exit with the first non-zero child status."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    for p in procs:
+        c = p.wait()
+        rc = rc or c
+    return rc
+
+
+def host_cpu():
+    """nproc and the CPU model of this host (lscpu 'Model name')."""
+    model = ""
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return os.cpu_count(), model
+
+
 def cpu_baseline(dims, cdims, seconds):
-    """The oracle (C restatement of the reference path, f32 math on bf16 weights, 1 request,
-    OpenMP over the host cores) timed on a bounded sample of the same request, extrapolated to
-    the full request (P + 33 + S - 1 forwards -> 320*S samples), plus the oracle vocoder timed
-    on a 16-frame utterance and scaled linearly to S frames (convolutions are linear in T)."""
+    """The oracle (C restatement of the reference path: fp16-stored weights, f32 math -- web-rwkv's
+    Bundle<f32> numerics -- 1 request, sequential like process_batch_with_independent_contexts)
+    built here with -O3 -march=native (the reference builds with target-cpu=native,
+    .cargo/config.toml:2) and run with OpenMP on this process's CPU share (OMP_NUM_THREADS, else
+    every core), timed on a bounded sample of the same request and extrapolated to the full
+    request (P + 33 + S - 1 forwards -> 320*S samples), plus the oracle vocoder timed on a
+    16-frame utterance and scaled linearly to S frames (convolutions are linear in T)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
+    from rwkvtts import _ffi
     from rwkvtts import weights as W
+    oracle.use_native()
     cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
-    cores = min(cores, 16)
     oracle.lib().oracle_set_threads(cores)
-    blob = W.synth_blob(dims, seed=20251205)
+    nproc, model = host_cpu()
+    blob = W.synth_blob(dims, seed=20251205, dtype=_ffi.DTYPE_F16)
     om = oracle.Model(blob)
     del blob
     st = om.new_state()
@@ -312,7 +358,9 @@ def cpu_baseline(dims, cdims, seconds):
     voc_s = (time.perf_counter() - t1) * SEMANTIC / Tc
     val = 320 * SEMANTIC / (fwd_per_req * per_fwd + voc_s)
     return {"value": round(val, 1), "unit": "samples/s", "cores": cores, "kind": "port",
-            "sample": f"oracle f32 RWKV-7 forward, 1 request, {n} forwards timed ({per_fwd*1e3:.1f} ms each), "
+            "host": {"nproc": nproc, "model": model, "build": "gcc -O3 -march=native -fopenmp"},
+            "sample": f"oracle f32 RWKV-7 forward on fp16 weights, 1 request, {n} forwards timed "
+                      f"({per_fwd*1e3:.1f} ms each), "
                       f"extrapolated to {fwd_per_req} forwards; oracle vocoder on {Tc} frames scaled to "
                       f"{SEMANTIC} ({voc_s:.2f} s); {320*SEMANTIC} samples per request"}
 

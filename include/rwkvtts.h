@@ -5,8 +5,10 @@
  * (paths relative to the reference root); the Rust-side binding a maintainer would add is in
  * INTEGRATION.md. Conventions: plain pointers + sizes, opaque handles, int status (0 = OK,
  * negative = error, message via rwkvtts_last_error()), no exceptions across the ABI, all
- * buffers caller-owned. One engine per GPU; calls on an engine come from one owning host
- * thread except rwkvtts_manager_submit/poll, which are thread-safe.
+ * buffers caller-owned. One engine per GPU. Engine entry points serialise on a per-engine
+ * lock (concurrent callers queue; they do not share GPU steps); the request manager
+ * (rwkvtts_manager_*: DynamicBatchManager) is the thread-safe, batching front door: any number
+ * of threads submit, one owner thread per GPU engine runs continuous batching.
  */
 #ifndef RWKVTTS_H
 #define RWKVTTS_H
@@ -36,7 +38,8 @@ extern "C" {
 #define RWKVTTS_EHIP -2
 #define RWKVTTS_ENOMEM -3
 #define RWKVTTS_EUNSUPPORTED -4
-#define RWKVTTS_EBUSY -5
+#define RWKVTTS_EBUSY -5     /* manager: result not ready yet (poll / wait timeout) */
+#define RWKVTTS_ECLOSED -6   /* manager: shut down before the request ran */
 
 /* weight storage dtypes (matrices; vectors are always f32) */
 #define RWKVTTS_DTYPE_BF16 0
@@ -149,6 +152,8 @@ typedef struct {
   int32_t max_slots;        /* state slots = Bundle max_batch (shared_runtime.rs:177) */
   int32_t token_chunk_size; /* rows per forward = RnnInput token_chunk_size (lightweight_tts_pipeline.rs:799) */
   int32_t use_graphs;       /* capture decode steps in hipGraphs */
+  int32_t wkv_variant;      /* 0 auto; 1 k_wkv4 (2 waves per (slot, head)); 2 k_wkv6 (4 waves).
+                               0.4B LoRA ranks only; both are tested against the oracle */
 } rwkvtts_engine_desc;
 
 /* weights: packed blob (header included). blob_on_device != 0: `weights` is a device pointer
@@ -223,13 +228,24 @@ typedef struct {
   int32_t n_ref_semantic;
   int32_t has_seed;
   uint64_t seed;
-  int32_t max_tokens;          /* SamplerArgs.max_tokens (semantic limit = min(max_tokens, 2048)) */
+  int32_t max_tokens;          /* SamplerArgs.max_tokens; normal mode emits at most
+                                  min(max_tokens, 2048) semantic tokens (normal_mode_inference.rs:316),
+                                  so 0 -> none; must be >= 0 (usize) */
   int32_t fixed_semantic;      /* >0: benchmark mode -- EOS masked, exactly this many semantic tokens */
   int32_t greedy;              /* 1: top_k = 1 for both phases (config 1 plumbing check) */
+  /* SamplerArgs.layered_randomness (LayeredRandomnessConfig, rwkv_sampler.rs:251-275) as used
+   * by normal_mode_inference.rs:138-174 and zero_shot_inference.rs:204-216.
+   * layered_set == 0 selects LayeredRandomnessConfig::default() (independent, 1000 / 2000). */
+  int32_t layered_set;
+  int32_t use_independent_seeds; /* 1: StdRng(seed + offset); 0: StdRng(seed + 100 / + 200),
+                                    zero-shot StdRng(0) (dynamic_batch_manager.rs:491-494) */
+  uint64_t global_seed_offset;
+  uint64_t semantic_seed_offset;
 } rwkvtts_request;
 
 typedef struct {
-  int32_t status;         /* 0 ok; <0 error -> (vec![], vec![]) as dbm.rs:387-392 */
+  int32_t status;         /* 0 ok; <0 this request failed -> (vec![], vec![]) as dbm.rs:466-469
+                             (the others of its batch still complete) */
   int32_t n_global;
   int32_t n_semantic;
   int32_t global_tokens[RWKVTTS_N_GLOBAL];
@@ -237,10 +253,54 @@ typedef struct {
 } rwkvtts_result;
 
 /* DynamicBatchManager::generate_tts_batch (dynamic_batch_manager.rs:124-164) with real GPU
- * continuous batching: up to max_slots requests decode together, one slot each. Per-request
- * outputs are identical to running the requests one at a time. */
+ * continuous batching: up to max_slots requests decode together, one slot each; a request is
+ * admitted as soon as a slot frees, and its prompt rows ride in the same forward steps as the
+ * other slots' decode rows. Per-request outputs are identical to running the requests one at a
+ * time. Returns RWKVTTS_OK when the batch ran (per-request failures are in results[i].status),
+ * or a negative code when the engine itself failed (then every status is that code). */
 int rwkvtts_generate_batch(rwkvtts_engine* e, const rwkvtts_request* reqs, int n,
                            rwkvtts_result* results);
+
+/* ---- request manager: DynamicBatchManager (dynamic_batch_manager.rs:22-164,185-405) ------ */
+/* The reference collects requests (enqueue_worker: first request, then try_recv up to
+ * max_batch_size; a lone request waits >= 10 ms for company, :185-264) and hands each batch to
+ * whichever infer worker is free (:350-405), which then runs the batch sequentially on state
+ * slot 0. Here one owner thread per engine (one engine per GPU: request-level data parallelism
+ * over the node's GPUs) runs continuous batching; each collected batch is routed to
+ * the least-loaded engine (fewest requests active + queued), and an engine admits queued
+ * requests between forward steps whenever it has free slots. Any thread may submit / wait. */
+typedef struct rwkvtts_manager rwkvtts_manager;
+#define RWKVTTS_MAX_ENGINES 16
+typedef struct {
+  int32_t n_engines;                      /* engines (owner threads) */
+  int32_t devices[RWKVTTS_MAX_ENGINES];   /* HIP device of each engine (repeats allowed) */
+  rwkvtts_engine_desc engine;             /* per-engine settings (its .device is ignored) */
+  int32_t max_batch_size;                 /* DynamicBatchConfig.max_batch_size (batch_types.rs:71) */
+  int32_t collect_timeout_ms;             /* DynamicBatchConfig.collect_timeout_ms (batch_types.rs:73) */
+} rwkvtts_manager_desc;
+/* weights: one host blob, uploaded to every engine's device. */
+int rwkvtts_manager_create(const rwkvtts_manager_desc* desc, const void* weights, size_t bytes,
+                           rwkvtts_manager** out);
+/* Stops the collector and the engine threads after the requests already submitted finish. */
+int rwkvtts_manager_destroy(rwkvtts_manager* m);
+/* generate_tts (dynamic_batch_manager.rs:90-121) split in two: submit copies the request
+ * (token arrays included) and returns a ticket; wait blocks up to timeout_ms (< 0: forever) and
+ * returns RWKVTTS_OK with the result (the ticket is then released), RWKVTTS_EBUSY if the
+ * request has not finished yet. out->semantic_tokens must hold RWKVTTS_SEMANTIC_LIMIT ids. */
+int rwkvtts_manager_submit(rwkvtts_manager* m, const rwkvtts_request* req, uint64_t* ticket);
+int rwkvtts_manager_wait(rwkvtts_manager* m, uint64_t ticket, int timeout_ms, rwkvtts_result* out);
+/* generate_tts_batch (dynamic_batch_manager.rs:124-164): submit all, wait all. */
+int rwkvtts_manager_generate_batch(rwkvtts_manager* m, const rwkvtts_request* reqs, int n,
+                                   rwkvtts_result* results);
+typedef struct {
+  int64_t submitted;
+  int64_t completed;
+  int64_t batches;                          /* batches the collector formed */
+  int64_t served[RWKVTTS_MAX_ENGINES];      /* requests completed per engine */
+  int64_t max_active[RWKVTTS_MAX_ENGINES];  /* most slots an engine had decoding at once */
+  int64_t steps[RWKVTTS_MAX_ENGINES];       /* forward steps per engine */
+} rwkvtts_manager_stats;
+int rwkvtts_manager_get_stats(rwkvtts_manager* m, rwkvtts_manager_stats* out);
 
 /* Step-level statistics of the last generate call (bench / roofline). */
 typedef struct {

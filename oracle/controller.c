@@ -11,7 +11,8 @@
  *      prompt = property ⧺ [TAG_2] ⧺ text ⧺ [TAG_0] ⧺ (clamp(g,0,4095)+8196)... ⧺ [TAG_1]
  *      (:47,76-85); EOS masked while i < hard_min (:128-142,256-261); window rule (12, 0.7) with
  *      re-draw (:219-309). Seed: the reference ignores it (B5); this build seeds the semantic
- *      stream with seed+2000 when a seed is given, as normal mode does.
+ *      stream with seed + semantic_seed_offset when a seed is given, as normal mode does
+ *      (StdRng(0) when use_independent_seeds is off, as the reference).
  *  - benchmark extensions: fixed_semantic > 0 masks EOS and emits exactly that
  *      many semantic tokens; greedy forces top_k = 1 in both phases.
  * Sampling always sees the prefix rows that can be drawn (global: 4096; semantic: 8193);
@@ -50,6 +51,14 @@ int oracle_generate(const oracle_model* m, const rwkvtts_request* req, oracle_re
 
   const int zero_shot = req->ref_global != NULL && req->ref_semantic != NULL;
   const uint64_t seed = req->has_seed ? req->seed : 0; /* no seed: caller must pass one */
+  /* LayeredRandomnessConfig (rwkv_sampler.rs:251-275): normal_mode_inference.rs:138-174 */
+  const int indep = req->layered_set ? req->use_independent_seeds != 0 : 1;
+  const uint64_t goff = req->layered_set ? req->global_seed_offset : 1000;
+  const uint64_t soff = req->layered_set ? req->semantic_seed_offset : 2000;
+  const uint64_t gseed = indep ? seed + goff : seed + 100;
+  /* zero-shot without independent seeds: the StdRng::seed_from_u64(0) of
+   * dynamic_batch_manager.rs:491-494 (zero_shot_inference.rs:204-216) */
+  const uint64_t sseed = indep ? seed + soff : (zero_shot ? 0 : seed + 200);
 
   /* ---- prompt ---- */
   int n_prompt = req->n_property + 1 + req->n_text + 1 + (zero_shot ? req->n_ref_global + 1 : 0);
@@ -71,14 +80,15 @@ int oracle_generate(const oracle_model* m, const rwkvtts_request* req, oracle_re
   free(prompt);
 
   const int kg = req->greedy ? 1 : 20, ks = req->greedy ? 1 : 80;
-  int limit = req->max_tokens > 0 ? req->max_tokens : RWKVTTS_SEMANTIC_LIMIT;
+  /* usize::min(max_tokens, 2048) (normal_mode_inference.rs:316): 0 -> no semantic tokens */
+  int limit = req->max_tokens > 0 ? req->max_tokens : 0;
   if (limit > RWKVTTS_SEMANTIC_LIMIT) limit = RWKVTTS_SEMANTIC_LIMIT;
   if (req->fixed_semantic > 0) limit = req->fixed_semantic < RWKVTTS_SEMANTIC_LIMIT ? req->fixed_semantic : RWKVTTS_SEMANTIC_LIMIT;
 
   if (!zero_shot) {
     oracle_rng rg, rs;
-    oracle_rng_seed_from_u64(seed + 1000, &rg);
-    oracle_rng_seed_from_u64(seed + 2000, &rs);
+    oracle_rng_seed_from_u64(gseed, &rg);
+    oracle_rng_seed_from_u64(sseed, &rs);
     for (int i = 0; i < RWKVTTS_N_GLOBAL; ++i) {
       if (i > 0) feed(&rn, (uint32_t)(out->global_tokens[i - 1] + RWKVTTS_GLOBAL_TOKEN_OFFSET), 1);
       int id = oracle_sample(rn.logits, 4096, 1.0f, 0.95f, kg, -1, &rg);
@@ -100,7 +110,7 @@ int oracle_generate(const oracle_model* m, const rwkvtts_request* req, oracle_re
       out->global_tokens[out->n_global++] = g < 0 ? 0 : (g > 4095 ? 4095 : g);
     }
     oracle_rng rs;
-    oracle_rng_seed_from_u64(seed + 2000, &rs);
+    oracle_rng_seed_from_u64(sseed, &rs);
     const int tlen = req->n_text;
     int min_sem = tlen / 4;
     min_sem = min_sem < 8 ? 8 : (min_sem > 64 ? 64 : min_sem);

@@ -29,6 +29,14 @@ def build():
     subprocess.check_call(["make", "-s", "-C", _HERE])
 
 
+def use_native():
+    """Switch to the -march=native build (built on first use on this host; bench cpu_baseline)."""
+    global LIB, _lib
+    subprocess.check_call(["make", "-s", "-C", _HERE, "native"])
+    LIB = os.path.join(_HERE, "liboracle_native.so")
+    _lib = None
+
+
 def lib():
     global _lib
     if _lib is None:

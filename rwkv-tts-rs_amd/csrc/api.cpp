@@ -2,6 +2,7 @@
 // method; errors become status codes + a thread-local message, never C++ exceptions.
 #include <string.h>
 
+#include <mutex>
 #include <new>
 
 #include "engine.h"
@@ -13,9 +14,14 @@ void set_error(const std::string& msg) { g_last_error = msg; }
 
 using namespace rwkvtts;
 
+// Every entry point on an engine holds its lock: concurrent host threads serialise (the engine
+// owns one stream, one set of step tables and the slot map). Batching across callers is the
+// manager's job (manager.cpp).
 struct rwkvtts_engine {
+  std::mutex mu;
   Engine eng;
 };
+#define LOCK(e) std::lock_guard<std::mutex> lock_((e)->mu)
 
 #define GUARD(body)                                      \
   try {                                                  \
@@ -49,6 +55,9 @@ int rwkvtts_engine_create(const rwkvtts_engine_desc* desc, const void* weights, 
 }
 
 int rwkvtts_engine_destroy(rwkvtts_engine* e) {
+  if (e) {
+    std::lock_guard<std::mutex> lk(e->mu);  // wait for a call still running on another thread
+  }
   delete e;
   return RWKVTTS_OK;
 }
@@ -63,26 +72,31 @@ int64_t rwkvtts_state_floats(const rwkvtts_engine* e) { return e ? e->eng.state_
 
 int rwkvtts_slot_reset(rwkvtts_engine* e, int slot) {
   RT_CHECK(e, RWKVTTS_EINVAL, "null engine");
+  LOCK(e);
   GUARD({ return e->eng.slot_reset(slot); })
 }
 int rwkvtts_slot_read(rwkvtts_engine* e, int slot, float* out) {
   RT_CHECK(e && out, RWKVTTS_EINVAL, "null argument");
+  LOCK(e);
   GUARD({ return e->eng.slot_read(slot, out); })
 }
 int rwkvtts_slot_write(rwkvtts_engine* e, int slot, const float* in) {
   RT_CHECK(e && in, RWKVTTS_EINVAL, "null argument");
+  LOCK(e);
   GUARD({ return e->eng.slot_write(slot, in); })
 }
 
 int rwkvtts_infer(rwkvtts_engine* e, const rwkvtts_input* inputs, int n_inputs, int head_rows,
                   float* logits, int32_t* consumed, int32_t* has_logits) {
   RT_CHECK(e && inputs && consumed && has_logits && n_inputs > 0, RWKVTTS_EINVAL, "infer: bad arguments");
+  LOCK(e);
   GUARD({ return e->eng.infer(inputs, n_inputs, head_rows, logits, consumed, has_logits); })
 }
 
 int rwkvtts_sample(rwkvtts_engine* e, const float* logits, int n_rows, int row_len,
                    const rwkvtts_sample_args* args, rwkvtts_rng* const* rngs, int32_t* out_tokens) {
   RT_CHECK(e && logits && args && out_tokens, RWKVTTS_EINVAL, "sample: bad arguments");
+  LOCK(e);
   GUARD({ return e->eng.sample(logits, n_rows, row_len, args, rngs, out_tokens); })
 }
 
@@ -93,12 +107,14 @@ int rwkvtts_debug_sample(rwkvtts_engine* e, const float* logits, int n_rows, int
                          const rwkvtts_sample_args* args, rwkvtts_rng* const* rngs, int32_t* out_tokens,
                          float* dbg) {
   RT_CHECK(e && logits && args && out_tokens && dbg, RWKVTTS_EINVAL, "debug_sample: bad arguments");
+  LOCK(e);
   GUARD({ return e->eng.sample(logits, n_rows, row_len, args, rngs, out_tokens, dbg); })
 }
 
 int rwkvtts_generate_batch(rwkvtts_engine* e, const rwkvtts_request* reqs, int n,
                            rwkvtts_result* results) {
   RT_CHECK(e && reqs && results && n >= 0, RWKVTTS_EINVAL, "generate_batch: bad arguments");
+  LOCK(e);
   GUARD({
     const int rc = e->eng.generate(reqs, n, results);
     if (rc != RWKVTTS_OK)
@@ -112,6 +128,7 @@ int rwkvtts_generate_batch(rwkvtts_engine* e, const rwkvtts_request* reqs, int n
 
 int rwkvtts_get_stats(rwkvtts_engine* e, rwkvtts_stats* out) {
   RT_CHECK(e && out, RWKVTTS_EINVAL, "null argument");
+  LOCK(e);
   *out = e->eng.stats;
   out->profile_kernel_count = (int32_t)e->eng.prof.size();
   return RWKVTTS_OK;
@@ -119,6 +136,7 @@ int rwkvtts_get_stats(rwkvtts_engine* e, rwkvtts_stats* out) {
 
 int rwkvtts_set_profiling(rwkvtts_engine* e, int on) {
   RT_CHECK(e, RWKVTTS_EINVAL, "null engine");
+  LOCK(e);
   e->eng.profiling = on != 0;
   e->eng.prof.clear();
   return RWKVTTS_OK;
@@ -126,7 +144,9 @@ int rwkvtts_set_profiling(rwkvtts_engine* e, int on) {
 
 int rwkvtts_profile_entry(rwkvtts_engine* e, int idx, char* name, int name_cap, int64_t* launches,
                           double* total_ms) {
-  RT_CHECK(e && idx >= 0 && idx < (int)e->eng.prof.size(), RWKVTTS_EINVAL, "profile index out of range");
+  RT_CHECK(e, RWKVTTS_EINVAL, "null engine");
+  LOCK(e);
+  RT_CHECK(idx >= 0 && idx < (int)e->eng.prof.size(), RWKVTTS_EINVAL, "profile index out of range");
   const ProfEntry& p = e->eng.prof[idx];
   if (name && name_cap > 0) {
     strncpy(name, p.name.c_str(), name_cap - 1);

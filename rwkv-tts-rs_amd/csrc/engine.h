@@ -33,6 +33,24 @@ struct StepPlan {
 
 constexpr int kLookahead = 8;  // decode steps queued per host poll of the control blocks
 
+// One request in flight through Engine::serve. The request's arrays stay valid until finish().
+struct Job {
+  rwkvtts_request req{};
+  rwkvtts_result* res = nullptr;
+  void* user = nullptr;
+};
+
+// Where Engine::serve gets requests and returns results (a fixed list for generate_batch, the
+// manager's per-engine inbox for rwkvtts_manager_*). Called only from the engine's owner thread.
+class JobSource {
+ public:
+  virtual ~JobSource() = default;
+  // Appends up to `max` new jobs to `out`. wait: block until at least one job is available or the
+  // source is closed. Returns false once the source is closed and drained (no job will follow).
+  virtual bool next(int max, bool wait, std::vector<Job*>& out) = 0;
+  virtual void finish(Job* j) = 0;  // j->res is filled
+};
+
 struct ProfEntry {
   std::string name;
   int64_t launches = 0;
@@ -55,6 +73,12 @@ class Engine {
   int sample(const float* logits, int n_rows, int row_len, const rwkvtts_sample_args* args,
              rwkvtts_rng* const* rngs, int32_t* out, float* dbg_host = nullptr);
   int generate(const rwkvtts_request* reqs, int n, rwkvtts_result* res);
+  // Continuous batching until `src` is closed and every admitted job has finished.
+  int serve(JobSource& src);
+  // Checks a request before admission; fills `why` and returns false for a bad one.
+  bool validate(const rwkvtts_request& q, std::string& why) const;
+  int max_slots() const { return S_; }
+  int64_t max_active = 0;  // most slots decoding at once (serve)
 
   rwkvtts_dims dims{};
   rwkvtts_stats stats{};

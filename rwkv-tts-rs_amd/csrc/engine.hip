@@ -89,7 +89,7 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
   splitH_ = pick(C, 512);   // head: 129 col tiles x 2
   RT_CHECK(C % 128 == 0 && F % 128 == 0, RWKVTTS_EUNSUPPORTED, "K dims must be multiples of 128");
   RT_CHECK(splitA_ <= kMaxParts, RWKVTTS_EUNSUPPORTED, "n_embd too large for the WKV partial sum (raise kMaxParts)");
-  state_perm_ = wkv_perm_layout(dims.d_decay, dims.d_aaa, dims.d_mv, dims.d_gate, splitA_, S_);
+  state_perm_ = wkv_perm_layout(dims.d_decay, dims.d_aaa, dims.d_mv, dims.d_gate, splitA_, S_, desc.wkv_variant);
   if (const char* ex = getenv("RWKVTTS_DEBUG_EXP")) dbg_exp_ = atoi(ex);
   if (const char* gp = getenv("RWKVTTS_GEMM_STAMPS")) {
     dbg_gstamp_path_ = gp;
@@ -371,7 +371,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
   if (!inplace) hipLaunchKernelGGL(k_rows_parity, dim3(nb), dim3(256), 0, stream_, d_rows_, slot_par_, R);
   prof_begin(&ev);
   tl_n_ = 0;
-  launch_embed(d_tok_, d_rows_, tok_from_ctrl ? &d_ctrl_[0].next_token : nullptr, (int)(sizeof(SlotCtrl) / 4), emb_,
+  launch_embed(d_tok_, d_rows_, &d_ctrl_[0].next_token, (int)(sizeof(SlotCtrl) / 4), emb_,
                ln0_w_, ln0_b_, h0_, R, C, f16_, stream_, tl_next("embed"), dims.n_vocab);
   prof_end("embed", ev);
   const int64_t RC = (int64_t)Rmax_ * C;
@@ -736,39 +736,90 @@ int Engine::sample(const float* logits, int n_rows, int row_len, const rwkvtts_s
 }
 
 // ------------------------------------------------------------------------------------------
-// Continuous-batching scheduler (DynamicBatchManager::generate_tts_batch semantics)
+// Continuous-batching scheduler (DynamicBatchManager semantics, src/dynamic_batch_manager.rs)
 // ------------------------------------------------------------------------------------------
 namespace {
 struct Active {
-  int req;
+  Job* job;
   int slot;
   std::vector<uint32_t> prompt;
   int prefilled = 0;
   int advances = 0;  // phase-controller invocations so far
+  int total = 0;     // advances after which the request is certainly done (its step limit)
   bool zero_shot = false;
-  bool done = false;
+};
+
+// generate_batch: a fixed list of requests
+class ListSource : public JobSource {
+ public:
+  ListSource(const rwkvtts_request* reqs, int n, rwkvtts_result* res) : jobs_(n) {
+    for (int i = 0; i < n; ++i) {
+      jobs_[i].req = reqs[i];
+      jobs_[i].res = &res[i];
+    }
+  }
+  bool next(int max, bool, std::vector<Job*>& out) override {
+    while (max-- > 0 && pos_ < jobs_.size()) out.push_back(&jobs_[pos_++]);
+    return pos_ < jobs_.size();
+  }
+  void finish(Job*) override {}
+
+ private:
+  std::vector<Job> jobs_;
+  size_t pos_ = 0;
 };
 }  // namespace
 
-// semantic-step limit of a request, as set at admission (c.sem_limit)
+bool Engine::validate(const rwkvtts_request& q, std::string& why) const {
+  auto ids_ok = [&](const int32_t* p, int n, int lo, int hi, const char* what) {
+    if (n < 0 || (n > 0 && !p)) {
+      why = std::string(what) + ": bad array";
+      return false;
+    }
+    for (int i = 0; i < n; ++i)
+      if (p[i] < lo || p[i] >= hi) {
+        why = std::string(what) + ": id " + std::to_string(p[i]) + " out of range";
+        return false;
+      }
+    return true;
+  };
+  const int V = dims.n_vocab;
+  if (!ids_ok(q.text_tokens, q.n_text, 0, V, "text_tokens")) return false;
+  if (!ids_ok(q.property_tokens, q.n_property, 0, V, "property_tokens")) return false;
+  if ((q.ref_global && q.n_ref_global < 0) || (q.ref_semantic && q.n_ref_semantic < 0)) {
+    why = "reference token counts must be >= 0";
+    return false;
+  }
+  if (q.max_tokens < 0 || q.fixed_semantic < 0) {
+    why = "max_tokens / fixed_semantic must be >= 0";
+    return false;
+  }
+  const bool zero_shot = q.ref_global != nullptr && q.ref_semantic != nullptr;
+  if (V <= RWKVTTS_TAG_2 || (!zero_shot && V <= RWKVTTS_GLOBAL_TOKEN_OFFSET + 4095) ||
+      (zero_shot && q.n_ref_global > 0 && V <= RWKVTTS_GLOBAL_TOKEN_OFFSET + 4095)) {
+    why = "model vocabulary too small for the TTS tags / global tokens";
+    return false;
+  }
+  return true;
+}
+
+// Semantic-step limit and RNG seeds of a request, as the reference derives them.
 static int sem_limit_of(const rwkvtts_request& q) {
   const bool zero_shot = q.ref_global != nullptr && q.ref_semantic != nullptr;
-  int limit = q.max_tokens > 0 ? std::min(q.max_tokens, RWKVTTS_SEMANTIC_LIMIT) : RWKVTTS_SEMANTIC_LIMIT;
-  if (q.fixed_semantic > 0) limit = std::min(q.fixed_semantic, RWKVTTS_SEMANTIC_LIMIT);
-  if (zero_shot) return q.fixed_semantic > 0 ? limit : RWKVTTS_SEMANTIC_LIMIT;
-  return limit;
+  if (q.fixed_semantic > 0) return std::min(q.fixed_semantic, RWKVTTS_SEMANTIC_LIMIT);
+  if (zero_shot) return RWKVTTS_SEMANTIC_LIMIT;                  // zero_shot_inference.rs:128-142
+  return std::min(std::max(q.max_tokens, 0), RWKVTTS_SEMANTIC_LIMIT);  // normal_mode_inference.rs:316
 }
 
 int Engine::generate(const rwkvtts_request* reqs, int n, rwkvtts_result* res) {
-  RT_HIP(hipSetDevice(device_));
-  auto t_start = std::chrono::steady_clock::now();
   stats = rwkvtts_stats{};
-  std::deque<int> pending;
-  for (int i = 0; i < n; ++i) {
-    pending.push_back(i);
-    res[i].status = 0;
-    res[i].n_global = res[i].n_semantic = 0;
-  }
+  max_active = 0;
+  ListSource src(reqs, n, res);
+  return serve(src);
+}
+
+int Engine::serve(JobSource& src) {
+  RT_HIP(hipSetDevice(device_));
   std::vector<int> free_slots;
   for (int s = S_ - 1; s >= 0; --s) free_slots.push_back(s);
   std::vector<Active> act;
@@ -776,72 +827,116 @@ int Engine::generate(const rwkvtts_request* reqs, int n, rwkvtts_result* res) {
   hipEvent_t e0, e1;
   RT_HIP(hipEventCreate(&e0));
   RT_HIP(hipEventCreate(&e1));
-  double decode_ms = 0, prefill_ms = 0;
+  bool open = true, decode_plan_valid = false;
+  StepPlan dp;  // the decode plan (all active slots, tokens from the control blocks)
+  std::vector<Job*> fresh;
 
-  while (!pending.empty() || !act.empty()) {
-    // ---- admit new requests into free slots
-    while (!pending.empty() && !free_slots.empty()) {
-      const int ri = pending.front();
-      pending.pop_front();
-      const rwkvtts_request& q = reqs[ri];
-      const int slot = free_slots.back();
-      free_slots.pop_back();
-      Active a;
-      a.req = ri;
-      a.slot = slot;
-      a.zero_shot = q.ref_global != nullptr && q.ref_semantic != nullptr;
-      for (int i = 0; i < q.n_property; ++i) a.prompt.push_back((uint32_t)q.property_tokens[i]);
-      a.prompt.push_back(RWKVTTS_TAG_2);
-      for (int i = 0; i < q.n_text; ++i) a.prompt.push_back((uint32_t)q.text_tokens[i]);
-      a.prompt.push_back(RWKVTTS_TAG_0);
-      SlotCtrl c;
-      memset(&c, 0, sizeof(c));
-      const uint64_t seed = q.has_seed ? q.seed : (((uint64_t)rd() << 32) ^ rd());
-      rwkvtts_rng rg, rs;
-      rwkvtts_rng_seed_from_u64(seed + 1000, &rg);
-      rwkvtts_rng_seed_from_u64(seed + 2000, &rs);
-      memcpy(c.gkey, rg.key, 32);
-      memcpy(c.skey, rs.key, 32);
-      c.top_k_g = q.greedy ? 1 : 20;
-      c.top_k_s = q.greedy ? 1 : 80;
-      int limit = q.max_tokens > 0 ? std::min(q.max_tokens, RWKVTTS_SEMANTIC_LIMIT) : RWKVTTS_SEMANTIC_LIMIT;
-      if (q.fixed_semantic > 0) limit = std::min(q.fixed_semantic, RWKVTTS_SEMANTIC_LIMIT);
-      c.fixed = q.fixed_semantic > 0;
-      if (a.zero_shot) {
-        c.mode = 1;
-        c.phase = kPhSemantic;
-        for (int i = 0; i < q.n_ref_global; ++i) {
-          const int g = std::min(std::max(q.ref_global[i], 0), 4095);
-          a.prompt.push_back((uint32_t)(g + RWKVTTS_GLOBAL_TOKEN_OFFSET));
-          if (i < RWKVTTS_N_GLOBAL) c.global_out[c.n_global++] = g;
-        }
-        a.prompt.push_back(RWKVTTS_TAG_1);
-        const int tlen = q.n_text;
-        const int min_sem = std::min(std::max(tlen / 4, 8), 64);
-        const int est = (int)ceilf((float)tlen * 1.8f);
-        const int upper = (int)floorf((float)RWKVTTS_SEMANTIC_LIMIT * 0.9f);
-        c.hard_min = std::min(upper, std::max(min_sem, est));
-        c.sem_limit = q.fixed_semantic > 0 ? limit : RWKVTTS_SEMANTIC_LIMIT;
-      } else {
-        c.mode = 0;
-        c.phase = kPhGlobal;
-        c.sem_limit = limit;
-      }
-      for (uint32_t t : a.prompt)
-        RT_CHECK(t < (uint32_t)dims.n_vocab, RWKVTTS_EINVAL, "prompt token id >= n_vocab");
-      RT_OK(slot_reset(slot));
-      RT_HIP(hipMemcpyAsync(d_ctrl_ + slot, &c, sizeof(c), hipMemcpyHostToDevice, stream_));
-      act.push_back(std::move(a));
+  auto admit = [&](Job* j) -> int {
+    const rwkvtts_request& q = j->req;
+    rwkvtts_result& r = *j->res;
+    r.status = 0;
+    r.n_global = r.n_semantic = 0;
+    std::string why;
+    if (!validate(q, why)) {  // dynamic_batch_manager.rs:466-469: this request fails alone
+      r.status = RWKVTTS_EINVAL;
+      set_error("request rejected: " + why);
+      src.finish(j);
+      return RWKVTTS_OK;
     }
-    // ---- prefill steps for slots with pending prompt tokens
+    const int slot = free_slots.back();
+    free_slots.pop_back();
+    Active a;
+    a.job = j;
+    a.slot = slot;
+    a.zero_shot = q.ref_global != nullptr && q.ref_semantic != nullptr;
+    for (int i = 0; i < q.n_property; ++i) a.prompt.push_back((uint32_t)q.property_tokens[i]);
+    a.prompt.push_back(RWKVTTS_TAG_2);
+    for (int i = 0; i < q.n_text; ++i) a.prompt.push_back((uint32_t)q.text_tokens[i]);
+    a.prompt.push_back(RWKVTTS_TAG_0);
+    SlotCtrl c;
+    memset(&c, 0, sizeof(c));
+    // RNG streams: normal_mode_inference.rs:138-174, zero_shot_inference.rs:204-216,
+    // dynamic_batch_manager.rs:491-499 (no seed -> from_entropy)
+    const uint64_t seed = q.has_seed ? q.seed : (((uint64_t)rd() << 32) ^ rd());
+    const bool indep = q.layered_set ? q.use_independent_seeds != 0 : true;
+    const uint64_t goff = q.layered_set ? q.global_seed_offset : 1000, soff = q.layered_set ? q.semantic_seed_offset : 2000;
+    uint64_t gseed = indep ? seed + goff : seed + 100, sseed = indep ? seed + soff : seed + 200;
+    if (a.zero_shot && !indep) sseed = 0;  // StdRng::seed_from_u64(0) handed to the zero-shot path
+    rwkvtts_rng rg, rs;
+    rwkvtts_rng_seed_from_u64(gseed, &rg);
+    rwkvtts_rng_seed_from_u64(sseed, &rs);
+    memcpy(c.gkey, rg.key, 32);
+    memcpy(c.skey, rs.key, 32);
+    c.top_k_g = q.greedy ? 1 : 20;
+    c.top_k_s = q.greedy ? 1 : 80;
+    c.fixed = q.fixed_semantic > 0;
+    c.sem_limit = sem_limit_of(q);
+    if (a.zero_shot) {
+      c.mode = 1;
+      c.phase = kPhSemantic;
+      for (int i = 0; i < q.n_ref_global; ++i) {
+        const int g = std::min(std::max(q.ref_global[i], 0), 4095);
+        a.prompt.push_back((uint32_t)(g + RWKVTTS_GLOBAL_TOKEN_OFFSET));
+        if (i < RWKVTTS_N_GLOBAL) c.global_out[c.n_global++] = g;
+      }
+      a.prompt.push_back(RWKVTTS_TAG_1);
+      const int tlen = q.n_text;
+      const int min_sem = std::min(std::max(tlen / 4, 8), 64);
+      const int est = (int)ceilf((float)tlen * 1.8f);
+      const int upper = (int)floorf((float)RWKVTTS_SEMANTIC_LIMIT * 0.9f);
+      c.hard_min = std::min(upper, std::max(min_sem, est));
+      a.total = std::max(c.sem_limit, 1);
+    } else {
+      c.mode = 0;
+      c.phase = kPhGlobal;
+      a.total = RWKVTTS_N_GLOBAL + 1 + c.sem_limit;
+    }
+    RT_OK(slot_reset(slot));
+    RT_HIP(hipMemcpyAsync(d_ctrl_ + slot, &c, sizeof(c), hipMemcpyHostToDevice, stream_));
+    act.push_back(std::move(a));
+    decode_plan_valid = false;
+    return RWKVTTS_OK;
+  };
+
+  int rc = RWKVTTS_OK;
+  while (true) {
+    // ---- admission: new requests take free slots between forward steps
+    if (open && !free_slots.empty()) {
+      fresh.clear();
+      open = src.next((int)free_slots.size(), act.empty(), fresh);
+      for (Job* j : fresh)
+        if ((rc = admit(j)) != RWKVTTS_OK) break;
+      if (rc != RWKVTTS_OK) break;
+    }
+    if (act.empty()) {
+      if (!open) break;
+      continue;
+    }
+    std::sort(act.begin(), act.end(), [](const Active& x, const Active& y) { return x.slot < y.slot; });
     bool any_prefill = false;
     for (auto& a : act) any_prefill |= a.prefilled < (int)a.prompt.size();
+    int K = 1;
+    bool all_global = true;
+    RT_HIP(hipEventRecord(e0, stream_));
     if (any_prefill) {
+      // ---- mixed step: every decoding slot's row (token from its control block) plus prompt
+      // rows of the admitted slots, up to token_chunk_size rows; the decoding slots never stall
       StepPlan p;
       p.advance = true;
-      p.head_rows = 8193;
       int budget = chunk_;
-      bool all_global = true;
+      for (auto& a : act) {
+        if (a.prefilled < (int)a.prompt.size()) continue;
+        const int r = (int)p.rows.size();
+        p.rows.push_back(make_int4(a.slot, kRowFirst | kRowLast | kRowCtrl, -1, 0));
+        p.tok.push_back(0);
+        p.segs.push_back(make_int4(a.slot, r, 1, 0));
+        p.lg_rows.push_back(r);
+        p.lg_slot.push_back(a.slot);
+        all_global &= !a.zero_shot && a.advances <= RWKVTTS_N_GLOBAL;
+        a.advances++;
+        --budget;
+      }
+      budget = std::max(budget, 1);
       for (auto& a : act) {
         const int left = (int)a.prompt.size() - a.prefilled;
         if (left <= 0 || budget <= 0) continue;
@@ -858,95 +953,79 @@ int Engine::generate(const rwkvtts_request* reqs, int n, rwkvtts_result* res) {
         if (a.prefilled == (int)a.prompt.size()) {
           p.lg_rows.push_back(r0 + take - 1);
           p.lg_slot.push_back(a.slot);
-          a.advances++;
           all_global &= !a.zero_shot;
+          a.advances++;
         }
       }
-      if (all_global) p.head_rows = std::min(4096, dims.n_vocab);
-      p.head_rows = std::min(p.head_rows, dims.n_vocab);
-      RT_HIP(hipEventRecord(e0, stream_));
-      RT_OK(run_step(p, true));
-      RT_HIP(hipEventRecord(e1, stream_));
-      RT_HIP(hipEventSynchronize(e1));
-      float ms = 0;
-      hipEventElapsedTime(&ms, e0, e1);
-      prefill_ms += ms;
+      p.head_rows = std::min(all_global ? 4096 : 8193, dims.n_vocab);
+      if ((rc = run_step(p, true)) != RWKVTTS_OK) break;
+      decode_plan_valid = false;
       stats.prefill_steps++;
-      RT_OK(flush_prof());
-      continue;
-    }
-    // ---- decode steps over all active slots until one finishes. Rows in slot order, so with
-    // every slot active row r is slot r (k_wkv2 speculates on that to start its state loads early).
-    std::sort(act.begin(), act.end(), [](const Active& x, const Active& y) { return x.slot < y.slot; });
-    StepPlan p;
-    p.tok_from_ctrl = true;
-    p.advance = true;
-    for (auto& a : act) {
-      const int r = (int)p.rows.size();
-      p.rows.push_back(make_int4(a.slot, kRowFirst | kRowLast, -1, 0));
-      p.segs.push_back(make_int4(a.slot, r, 1, 0));
-      p.lg_rows.push_back(r);
-      p.lg_slot.push_back(a.slot);
-    }
-    RT_OK(upload_plan(p));
-    const int R = (int)p.rows.size();
-    bool finished = false;
-    while (!finished) {
-      // Up to kLookahead decode steps are queued back to back before the host reads the control
-      // blocks: no slot can pass its step limit inside the window (EOS may end a request
-      // earlier: its slot then idles through the rest of the window, k_advance skips it).
-      int K = (profiling || d_tl_) ? 1 : kLookahead;
-      if (d_tl_) {
-        RT_HIP(hipMemsetAsync(d_tl_, 0, (size_t)kTlStride * kTlMax * 8, stream_));
+    } else {
+      // ---- decode window: up to kLookahead steps queued back to back before the host reads
+      // the control blocks; no slot can pass its step limit inside the window (EOS may end a
+      // request earlier: its slot then idles through the rest of the window, k_advance skips it)
+      if (!decode_plan_valid) {
+        dp = StepPlan();
+        dp.tok_from_ctrl = true;
+        dp.advance = true;
+        for (auto& a : act) {
+          const int r = (int)dp.rows.size();
+          dp.rows.push_back(make_int4(a.slot, kRowFirst | kRowLast | kRowCtrl, -1, 0));
+          dp.segs.push_back(make_int4(a.slot, r, 1, 0));
+          dp.lg_rows.push_back(r);
+          dp.lg_slot.push_back(a.slot);
+        }
+        if ((rc = upload_plan(dp)) != RWKVTTS_OK) break;
+        decode_plan_valid = true;
       }
-      for (auto& a : act) {
-        const Active& aa = a;
-        const int total = aa.zero_shot ? sem_limit_of(reqs[aa.req]) : RWKVTTS_N_GLOBAL + 1 + sem_limit_of(reqs[aa.req]);
-        K = std::min(K, std::max(1, total - aa.advances));
-      }
-      RT_HIP(hipEventRecord(e0, stream_));
-      for (int k = 0; k < K; ++k) {
+      K = (profiling || d_tl_) ? 1 : kLookahead;
+      for (auto& a : act) K = std::min(K, std::max(1, a.total - a.advances));
+      if (d_tl_) RT_HIP(hipMemsetAsync(d_tl_, 0, (size_t)kTlStride * kTlMax * 8, stream_));
+      for (int k = 0; k < K && rc == RWKVTTS_OK; ++k) {
         // head rows: 4096 while every slot samples global tokens (or feeds g31), else 8193
-        bool all_global = true;
+        all_global = true;
         for (auto& a : act) all_global &= !a.zero_shot && a.advances <= RWKVTTS_N_GLOBAL;
-        p.head_rows = std::min(all_global ? 4096 : 8193, dims.n_vocab);
-        RT_OK(run_step(p, false));
+        dp.head_rows = std::min(all_global ? 4096 : 8193, dims.n_vocab);
+        rc = run_step(dp, false);
         for (auto& a : act) a.advances++;
       }
-      RT_HIP(hipMemcpyAsync(h_ctrl_, d_ctrl_, sizeof(SlotCtrl) * S_, hipMemcpyDeviceToHost, stream_));
-      RT_HIP(hipEventRecord(e1, stream_));
-      RT_HIP(hipEventSynchronize(e1));
-      float ms = 0;
-      hipEventElapsedTime(&ms, e0, e1);
-      decode_ms += ms;
+      if (rc != RWKVTTS_OK) break;
       stats.steps += K;
-      stats.decode_rows += (int64_t)R * K;
-      RT_OK(flush_prof());
-      if (d_tl_ && stats.steps > 40) {  // semantic-phase steps only
-        std::vector<unsigned long long> h((size_t)kTlStride * kTlMax);
-        RT_HIP(hipMemcpy(h.data(), d_tl_, h.size() * 8, hipMemcpyDeviceToHost));
-        const int n = (int)tl_names_.size();
-        tl_start_.resize(n, 0.0);
-        tl_dur_.resize(n, 0.0);
-        for (int i = 0; i < n; ++i) {
-          const unsigned long long* q = h.data() + (size_t)kTlStride * i;
-          unsigned long long e = 0;
-          for (int j = 2; j < kTlStride; ++j) e = std::max(e, q[j]);
-          tl_start_[i] += (double)(q[0] - h[0]) * 0.01;  // us
-          tl_dur_[i] += (double)(e - q[0]) * 0.01;
-        }
-        tl_steps_++;
+      stats.decode_rows += (int64_t)dp.rows.size() * K;
+      max_active = std::max<int64_t>(max_active, (int64_t)dp.rows.size());
+    }
+    RT_HIP(hipMemcpyAsync(h_ctrl_, d_ctrl_, sizeof(SlotCtrl) * S_, hipMemcpyDeviceToHost, stream_));
+    RT_HIP(hipEventRecord(e1, stream_));
+    RT_HIP(hipEventSynchronize(e1));
+    float ms = 0;
+    hipEventElapsedTime(&ms, e0, e1);
+    (any_prefill ? stats.prefill_ms : stats.decode_ms) += ms;
+    if ((rc = flush_prof()) != RWKVTTS_OK) break;
+    if (d_tl_ && !any_prefill && stats.steps > 40) {  // semantic-phase steps only
+      std::vector<unsigned long long> h((size_t)kTlStride * kTlMax);
+      RT_HIP(hipMemcpy(h.data(), d_tl_, h.size() * 8, hipMemcpyDeviceToHost));
+      const int n = (int)tl_names_.size();
+      tl_start_.resize(n, 0.0);
+      tl_dur_.resize(n, 0.0);
+      for (int i = 0; i < n; ++i) {
+        const unsigned long long* q = h.data() + (size_t)kTlStride * i;
+        unsigned long long e = 0;
+        for (int j = 2; j < kTlStride; ++j) e = std::max(e, q[j]);
+        tl_start_[i] += (double)(q[0] - h[0]) * 0.01;  // us
+        tl_dur_[i] += (double)(e - q[0]) * 0.01;
       }
-      for (auto& a : act) {
-        if (h_ctrl_[a.slot].phase == kPhDone) finished = true;
-      }
+      tl_steps_++;
     }
     // ---- retire finished slots
     for (size_t i = 0; i < act.size();) {
       Active& a = act[i];
       const SlotCtrl& c = h_ctrl_[a.slot];
-      if (c.phase != kPhDone) { ++i; continue; }
-      rwkvtts_result& r = res[a.req];
+      if (a.prefilled < (int)a.prompt.size() || c.phase != kPhDone) {
+        ++i;
+        continue;
+      }
+      rwkvtts_result& r = *a.job->res;
       r.status = 0;
       r.n_global = c.n_global;
       memcpy(r.global_tokens, c.global_out, sizeof(int32_t) * RWKVTTS_N_GLOBAL);
@@ -954,15 +1033,22 @@ int Engine::generate(const rwkvtts_request* reqs, int n, rwkvtts_result* res) {
       if (r.semantic_tokens && c.n_sem > 0)
         RT_HIP(hipMemcpy(r.semantic_tokens, d_sem_ + (int64_t)a.slot * RWKVTTS_SEMANTIC_LIMIT,
                          sizeof(int32_t) * c.n_sem, hipMemcpyDeviceToHost));
+      src.finish(a.job);
       free_slots.push_back(a.slot);
       act.erase(act.begin() + i);
+      decode_plan_valid = false;
     }
   }
   hipEventDestroy(e0);
   hipEventDestroy(e1);
-  stats.decode_ms = decode_ms;
-  stats.prefill_ms = prefill_ms;
-  (void)t_start;
+  if (rc != RWKVTTS_OK) {  // engine failure: every job still in flight fails with it
+    for (auto& a : act) {
+      a.job->res->status = rc;
+      a.job->res->n_global = a.job->res->n_semantic = 0;
+      src.finish(a.job);
+    }
+    return rc;
+  }
   return dump_stamps();
 }
 

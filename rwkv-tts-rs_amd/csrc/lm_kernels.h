@@ -9,6 +9,7 @@ constexpr int kMaxLoraTotal = 512;   // Dw + Da + Dv + Dg
 constexpr int kMaxParts = 8;         // split-K slabs a WKV row sums (r, k, v, LoRA hidden)
 constexpr int kRowFirst = 1;         // row flags
 constexpr int kRowLast = 2;
+constexpr int kRowCtrl = 4;          // the row's token is its slot's SlotCtrl::next_token (decode)
 constexpr int kXPlanes = 0;  // gemm X: bf16 hi/lo planes
 constexpr int kXRelu2 = 1;   // gemm X: relu(sum of f32 partial slabs)^2
 
@@ -105,7 +106,7 @@ struct WkvArgs {
   unsigned long long* tl;  // debug timeline slot (null in production)
 };
 
-// tokens: per-row ids, or (ctrl_tok != null, decode) row r's id = ctrl_tok[rows[r].x * ctrl_stride]
+// tokens: per-row ids; a row flagged kRowCtrl (decode) reads ctrl_tok[rows[r].x * ctrl_stride]
 void launch_embed(const uint32_t* tokens, const int4* rows, const int* ctrl_tok, int ctrl_stride,
                   const bf16_t* emb, const float* w, const float* b, float* h, int R, int C, int f16, hipStream_t st,
                   unsigned long long* tl, int n_vocab);
@@ -118,8 +119,9 @@ int launch_gemm(const GemmArgs& a, hipStream_t st);
 bool gemm_tile_table(GemmArgs& a, int64_t x_mix_stride);
 int launch_wkv(const WkvArgs& a, int n_seg, int H, hipStream_t st);
 // Which coalesced WKV state layout launch_wkv expects for these LoRA ranks / slab count: 0 none
-// (row-major S[i][j]), 1 k_wkv4 (two waves per block, the default), 2 k_wkv6 (four waves).
-int wkv_perm_layout(int Dw, int Da, int Dv, int Dg, int n_part, int max_slots);
+// (row-major S[i][j], generic kernels), 1 k_wkv4 (two waves per block), 2 k_wkv6 (four waves).
+// variant: rwkvtts_engine_desc.wkv_variant (0 auto by slot count).
+int wkv_perm_layout(int Dw, int Da, int Dv, int Dg, int n_part, int max_slots, int variant);
 // Repack a GEMM matrix W [N][K] (K % 32 == 0) into MFMA fragment blocks (k_gemm's layout):
 // out holds ceil(N/16)*16*K elements.
 void launch_pack_frag(const bf16_t* W, int N, int K, bf16_t* out, hipStream_t st);

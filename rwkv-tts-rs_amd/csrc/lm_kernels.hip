@@ -69,7 +69,8 @@ __global__ __launch_bounds__(256) void k_embed(const uint32_t* tokens, const int
   __shared__ float red[4];
   tl_begin(tl);
   const int r = blockIdx.x;
-  uint32_t tok = ctrl_tok ? (uint32_t)ctrl_tok[(int64_t)rows[r].x * ctrl_stride] : tokens[r];
+  const int4 info = rows[r];
+  uint32_t tok = (info.y & kRowCtrl) ? (uint32_t)ctrl_tok[(int64_t)info.x * ctrl_stride] : tokens[r];
   if (tok >= (uint32_t)n_vocab) tok = 0;  // ids are validated on the host; never index past the table
   const bf16_t* e = emb + (int64_t)tok * C;
   float v[kMaxPerThread];
@@ -885,8 +886,7 @@ int launch_ln_mix(const LnMixArgs& a, int n_out_rows, hipStream_t st) {
   LnMixArgs b = a;
   b.n_rows = n_out_rows;
   const dim3 grid(n_out_rows);
-  static const bool fast = !getenv("RWKVTTS_LN_OLD");
-  if (fast && a.C == 1024 && (a.shift ? (a.n_mix == 6 || a.n_mix == 1) : true) &&
+  if (a.C == 1024 && (a.shift ? (a.n_mix == 6 || a.n_mix == 1) : true) &&
       (a.n_part == 0 || a.n_part == 8 || a.n_part == 16)) {
 #define LN_CASE(F, MO, NM)                                                                                  \
   switch (a.n_part) {                                                                                      \
@@ -918,8 +918,9 @@ int launch_ln_mix(const LnMixArgs& a, int n_out_rows, hipStream_t st) {
 template <int MT, int KSTEPS>
 static void launch_gemm_t(const GemmArgs& a, dim3 grid, hipStream_t st) {
   const size_t lds = (size_t)MT * 16 * (KSTEPS * 32 + 8) * 2 * 2;
-  static const bool v2 = !getenv("RWKVTTS_GEMM_OLD");
-  if (v2 && (a.xmode == kXPlanes || a.x_nsplit == 4 || a.x_nsplit == 2) && a.stamps == nullptr && a.exp == 0) {
+  // k_gemm2 (fragment-packed weights, per-tile descriptors) covers the 0.4B shapes; k_gemm is the
+  // generic fallback (other slab counts) and the debug-stamp build
+  if ((a.xmode == kXPlanes || a.x_nsplit == 4 || a.x_nsplit == 2) && a.stamps == nullptr && a.exp == 0) {
     const int ms = a.nseg > 1 ? (a.n_tinfo > 0 ? 2 : 1) : 0;
 #define G2(F, XM, NX_, MS_) RT_LAUNCH((k_gemm2<MT, KSTEPS, XM, F, NX_, MS_>), grid, dim3(256), lds, st, a)
     if (a.f16) {
@@ -1646,32 +1647,31 @@ __global__ __launch_bounds__(256) void k_wkv6(WkvArgs a) {
   tl_end(a.tl);
 }
 
-int wkv_perm_layout(int Dw, int Da, int Dv, int Dg, int n_part, int max_slots) {
-  if (!(Dw == 64 && Da == 64 && Dv == 32 && Dg == 128 && n_part == 4 && !getenv("RWKVTTS_WKV_OLD"))) return 0;
-  if (const char* e = getenv("RWKVTTS_WKV_LAYOUT")) return atoi(e) == 2 ? 2 : 1;
-  // measured per decode step: k_wkv6 1 % faster at one slot (16 workgroups on an idle chip),
-  // k_wkv4 1 % faster at 32 slots (512 workgroups)
+int wkv_perm_layout(int Dw, int Da, int Dv, int Dg, int n_part, int max_slots, int variant) {
+  if (!(Dw == 64 && Da == 64 && Dv == 32 && Dg == 128 && n_part == 4)) return 0;
+  if (const char* e = getenv("RWKVTTS_WKV_LAYOUT")) variant = atoi(e);  // A/B timing override
+  if (variant == 1 || variant == 2) return variant;
+  // auto, measured per decode step: k_wkv6 1 % faster at one slot (16 workgroups on an idle
+  // chip), k_wkv4 1 % faster at 32 slots (512 workgroups)
   return max_slots <= 8 ? 2 : 1;
 }
 int launch_wkv(const WkvArgs& a, int n_seg, int H, hipStream_t st) {
   const dim3 grid(n_seg, H);
-  if (a.Dw == 64 && a.Da == 64 && a.Dv == 32 && a.Dg == 128 && a.n_part <= 4 && !getenv("RWKVTTS_WKV_OLD")) {
+  if (a.Dw == 64 && a.Da == 64 && a.Dv == 32 && a.Dg == 128 && a.n_part == 4 && (a.perm == 1 || a.perm == 2)) {
     if (a.perm == 2) {
       if (a.f16) RT_LAUNCH((k_wkv6<true>), grid, dim3(256), 0, st, a);
       else RT_LAUNCH((k_wkv6<false>), grid, dim3(256), 0, st, a);
-    } else if (a.perm == 1) {
+    } else {
       if (a.f16) RT_LAUNCH((k_wkv4<true>), grid, dim3(128), 0, st, a);
       else RT_LAUNCH((k_wkv4<false>), grid, dim3(128), 0, st, a);
-    } else {
-      RT_LAUNCH((k_wkv2<64, 64, 32, 128, 4>), grid, dim3(128), 0, st, a);
     }
     return n_seg * H;
   }
-  if (a.Dw == 16 && a.Da == 16 && a.Dv == 16 && a.Dg == 32 && a.n_part <= 1 && !getenv("RWKVTTS_WKV_OLD")) {
+  if (a.Dw == 16 && a.Da == 16 && a.Dv == 16 && a.Dg == 32 && a.n_part <= 1) {
     RT_LAUNCH((k_wkv2<16, 16, 16, 32, 1>), grid, dim3(128), 0, st, a);
     return n_seg * H;
   }
-  if (a.Dw == 32 && a.Da == 32 && a.Dv == 16 && a.Dg == 64 && a.n_part <= 1 && !getenv("RWKVTTS_WKV_OLD")) {
+  if (a.Dw == 32 && a.Da == 32 && a.Dv == 16 && a.Dg == 64 && a.n_part <= 1) {
     RT_LAUNCH((k_wkv2<32, 32, 16, 64, 1>), grid, dim3(128), 0, st, a);
     return n_seg * H;
   }

@@ -1,0 +1,415 @@
+// manager.cpp -- rwkvtts_manager_*: the DynamicBatchManager of the reference
+// (src/dynamic_batch_manager.rs:22-405, src/batch_types.rs:67-97) as native host code.
+//
+// Reference structure: generate_tts sends the request over a flume channel and waits on a
+// oneshot (:90-121); one enqueue_worker collects requests into batches (:185-264) and hands each
+// batch to whichever of max_concurrent_batches infer workers is free (:267-405), which then runs
+// the batch's requests one after another on state slot 0.
+//
+// Here: submit() copies the request and queues it; the collector thread forms batches with the
+// same rules (first request, then try_recv up to max_batch_size with at most 50 quick pulls; go
+// once more than one request is pending or a lone request has waited 10 ms, or when
+// collect_timeout_ms passes with requests pending) and routes every request of a batch to the
+// least-loaded engine (fewest requests queued or decoding; ties -> lowest index). Each engine
+// has one owner thread running Engine::serve, which admits queued requests into free state slots
+// between forward steps (continuous batching). One engine per GPU = request-level data
+// parallelism over the node; no collective is needed on this path.
+#include <string.h>
+
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <thread>
+
+#include "engine.h"
+
+namespace rwkvtts {
+
+namespace {
+
+using Clock = std::chrono::steady_clock;
+
+struct MJob : Job {
+  uint64_t ticket = 0;
+  std::vector<int32_t> text, props, ref_g, ref_s;  // owned copies of the request arrays
+  std::vector<int32_t> sem;                        // semantic token buffer
+  rwkvtts_result out{};
+  bool done = false;
+  int engine = -1;
+};
+
+class Manager;
+
+class Worker : public JobSource {
+ public:
+  Worker(Manager* m, int idx) : m_(m), idx_(idx) {}
+  bool next(int max, bool wait, std::vector<Job*>& out) override {
+    std::unique_lock<std::mutex> lk(mu_);
+    if (wait) cv_.wait(lk, [&] { return !inbox_.empty() || closing_; });
+    while (max > 0 && !inbox_.empty()) {
+      out.push_back(inbox_.front());
+      inbox_.pop_front();
+      --max;
+    }
+    return !(closing_ && inbox_.empty());
+  }
+  void finish(Job* j) override;
+  void push(MJob* j) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      inbox_.push_back(j);
+    }
+    cv_.notify_one();
+  }
+  void close() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      closing_ = true;
+    }
+    cv_.notify_one();
+  }
+  void run(rwkvtts_engine_desc desc, const void* w, size_t bytes);
+
+  Engine eng;
+  std::thread th;
+  std::atomic<int> load{0};  // requests routed here and not finished
+  std::atomic<bool> dead{false};
+  std::atomic<int64_t> served{0}, max_active{0}, steps{0};
+  int init_rc = 1;  // 1 = initialising
+  std::string init_err;
+
+ private:
+  Manager* m_;
+  int idx_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<MJob*> inbox_;
+  bool closing_ = false;
+};
+
+class Manager {
+ public:
+  int create(const rwkvtts_manager_desc& d, const void* w, size_t bytes) {
+    desc_ = d;
+    RT_CHECK(d.n_engines >= 1 && d.n_engines <= RWKVTTS_MAX_ENGINES, RWKVTTS_EINVAL, "manager: 1..16 engines");
+    for (int i = 0; i < d.n_engines; ++i) workers_.emplace_back(new Worker(this, i));
+    for (int i = 0; i < d.n_engines; ++i) {
+      rwkvtts_engine_desc ed = d.engine;
+      ed.device = d.devices[i];
+      Worker* wk = workers_[i].get();
+      wk->th = std::thread([wk, ed, w, bytes] { wk->run(ed, w, bytes); });
+    }
+    // engines upload their weights in parallel; create() returns once all are ready
+    int rc = RWKVTTS_OK;
+    {
+      std::unique_lock<std::mutex> lk(init_mu_);
+      init_cv_.wait(lk, [&] {
+        for (auto& wk : workers_)
+          if (wk->init_rc == 1) return false;
+        return true;
+      });
+      for (auto& wk : workers_)
+        if (wk->init_rc != RWKVTTS_OK && rc == RWKVTTS_OK) {
+          rc = wk->init_rc;
+          set_error("manager: engine init failed: " + wk->init_err);
+        }
+    }
+    collector_ = std::thread([this] { collect_loop(); });
+    return rc;
+  }
+
+  void shutdown() {
+    {
+      std::lock_guard<std::mutex> lk(q_mu_);
+      closing_ = true;
+    }
+    q_cv_.notify_all();
+    if (collector_.joinable()) collector_.join();
+    for (auto& wk : workers_) wk->close();
+    for (auto& wk : workers_)
+      if (wk->th.joinable()) wk->th.join();
+    std::lock_guard<std::mutex> lk(t_mu_);
+    for (auto& kv : jobs_) delete kv.second;
+    jobs_.clear();
+  }
+
+  int submit(const rwkvtts_request& q, uint64_t* ticket) {
+    MJob* j = new MJob();
+    auto copy = [](const int32_t* p, int n, std::vector<int32_t>& v) {
+      if (p && n > 0) v.assign(p, p + n);
+    };
+    copy(q.text_tokens, q.n_text, j->text);
+    copy(q.property_tokens, q.n_property, j->props);
+    copy(q.ref_global, q.n_ref_global, j->ref_g);
+    copy(q.ref_semantic, q.n_ref_semantic, j->ref_s);
+    j->req = q;
+    j->req.text_tokens = j->text.empty() ? nullptr : j->text.data();
+    j->req.property_tokens = j->props.empty() ? nullptr : j->props.data();
+    // presence (Some / None) of the reference token sets is part of the request's meaning
+    static const int32_t kEmpty[1] = {0};
+    j->req.ref_global = q.ref_global ? (j->ref_g.empty() ? kEmpty : j->ref_g.data()) : nullptr;
+    j->req.ref_semantic = q.ref_semantic ? (j->ref_s.empty() ? kEmpty : j->ref_s.data()) : nullptr;
+    j->sem.assign(RWKVTTS_SEMANTIC_LIMIT, 0);
+    j->out.semantic_tokens = j->sem.data();
+    j->res = &j->out;
+    {
+      std::lock_guard<std::mutex> lk(t_mu_);
+      j->ticket = ++next_ticket_;
+      jobs_[j->ticket] = j;
+      submitted_++;
+    }
+    *ticket = j->ticket;
+    {
+      std::lock_guard<std::mutex> lk(q_mu_);
+      if (closing_) {
+        fail(j, RWKVTTS_ECLOSED);
+        return RWKVTTS_OK;
+      }
+      queue_.push_back(j);
+    }
+    q_cv_.notify_one();
+    return RWKVTTS_OK;
+  }
+
+  int wait(uint64_t ticket, int timeout_ms, rwkvtts_result* out) {
+    std::unique_lock<std::mutex> lk(t_mu_);
+    auto it = jobs_.find(ticket);
+    RT_CHECK(it != jobs_.end(), RWKVTTS_EINVAL, "manager_wait: unknown ticket");
+    MJob* j = it->second;
+    auto ready = [&] { return j->done; };
+    if (timeout_ms < 0) {
+      t_cv_.wait(lk, ready);
+    } else if (!t_cv_.wait_for(lk, std::chrono::milliseconds(timeout_ms), ready)) {
+      return RWKVTTS_EBUSY;
+    }
+    int32_t* sem = out->semantic_tokens;
+    *out = j->out;
+    out->semantic_tokens = sem;
+    if (sem && j->out.n_semantic > 0) memcpy(sem, j->sem.data(), sizeof(int32_t) * j->out.n_semantic);
+    jobs_.erase(it);
+    delete j;
+    return RWKVTTS_OK;
+  }
+
+  void complete(MJob* j, int engine) {
+    {
+      std::lock_guard<std::mutex> lk(t_mu_);
+      j->done = true;
+      j->engine = engine;
+      completed_++;
+    }
+    t_cv_.notify_all();
+  }
+
+  void stats(rwkvtts_manager_stats* s) {
+    memset(s, 0, sizeof(*s));
+    {
+      std::lock_guard<std::mutex> lk(t_mu_);
+      s->submitted = submitted_;
+      s->completed = completed_;
+    }
+    s->batches = batches_.load();
+    for (size_t i = 0; i < workers_.size(); ++i) {
+      s->served[i] = workers_[i]->served.load();
+      s->max_active[i] = workers_[i]->max_active.load();
+      s->steps[i] = workers_[i]->steps.load();
+    }
+  }
+
+  void init_done() { init_cv_.notify_all(); }
+  std::mutex init_mu_;
+
+ private:
+  void fail(MJob* j, int code) {
+    j->out.status = code;
+    j->out.n_global = j->out.n_semantic = 0;
+    complete(j, -1);
+  }
+
+  // enqueue_worker (dynamic_batch_manager.rs:185-264)
+  void collect_loop() {
+    const int max_batch = std::max(1, desc_.max_batch_size);
+    const auto tmo = std::chrono::milliseconds(std::max(0, desc_.collect_timeout_ms));
+    std::vector<MJob*> pending;
+    std::unique_lock<std::mutex> lk(q_mu_);
+    while (true) {
+      const auto collect_start = Clock::now();
+      pending.clear();
+      while (true) {
+        const bool got = q_cv_.wait_for(lk, tmo, [&] { return !queue_.empty() || closing_; }) && !queue_.empty();
+        if (got) {
+          pending.push_back(queue_.front());
+          queue_.pop_front();
+          int quick = 0;  // take whatever is immediately available
+          while ((int)pending.size() < max_batch && quick < 50 && !queue_.empty()) {
+            pending.push_back(queue_.front());
+            queue_.pop_front();
+            ++quick;
+          }
+          if (pending.size() > 1) break;
+          if (Clock::now() - collect_start >= std::chrono::milliseconds(10)) break;
+        } else if (!pending.empty() || closing_) {
+          break;
+        }
+      }
+      if (pending.empty() && closing_ && queue_.empty()) return;
+      lk.unlock();
+      route(pending);
+      lk.lock();
+    }
+  }
+
+  void route(const std::vector<MJob*>& batch) {
+    if (batch.empty()) return;
+    batches_++;
+    for (MJob* j : batch) {
+      Worker* best = nullptr;
+      for (auto& wk : workers_) {
+        if (wk->dead || wk->init_rc != RWKVTTS_OK) continue;
+        if (!best || wk->load.load() < best->load.load()) best = wk.get();
+      }
+      if (!best) {
+        fail(j, RWKVTTS_EHIP);
+        continue;
+      }
+      best->load++;
+      best->push(j);
+    }
+  }
+
+  rwkvtts_manager_desc desc_{};
+  std::vector<std::unique_ptr<Worker>> workers_;
+  std::thread collector_;
+  std::condition_variable init_cv_;
+  // request queue (flume channel of the reference)
+  std::mutex q_mu_;
+  std::condition_variable q_cv_;
+  std::deque<MJob*> queue_;
+  bool closing_ = false;
+  // tickets (oneshot channels of the reference)
+  std::mutex t_mu_;
+  std::condition_variable t_cv_;
+  std::map<uint64_t, MJob*> jobs_;
+  uint64_t next_ticket_ = 0;
+  int64_t submitted_ = 0, completed_ = 0;
+  std::atomic<int64_t> batches_{0};
+};
+
+void Worker::finish(Job* j) {
+  served++;
+  load--;
+  m_->complete(static_cast<MJob*>(j), idx_);
+}
+
+void Worker::run(rwkvtts_engine_desc desc, const void* w, size_t bytes) {
+  int rc = eng.init(desc, w, bytes, 0);
+  {
+    std::lock_guard<std::mutex> lk(m_->init_mu_);
+    init_rc = rc;
+    if (rc != RWKVTTS_OK) init_err = "device " + std::to_string(desc.device);
+  }
+  m_->init_done();
+  if (rc != RWKVTTS_OK) return;
+  while (true) {
+    rc = eng.serve(*this);
+    steps = eng.stats.steps + eng.stats.prefill_steps;
+    max_active = eng.max_active;
+    if (rc != RWKVTTS_OK) {
+      dead = true;  // an engine failure fails its in-flight jobs (serve) and everything queued here
+      std::vector<Job*> rest;
+      bool open = true;
+      while (open) {
+        rest.clear();
+        open = next(1 << 30, true, rest);
+        for (Job* j : rest) {
+          j->res->status = rc;
+          j->res->n_global = j->res->n_semantic = 0;
+          finish(j);
+        }
+      }
+      return;
+    }
+    std::lock_guard<std::mutex> lk(mu_);
+    if (closing_ && inbox_.empty()) return;
+  }
+}
+
+}  // namespace
+}  // namespace rwkvtts
+
+using namespace rwkvtts;
+
+struct rwkvtts_manager {
+  Manager m;
+};
+
+extern "C" {
+
+int rwkvtts_manager_create(const rwkvtts_manager_desc* desc, const void* weights, size_t bytes,
+                           rwkvtts_manager** out) {
+  RT_CHECK(desc && weights && out, RWKVTTS_EINVAL, "manager_create: null argument");
+  *out = nullptr;
+  try {
+    rwkvtts_manager* m = new rwkvtts_manager();
+    const int rc = m->m.create(*desc, weights, bytes);
+    if (rc != RWKVTTS_OK) {
+      m->m.shutdown();
+      delete m;
+      return rc;
+    }
+    *out = m;
+    return RWKVTTS_OK;
+  } catch (const std::exception& ex) {
+    set_error(ex.what());
+    return RWKVTTS_ENOMEM;
+  }
+}
+
+int rwkvtts_manager_destroy(rwkvtts_manager* m) {
+  if (!m) return RWKVTTS_OK;
+  m->m.shutdown();
+  delete m;
+  return RWKVTTS_OK;
+}
+
+int rwkvtts_manager_submit(rwkvtts_manager* m, const rwkvtts_request* req, uint64_t* ticket) {
+  RT_CHECK(m && req && ticket, RWKVTTS_EINVAL, "manager_submit: null argument");
+  try {
+    return m->m.submit(*req, ticket);
+  } catch (const std::exception& ex) {
+    set_error(ex.what());
+    return RWKVTTS_ENOMEM;
+  }
+}
+
+int rwkvtts_manager_wait(rwkvtts_manager* m, uint64_t ticket, int timeout_ms, rwkvtts_result* out) {
+  RT_CHECK(m && out, RWKVTTS_EINVAL, "manager_wait: null argument");
+  return m->m.wait(ticket, timeout_ms, out);
+}
+
+int rwkvtts_manager_generate_batch(rwkvtts_manager* m, const rwkvtts_request* reqs, int n,
+                                   rwkvtts_result* results) {
+  RT_CHECK(m && (n == 0 || (reqs && results)) && n >= 0, RWKVTTS_EINVAL, "manager_generate_batch: bad arguments");
+  std::vector<uint64_t> t(n);
+  for (int i = 0; i < n; ++i) {
+    const int rc = rwkvtts_manager_submit(m, &reqs[i], &t[i]);
+    if (rc != RWKVTTS_OK) return rc;
+  }
+  for (int i = 0; i < n; ++i) {
+    const int rc = m->m.wait(t[i], -1, &results[i]);
+    if (rc != RWKVTTS_OK) return rc;
+  }
+  return RWKVTTS_OK;
+}
+
+int rwkvtts_manager_get_stats(rwkvtts_manager* m, rwkvtts_manager_stats* out) {
+  RT_CHECK(m && out, RWKVTTS_EINVAL, "manager_get_stats: null argument");
+  m->m.stats(out);
+  return RWKVTTS_OK;
+}
+
+}  // extern "C"

@@ -901,7 +901,9 @@ __device__ __attribute__((always_inline)) void advance_body(const AdvanceArgs& a
   if (phase == kPhGFeed) {  // this step fed g31+8196: its logits are unused (RnnOption::Last)
     if (threadIdx.x == 0) {
       c->next_token = RWKVTTS_TAG_1;
-      c->phase = kPhSemantic;
+      // semantic_limit = min(max_tokens, 2048) may be 0 (normal_mode_inference.rs:316): the
+      // TAG_1 forward that follows has no observable output then, so the request ends here
+      c->phase = c->sem_limit > 0 ? kPhSemantic : kPhDone;
     }
     return;
   }

@@ -20,7 +20,8 @@ SEMANTIC_LIMIT = 2048
 HOP = 320
 SAMPLE_RATE = 16000
 
-OK, EINVAL, EHIP, ENOMEM, EUNSUPPORTED, EBUSY = 0, -1, -2, -3, -4, -5
+OK, EINVAL, EHIP, ENOMEM, EUNSUPPORTED, EBUSY, ECLOSED = 0, -1, -2, -3, -4, -5, -6
+MAX_ENGINES = 16
 DTYPE_BF16, DTYPE_F16 = 0, 1
 OPT_LAST, OPT_FULL = 0, 1
 
@@ -32,7 +33,8 @@ class Dims(ctypes.Structure):
 
 class EngineDesc(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("max_slots", ctypes.c_int32),
-                ("token_chunk_size", ctypes.c_int32), ("use_graphs", ctypes.c_int32)]
+                ("token_chunk_size", ctypes.c_int32), ("use_graphs", ctypes.c_int32),
+                ("wkv_variant", ctypes.c_int32)]
 
 
 class Input(ctypes.Structure):
@@ -56,7 +58,9 @@ class Request(ctypes.Structure):
                 ("ref_semantic", ctypes.POINTER(ctypes.c_int32)), ("n_ref_semantic", ctypes.c_int32),
                 ("has_seed", ctypes.c_int32), ("seed", ctypes.c_uint64),
                 ("max_tokens", ctypes.c_int32), ("fixed_semantic", ctypes.c_int32),
-                ("greedy", ctypes.c_int32)]
+                ("greedy", ctypes.c_int32), ("layered_set", ctypes.c_int32),
+                ("use_independent_seeds", ctypes.c_int32), ("global_seed_offset", ctypes.c_uint64),
+                ("semantic_seed_offset", ctypes.c_uint64)]
 
 
 class Result(ctypes.Structure):
@@ -70,6 +74,18 @@ class Stats(ctypes.Structure):
                 ("decode_ms", ctypes.c_double), ("prefill_ms", ctypes.c_double),
                 ("sample_ms", ctypes.c_double), ("decode_rows", ctypes.c_int64),
                 ("profile_kernel_count", ctypes.c_int32)]
+
+
+class ManagerDesc(ctypes.Structure):
+    _fields_ = [("n_engines", ctypes.c_int32), ("devices", ctypes.c_int32 * MAX_ENGINES),
+                ("engine", EngineDesc), ("max_batch_size", ctypes.c_int32),
+                ("collect_timeout_ms", ctypes.c_int32)]
+
+
+class ManagerStats(ctypes.Structure):
+    _fields_ = [("submitted", ctypes.c_int64), ("completed", ctypes.c_int64), ("batches", ctypes.c_int64),
+                ("served", ctypes.c_int64 * MAX_ENGINES), ("max_active", ctypes.c_int64 * MAX_ENGINES),
+                ("steps", ctypes.c_int64 * MAX_ENGINES)]
 
 
 class CodecDims(ctypes.Structure):
@@ -98,6 +114,15 @@ EXPORTS = {
                                       ctypes.POINTER(SampleArgs), ctypes.c_void_p, ctypes.c_void_p]),
     "rwkvtts_generate_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Request), ctypes.c_int,
                                               ctypes.POINTER(Result)]),
+    "rwkvtts_manager_create": (ctypes.c_int, [ctypes.POINTER(ManagerDesc), ctypes.c_void_p, ctypes.c_size_t,
+                                              ctypes.POINTER(ctypes.c_void_p)]),
+    "rwkvtts_manager_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "rwkvtts_manager_submit": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Request),
+                                              ctypes.POINTER(ctypes.c_uint64)]),
+    "rwkvtts_manager_wait": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(Result)]),
+    "rwkvtts_manager_generate_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Request), ctypes.c_int,
+                                                      ctypes.POINTER(Result)]),
+    "rwkvtts_manager_get_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ManagerStats)]),
     "rwkvtts_get_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Stats)]),
     "rwkvtts_set_profiling": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "rwkvtts_profile_entry": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,

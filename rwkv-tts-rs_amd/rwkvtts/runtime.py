@@ -10,10 +10,12 @@ C-ABI (include/rwkvtts.h). Names and argument meaning follow the Rust originals:
 * `SamplerArgs`, `TtsBatchRequest`, `DynamicBatchConfig` -- src/rwkv_sampler.rs:222-290,
   src/batch_types.rs:67-97
 * `DynamicBatchManager`    -- src/dynamic_batch_manager.rs:22-164: generate_tts /
-  generate_tts_batch; requests run concurrently in GPU slots (one slot per request).
+  generate_tts_batch over the native request manager (include/rwkvtts.h rwkvtts_manager_*):
+  thread-safe submit, the reference's collect window, one engine per GPU, continuous batching.
 """
 import ctypes
 import dataclasses
+import threading
 from typing import List, Optional, Sequence
 
 import numpy as np
@@ -63,13 +65,76 @@ class RnnInput:
     token_chunk_size: int = 512
 
 
+def _locked(fn):
+    def wrapper(self, *a, **k):
+        with self._lock:
+            return fn(self, *a, **k)
+    wrapper.__name__ = fn.__name__
+    wrapper.__doc__ = fn.__doc__
+    return wrapper
+
+
+def request_struct(r: "TtsBatchRequest"):
+    """TtsBatchRequest -> (_ffi.Request, keepalive arrays)."""
+    keep = []
+
+    def arr(x):
+        if x is None:
+            return None
+        a = np.ascontiguousarray(np.asarray(x, dtype=np.int32))
+        keep.append(a)
+        return a
+    P = ctypes.POINTER(ctypes.c_int32)
+    q = _ffi.Request()
+    tt, pt, rg, rs = arr(r.text_tokens), arr(r.property_tokens), arr(r.ref_global_tokens), arr(r.ref_semantic_tokens)
+    q.text_tokens = tt.ctypes.data_as(P) if tt is not None and len(tt) else None
+    q.n_text = 0 if tt is None else len(tt)
+    q.property_tokens = pt.ctypes.data_as(P) if pt is not None and len(pt) else None
+    q.n_property = 0 if pt is None else len(pt)
+    # Some(empty) stays distinguishable from None: a non-null pointer with count 0
+    q.ref_global = (rg.ctypes.data_as(P) if len(rg) else ctypes.cast(ctypes.pointer(_EMPTY), P)) if rg is not None else None
+    q.n_ref_global = 0 if rg is None else len(rg)
+    q.ref_semantic = (rs.ctypes.data_as(P) if len(rs) else ctypes.cast(ctypes.pointer(_EMPTY), P)) if rs is not None else None
+    q.n_ref_semantic = 0 if rs is None else len(rs)
+    q.has_seed = 0 if r.args.seed is None else 1
+    q.seed = 0 if r.args.seed is None else int(r.args.seed) & 0xFFFFFFFFFFFFFFFF
+    q.max_tokens = int(r.args.max_tokens)
+    q.fixed_semantic = r.fixed_semantic
+    q.greedy = 1 if r.greedy else 0
+    lr = r.args.layered_randomness
+    q.layered_set = 1
+    q.use_independent_seeds = 1 if lr.use_independent_seeds else 0
+    q.global_seed_offset = int(lr.global_seed_offset) & 0xFFFFFFFFFFFFFFFF
+    q.semantic_seed_offset = int(lr.semantic_seed_offset) & 0xFFFFFFFFFFFFFFFF
+    return q, keep
+
+
+_EMPTY = ctypes.c_int32(0)
+
+
+def _unpack_results(res, sem_bufs):
+    """(global, semantic) per request; a failed request gives ([], []) like
+    dynamic_batch_manager.rs:466-469. Also returns the per-request status codes."""
+    out, status = [], []
+    for i in range(len(res)):
+        status.append(int(res[i].status))
+        if res[i].status != 0:
+            out.append(([], []))
+            continue
+        out.append((list(res[i].global_tokens[:res[i].n_global]), sem_bufs[i][:res[i].n_semantic].tolist()))
+    return out, status
+
+
 class SharedRwkvRuntime:
     """One engine per GPU: weights resident in HBM, `max_concurrent_batches` state slots."""
 
     def __init__(self, weights: np.ndarray, device: int = 0, max_slots: int = 10,
                  token_chunk_size: int = 512, use_graphs: bool = True, weights_on_device: bool = False,
-                 device_ptr: Optional[int] = None):
-        desc = _ffi.EngineDesc(device, max_slots, token_chunk_size, 1 if use_graphs else 0)
+                 device_ptr: Optional[int] = None, wkv_variant: int = 0):
+        # the C ABI serialises calls per engine; this lock also keeps Python-side buffers of one
+        # call from interleaving with another thread's
+        self._lock = threading.RLock()
+        desc = _ffi.EngineDesc(device, max_slots, token_chunk_size, 1 if use_graphs else 0, wkv_variant)
         h = ctypes.c_void_p()
         if device_ptr is not None:
             check(lib().rwkvtts_engine_create(ctypes.byref(desc), ctypes.c_void_p(device_ptr),
@@ -101,22 +166,27 @@ class SharedRwkvRuntime:
         return self._h
 
     # ---- state (State::init / load / back) ----
+    @_locked
     def state_floats(self) -> int:
         return int(lib().rwkvtts_state_floats(self._h))
 
+    @_locked
     def reset_slot(self, slot: int):
         check(lib().rwkvtts_slot_reset(self._h, slot), "slot_reset")
 
+    @_locked
     def read_slot(self, slot: int) -> np.ndarray:
         out = np.empty(self.state_floats(), dtype=np.float32)
         check(lib().rwkvtts_slot_read(self._h, slot, out.ctypes.data_as(ctypes.c_void_p)), "slot_read")
         return out
 
+    @_locked
     def write_slot(self, slot: int, state: np.ndarray):
         s = np.ascontiguousarray(state, dtype=np.float32)
         check(lib().rwkvtts_slot_write(self._h, slot, s.ctypes.data_as(ctypes.c_void_p)), "slot_write")
 
     # ---- Runtime<Rnn>::infer ----
+    @_locked
     def infer(self, inp: RnnInput, head_rows: Optional[int] = None, slots: Optional[Sequence[int]] = None):
         """Returns (remaining RnnInput, outputs) where outputs[i] is an np.ndarray of logits
         (empty while batch i still has pending input). Batch index == state slot unless
@@ -155,6 +225,7 @@ class SharedRwkvRuntime:
         return remaining, outputs
 
     # ---- device sampler ----
+    @_locked
     def sample(self, logits: np.ndarray, temperature=1.0, top_p=0.85, top_k=0, forbid_token=None,
                rngs: Optional[Sequence[Optional[StdRng]]] = None) -> np.ndarray:
         lg = np.ascontiguousarray(np.atleast_2d(logits), dtype=np.float32)
@@ -170,52 +241,36 @@ class SharedRwkvRuntime:
         return out
 
     # ---- scheduler ----
+    @_locked
     def generate_batch(self, requests: Sequence["TtsBatchRequest"]):
+        """generate_tts_batch on this engine; failed requests give ([], []) (status in
+        self.last_status)."""
         n = len(requests)
         reqs = (_ffi.Request * n)()
         res = (_ffi.Result * n)()
         keep, sem_bufs = [], []
         for i, r in enumerate(requests):
-            def arr(x):
-                if x is None:
-                    return None
-                a = np.ascontiguousarray(np.asarray(x, dtype=np.int32))
-                keep.append(a)
-                return a
-            tt, pt, rg, rs = arr(r.text_tokens), arr(r.property_tokens), arr(r.ref_global_tokens), arr(r.ref_semantic_tokens)
-            P = ctypes.POINTER(ctypes.c_int32)
-            reqs[i].text_tokens = tt.ctypes.data_as(P) if tt is not None and len(tt) else None
-            reqs[i].n_text = 0 if tt is None else len(tt)
-            reqs[i].property_tokens = pt.ctypes.data_as(P) if pt is not None and len(pt) else None
-            reqs[i].n_property = 0 if pt is None else len(pt)
-            reqs[i].ref_global = rg.ctypes.data_as(P) if rg is not None else None
-            reqs[i].n_ref_global = 0 if rg is None else len(rg)
-            reqs[i].ref_semantic = rs.ctypes.data_as(P) if rs is not None else None
-            reqs[i].n_ref_semantic = 0 if rs is None else len(rs)
-            reqs[i].has_seed = 0 if r.args.seed is None else 1
-            reqs[i].seed = 0 if r.args.seed is None else r.args.seed
-            reqs[i].max_tokens = r.args.max_tokens
-            reqs[i].fixed_semantic = r.fixed_semantic
-            reqs[i].greedy = 1 if r.greedy else 0
+            q, k = request_struct(r)
+            keep.append(k)
+            reqs[i] = q
             sb = np.zeros(_ffi.SEMANTIC_LIMIT, dtype=np.int32)
             sem_bufs.append(sb)
             res[i].semantic_tokens = sb.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
         check(lib().rwkvtts_generate_batch(self._h, reqs, n, res), "generate_batch")
-        out = []
-        for i in range(n):
-            g = list(res[i].global_tokens[:res[i].n_global])
-            s = sem_bufs[i][:res[i].n_semantic].tolist()
-            out.append((g, s))
+        out, self.last_status = _unpack_results(res, sem_bufs)
         return out
 
+    @_locked
     def stats(self):
         s = _ffi.Stats()
         check(lib().rwkvtts_get_stats(self._h, ctypes.byref(s)), "get_stats")
         return {f: getattr(s, f) for f, _ in _ffi.Stats._fields_}
 
+    @_locked
     def set_profiling(self, on: bool):
         check(lib().rwkvtts_set_profiling(self._h, 1 if on else 0), "set_profiling")
 
+    @_locked
     def profile(self):
         out = {}
         n = self.stats()["profile_kernel_count"]
@@ -280,19 +335,91 @@ class DynamicBatchConfig:  # src/batch_types.rs:67-97
 
 
 class DynamicBatchManager:
-    """generate_tts / generate_tts_batch over one GPU engine. Unlike the reference (which runs a
-    collected batch sequentially on state slot 0), requests decode concurrently, one slot each;
-    per-request outputs equal the serial run."""
+    """src/dynamic_batch_manager.rs:22-164 over the native manager (rwkvtts_manager_*): any
+    thread may call generate_tts; the collector batches concurrent calls with the reference's
+    collect window and routes each request to the least-loaded engine (one per device, one owner
+    thread each), whose continuous batching decodes all its requests together. Per-request
+    outputs equal the serial single-engine run."""
 
-    def __init__(self, runtime: SharedRwkvRuntime, config: Optional[DynamicBatchConfig] = None):
-        self.runtime = runtime
+    def __init__(self, weights: np.ndarray, config: Optional[DynamicBatchConfig] = None,
+                 devices: Sequence[int] = (0,), max_slots: int = 32, token_chunk_size: int = 512,
+                 use_graphs: bool = True, wkv_variant: int = 0, tokenizer=None):
         self.config = config or DynamicBatchConfig()
+        devices = list(devices)
+        if not 1 <= len(devices) <= _ffi.MAX_ENGINES:
+            raise ValueError("1..16 engines")
+        d = _ffi.ManagerDesc()
+        d.n_engines = len(devices)
+        for i, dev in enumerate(devices):
+            d.devices[i] = dev
+        d.engine = _ffi.EngineDesc(0, max_slots, token_chunk_size, 1 if use_graphs else 0, wkv_variant)
+        d.max_batch_size = self.config.max_batch_size
+        d.collect_timeout_ms = self.config.collect_timeout_ms
+        w = np.ascontiguousarray(weights)
+        h = ctypes.c_void_p()
+        check(lib().rwkvtts_manager_create(ctypes.byref(d), w.ctypes.data_as(ctypes.c_void_p), w.nbytes,
+                                           ctypes.byref(h)), "manager_create")
+        self._h = h
+        self.devices = devices
+        self.tokenizer = tokenizer
+        self.last_status = []
 
-    def generate_tts(self, text_tokens, property_tokens, ref_global_tokens=None, ref_semantic_tokens=None,
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().rwkvtts_manager_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _tokens(self, text):
+        if isinstance(text, str):
+            if self.tokenizer is None:
+                raise ValueError("text given as a string but the manager has no tokenizer")
+            return self.tokenizer.encode(text)  # dynamic_batch_manager.rs:512-515
+        return list(text)
+
+    def submit(self, request: "TtsBatchRequest") -> int:
+        q, keep = request_struct(request)
+        t = ctypes.c_uint64()
+        check(lib().rwkvtts_manager_submit(self._h, ctypes.byref(q), ctypes.byref(t)), "manager_submit")
+        return int(t.value)
+
+    def wait(self, ticket: int, timeout_ms: int = -1):
+        """(global, semantic) or None if not ready within timeout_ms; ([], []) for a failed request."""
+        r = _ffi.Result()
+        sb = np.zeros(_ffi.SEMANTIC_LIMIT, dtype=np.int32)
+        r.semantic_tokens = sb.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+        rc = lib().rwkvtts_manager_wait(self._h, ctypes.c_uint64(ticket), timeout_ms, ctypes.byref(r))
+        if rc == _ffi.EBUSY:
+            return None
+        check(rc, "manager_wait")
+        res = (_ffi.Result * 1)(r)
+        out, status = _unpack_results(res, [sb])
+        self.last_status = status
+        return out[0]
+
+    def generate_tts(self, text, property_tokens, ref_global_tokens=None, ref_semantic_tokens=None,
                      voice_id=None, args: Optional[SamplerArgs] = None):
-        req = TtsBatchRequest(list(text_tokens), list(property_tokens), ref_global_tokens, ref_semantic_tokens,
+        req = TtsBatchRequest(self._tokens(text), list(property_tokens), ref_global_tokens, ref_semantic_tokens,
                               args or SamplerArgs(), voice_id)
-        return self.runtime.generate_batch([req])[0]
+        return self.wait(self.submit(req))
 
     def generate_tts_batch(self, requests: Sequence[TtsBatchRequest]):
-        return self.runtime.generate_batch(list(requests))
+        tickets = [self.submit(r) for r in requests]
+        out, status = [], []
+        for t in tickets:
+            out.append(self.wait(t))
+            status.extend(self.last_status)
+        self.last_status = status
+        return out
+
+    def stats(self):
+        s = _ffi.ManagerStats()
+        check(lib().rwkvtts_manager_get_stats(self._h, ctypes.byref(s)), "manager_get_stats")
+        n = len(self.devices)
+        return {"submitted": s.submitted, "completed": s.completed, "batches": s.batches,
+                "served": list(s.served[:n]), "max_active": list(s.max_active[:n]), "steps": list(s.steps[:n])}

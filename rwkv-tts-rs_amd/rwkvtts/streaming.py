@@ -148,19 +148,22 @@ class StreamingInference:  # :141-416
     def _process(self, batch: Sequence[tuple]):
         t0 = time.monotonic()
         slots = list(range(len(batch)))
-        for s in slots:
-            self.runtime.reset_slot(s)
         inp = RnnInput([RnnInputBatch(list(r.tokens)) for r, _ in batch], self.runtime.token_chunk_size)
         outs = [None] * len(batch)
         try:
-            while any(o is None for o in outs):  # feed until every request produced its logits
-                idx = [i for i, o in enumerate(outs) if o is None]
-                sub = RnnInput([inp.batches[i] for i in idx], inp.token_chunk_size)
-                rem, got = self.runtime.infer(sub, slots=[slots[i] for i in idx])
-                for j, i in enumerate(idx):
-                    inp.batches[i] = rem.batches[j]
-                    if got[j].size:
-                        outs[i] = got[j]
+            # the whole batch (slot resets + every infer call) holds the runtime's lock, so another
+            # thread's generate_batch / infer on the same engine cannot touch these slots meanwhile
+            with self.runtime._lock:
+                for s in slots:
+                    self.runtime.reset_slot(s)
+                while any(o is None for o in outs):  # feed until every request produced its logits
+                    idx = [i for i, o in enumerate(outs) if o is None]
+                    sub = RnnInput([inp.batches[i] for i in idx], inp.token_chunk_size)
+                    rem, got = self.runtime.infer(sub, slots=[slots[i] for i in idx])
+                    for j, i in enumerate(idx):
+                        inp.batches[i] = rem.batches[j]
+                        if got[j].size:
+                            outs[i] = got[j]
         except Exception as ex:  # noqa: BLE001 -- every waiter gets the failure
             for _, fut in batch:
                 fut.set_exception(ex)

@@ -1,0 +1,235 @@
+"""The benchmarked configuration (config 3: 32 decode slots) and the scheduler's request
+semantics on the GPU, against the oracle's serial reference loop.
+
+* 32 slots select the k_wkv4 path (state layout 1, LoRA-up repack launch_pack_lora4); the
+  engine's wkv_variant forces k_wkv6 (layout 2) in the same session, so both kernels and both
+  slot_read / slot_write layout conversions are checked at the 0.4B widths.
+* the full 24-layer 0.4B model at 32 slots: logits and tokens against the oracle.
+* per-request failure (dynamic_batch_manager.rs:466-469), max_tokens == 0
+  (normal_mode_inference.rs:316), LayeredRandomnessConfig seeds (normal_mode_inference.rs:138-174),
+  staggered admission (prompt rows riding in decode steps), the native request manager with two
+  engines and concurrent callers.
+"""
+import json
+import os
+import threading
+
+import numpy as np
+import pytest
+
+import rwkvtts
+from rwkvtts import weights as W
+from helpers import PROPS, make_request, synth_text, to_struct
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+LOGIT_ATOL = 2e-3  # as test_gpu_forward.py: bf16 weights exact, activations at ~2^-17 relative
+
+
+def _oracle(om, req):
+    q, keep = to_struct(req)
+    g, s, _ = om.generate(q)
+    return g, s
+
+
+def _dtype(name):
+    return rwkvtts._ffi.DTYPE_F16 if name == "f16" else rwkvtts._ffi.DTYPE_BF16
+
+
+@pytest.fixture(scope="module", params=[("bf16", 1), ("bf16", 2), ("f16", 1), ("f16", 2)],
+                ids=["bf16-wkv4", "bf16-wkv6", "f16-wkv4", "f16-wkv6"])
+def mid32(request):
+    dt, variant = request.param
+    blob = W.synth_blob(W.DIMS_MID, seed=5, dtype=_dtype(dt))
+    import oracle
+    om = oracle.Model(blob)
+    rt = rwkvtts.SharedRwkvRuntime(blob, max_slots=32, token_chunk_size=512, use_graphs=True, wkv_variant=variant)
+    yield om, rt
+    rt.close()
+
+
+def test_32_slots_token_exact(mid32):
+    """32 concurrent requests (config 3's decode shape) at the 0.4B widths, every token equal."""
+    om, rt = mid32
+    reqs = [make_request(synth_text(700 + i), seed=900 + i, fixed=16) for i in range(32)]
+    got = rt.generate_batch(reqs)
+    assert rt.stats()["decode_rows"] >= 32 * 40  # the steps really ran 32 rows
+    for r, gs in zip(reqs, got):
+        assert gs == _oracle(om, r)
+
+
+def test_32_slots_state_readback(mid32):
+    """slot_read (layout -> S[i][j]) after a 32-slot prefill equals the oracle state; slot_write
+    then slot_read round-trips bitwise."""
+    om, rt = mid32
+    prompts = [PROPS + [rwkvtts.TAG_2] + synth_text(40 + s) + [rwkvtts.TAG_0] for s in range(32)]
+    for s in range(32):
+        rt.reset_slot(s)
+    inp = rwkvtts.RnnInput([rwkvtts.RnnInputBatch(list(p)) for p in prompts], 512)
+    outs = [None] * 32
+    while any(o is None for o in outs):
+        inp, o = rt.infer(inp, head_rows=8193, slots=list(range(32)))
+        for i in range(32):
+            if outs[i] is None and o[i].size:
+                outs[i] = o[i]
+    for s in (0, 13, 31):
+        st = om.new_state()
+        ref = [om.forward(st, t, 8193) for t in prompts[s]][-1]
+        assert np.abs(outs[s] - ref).max() < LOGIT_ATOL
+        assert np.abs(rt.read_slot(s) - st).max() < 1e-3
+    s5 = rt.read_slot(5)
+    rt.write_slot(31, s5)
+    assert np.array_equal(rt.read_slot(31), s5)
+
+
+@pytest.mark.parametrize("dt", ["bf16", "f16"])
+def test_full_04b_32_slots(dt):
+    """The full 24-layer 0.4B model at 32 slots: logits of a 32-slot prefill + decode step and
+    the tokens of 4 of 32 concurrent requests equal the oracle."""
+    blob = W.synth_blob(W.DIMS_04B, seed=20251205, dtype=_dtype(dt))
+    import oracle
+    om = oracle.Model(blob)
+    rt = rwkvtts.SharedRwkvRuntime(blob, max_slots=32, token_chunk_size=512, use_graphs=True)
+    try:
+        reqs = [make_request(synth_text(1000 + i), seed=2000 + i, fixed=8) for i in range(32)]
+        got = rt.generate_batch(reqs)
+        for i in (0, 9, 22, 31):
+            assert got[i] == _oracle(om, reqs[i]), i
+        # teacher-forced logits on 32 slots
+        prompts = [PROPS + [rwkvtts.TAG_2] + synth_text(50 + s) + [rwkvtts.TAG_0] for s in range(32)]
+        for s in range(32):
+            rt.reset_slot(s)
+        inp = rwkvtts.RnnInput([rwkvtts.RnnInputBatch(list(p)) for p in prompts], 512)
+        outs = [None] * 32
+        while any(o is None for o in outs):
+            inp, o = rt.infer(inp, head_rows=8193, slots=list(range(32)))
+            for i in range(32):
+                if outs[i] is None and o[i].size:
+                    outs[i] = o[i]
+        _, dec = rt.infer(rwkvtts.RnnInput([rwkvtts.RnnInputBatch([8196 + 17 * s]) for s in range(32)], 512),
+                          head_rows=8193, slots=list(range(32)))
+        for s in (3, 30):
+            st = om.new_state()
+            ref = [om.forward(st, t, 8193) for t in prompts[s]][-1]
+            assert np.abs(outs[s] - ref).max() < LOGIT_ATOL
+            ref2 = om.forward(st, 8196 + 17 * s, 8193)
+            assert np.abs(dec[s] - ref2).max() < LOGIT_ATOL
+    finally:
+        rt.close()
+
+
+# ---- request semantics (tiny model) ---------------------------------------------------------
+@pytest.fixture(scope="module")
+def tiny():
+    blob = W.synth_blob(W.DIMS_TINY, seed=99)
+    import oracle
+    om = oracle.Model(blob)
+    rt = rwkvtts.SharedRwkvRuntime(blob, max_slots=8, token_chunk_size=128, use_graphs=True)
+    yield blob, om, rt
+    rt.close()
+
+
+def test_bad_request_fails_alone(tiny):
+    """One request with an out-of-vocabulary id gets status < 0 and ([], []); the other 7 of
+    the batch complete exactly as when run alone (dynamic_batch_manager.rs:466-469)."""
+    blob, om, rt = tiny
+    reqs = [make_request(synth_text(300 + i), seed=10 + i, max_tokens=20) for i in range(8)]
+    reqs[3] = make_request(synth_text(303)[:5] + [80000] + synth_text(303)[5:], seed=13, max_tokens=20)
+    got = rt.generate_batch(reqs)
+    assert rt.last_status[3] == rwkvtts._ffi.EINVAL and got[3] == ([], [])
+    for i in range(8):
+        if i != 3:
+            assert rt.last_status[i] == 0
+            assert got[i] == _oracle(om, reqs[i])
+    bad_neg = make_request(synth_text(1), seed=1, max_tokens=-1)
+    assert rt.generate_batch([bad_neg]) == [([], [])] and rt.last_status == [rwkvtts._ffi.EINVAL]
+
+
+def test_max_tokens_zero(tiny):
+    """usize::min(max_tokens, 2048) == 0: 32 global tokens, no semantic tokens."""
+    blob, om, rt = tiny
+    r = make_request(synth_text(5), seed=3, max_tokens=0)
+    (g, s), = rt.generate_batch([r])
+    assert len(g) == 32 and s == []
+    assert (g, s) == _oracle(om, r)
+
+
+def test_layered_randomness_seeds(tiny):
+    """use_independent_seeds false -> StdRng(seed+100 / +200); custom offsets honoured."""
+    blob, om, rt = tiny
+    a = make_request(synth_text(6), seed=44, max_tokens=12)
+    a.args.layered_randomness = rwkvtts.LayeredRandomnessConfig(use_independent_seeds=False)
+    b = make_request(synth_text(6), seed=44, max_tokens=12)
+    b.args.layered_randomness = rwkvtts.LayeredRandomnessConfig(global_seed_offset=7, semantic_seed_offset=9)
+    c = make_request(synth_text(6), seed=44, max_tokens=12)
+    got = rt.generate_batch([a, b, c])
+    assert got == [_oracle(om, a), _oracle(om, b), _oracle(om, c)]
+    assert got[0] != got[2] and got[1] != got[2]
+    raf = json.load(open(os.path.join(GOLDEN, "raf_voice_05d8f5ed.json")))
+    z = make_request(synth_text(8, n=6), props=[], seed=5, ref_global=raf["global_tokens"],
+                     ref_semantic=raf["semantic_tokens"][:20])
+    z.args.layered_randomness = rwkvtts.LayeredRandomnessConfig(use_independent_seeds=False)
+    assert rt.generate_batch([z]) == [_oracle(om, z)]  # zero-shot: StdRng(0) as the reference
+
+
+def test_staggered_admission_equals_serial():
+    """3 slots, 8 requests of different lengths: later requests are admitted while others decode
+    (their prompt rows ride in the decode steps); every result equals its serial run."""
+    blob = W.synth_blob(W.DIMS_TINY, seed=99)
+    import oracle
+    om = oracle.Model(blob)
+    rt = rwkvtts.SharedRwkvRuntime(blob, max_slots=3, token_chunk_size=64, use_graphs=True)
+    try:
+        reqs = [make_request(synth_text(500 + i, n=8 + 5 * i), seed=70 + i, max_tokens=6 + 7 * i) for i in range(8)]
+        got = rt.generate_batch(reqs)
+        st = rt.stats()
+        assert st["prefill_steps"] >= 4  # admissions happened while slots were decoding
+        for r, gs in zip(reqs, got):
+            assert gs == _oracle(om, r)
+    finally:
+        rt.close()
+
+
+def test_runtime_is_thread_safe(tiny):
+    """Concurrent callers on one engine serialise on its lock and get correct results."""
+    blob, om, rt = tiny
+    reqs = [make_request(synth_text(900 + i), seed=400 + i, max_tokens=15) for i in range(6)]
+    got = [None] * 6
+    ths = [threading.Thread(target=lambda i=i: got.__setitem__(i, rt.generate_batch([reqs[i]])[0])) for i in range(6)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    for r, gs in zip(reqs, got):
+        assert gs == _oracle(om, r)
+
+
+def test_manager_two_engines_concurrent_callers():
+    """DynamicBatchManager over two engines (both on device 0): 12 threads call generate_tts at
+    once; the collector batches them, both engines serve, and every result equals the oracle."""
+    blob = W.synth_blob(W.DIMS_TINY, seed=99)
+    import oracle
+    om = oracle.Model(blob)
+    m = rwkvtts.DynamicBatchManager(blob, rwkvtts.DynamicBatchConfig(max_batch_size=10, collect_timeout_ms=20),
+                                    devices=[0, 0], max_slots=4, token_chunk_size=64)
+    try:
+        reqs = [make_request(synth_text(1200 + i), seed=600 + i, max_tokens=10 + i) for i in range(12)]
+        got = [None] * 12
+        ths = [threading.Thread(target=lambda i=i: got.__setitem__(
+            i, m.generate_tts(reqs[i].text_tokens, reqs[i].property_tokens, args=reqs[i].args))) for i in range(12)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        for r, gs in zip(reqs, got):
+            assert gs == _oracle(om, r)
+        st = m.stats()
+        assert st["completed"] == 12 and all(n > 0 for n in st["served"]), st
+        assert st["batches"] < 12  # concurrent callers shared batches
+        # generate_tts_batch through the manager, including a failing request
+        reqs[2] = make_request([80000], seed=1)
+        out = m.generate_tts_batch(reqs[:4])
+        assert out[2] == ([], []) and m.last_status[2] == rwkvtts._ffi.EINVAL
+        assert out[0] == _oracle(om, reqs[0])
+    finally:
+        m.close()

@@ -15,6 +15,7 @@ class FakeRuntime:
 
     def __init__(self):
         self.calls = []
+        self._lock = threading.RLock()
 
     def reset_slot(self, s):
         pass
@@ -58,8 +59,10 @@ def test_priority_order_cache_and_stats():
 def test_streaming_matches_direct_infer():
     import rwkvtts
     from rwkvtts import weights as W
-    rt = rwkvtts.SharedRwkvRuntime(W.synth_blob(W.DIMS_TINY, seed=5), max_slots=4, token_chunk_size=16,
-                                   use_graphs=False)
+    import oracle
+    blob = W.synth_blob(W.DIMS_TINY, seed=5)
+    om = oracle.Model(blob)
+    rt = rwkvtts.SharedRwkvRuntime(blob, max_slots=4, token_chunk_size=16, use_graphs=False)
     si = S.StreamingInference(rt, S.BatchConfig(max_batch_size=4))
     si.start()
     toks = [[77823, 77838, 8195] + list(range(20000 + i, 20000 + i + 5 + 7 * i)) + [8193] for i in range(6)]
@@ -79,4 +82,9 @@ def test_streaming_matches_direct_infer():
             inp, o = rt.infer(inp, slots=[0])
             out = o[0]
         assert np.array_equal(got[i].logits, out)
+        # and against the oracle's f32 restatement (tolerance of test_gpu_forward.py)
+        st = om.new_state()
+        V = out.size
+        ref = [om.forward(st, t, V) for t in toks[i]][-1]
+        assert np.abs(got[i].logits - ref).max() < 2e-3
     rt.close()
