@@ -355,6 +355,21 @@ int rwkvtts_codec_profile_count(rwkvtts_codec* c);
 int rwkvtts_codec_profile_entry(rwkvtts_codec* c, int idx, char* name, int name_cap, int64_t* launches,
                                 double* total_ms);
 
+/* ---- text tokenizer: web-rwkv Tokenizer::new / encode (src/shared_runtime.rs:187-192,
+ * src/dynamic_batch_manager.rs:512-515) over assets/model/tokenizer.json -------------------- */
+typedef struct rwkvtts_tokenizer rwkvtts_tokenizer;
+/* vocab_json: the vocabulary file's bytes ({"id": "token" | [bytes], ...}). */
+int rwkvtts_tokenizer_create(const char* vocab_json, size_t len, rwkvtts_tokenizer** out);
+int rwkvtts_tokenizer_destroy(rwkvtts_tokenizer* t);
+/* Greedy longest match over UTF-8 bytes. ids == NULL (or cap too small) only counts: *n_ids is
+ * always the full count. A byte position no token matches -> RWKVTTS_EINVAL
+ * (TokenizerError::NoMatchingTokenFound). */
+int rwkvtts_tokenizer_encode(const rwkvtts_tokenizer* t, const uint8_t* text, size_t n, uint32_t* ids,
+                             size_t cap, size_t* n_ids);
+int rwkvtts_tokenizer_decode(const rwkvtts_tokenizer* t, const uint32_t* ids, size_t n, uint8_t* text,
+                             size_t cap, size_t* n_bytes);
+int64_t rwkvtts_tokenizer_vocab_size(const rwkvtts_tokenizer* t); /* max id + 1 */
+
 /* ---- zero-shot reference mel (src/tts_pipeline_fixes.rs:12-159) ------------------------- */
 /* wav [n] f32 @16 kHz -> mel [128][n_frames] (n_frames = (n + 1024 - 1024) / 320 + 1). */
 int rwkvtts_mel(int device, const float* wav, int n, float* mel, int* n_frames);

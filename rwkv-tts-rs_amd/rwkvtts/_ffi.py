@@ -140,6 +140,13 @@ EXPORTS = {
     "rwkvtts_codec_profile_count": (ctypes.c_int, [ctypes.c_void_p]),
     "rwkvtts_codec_profile_entry": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
                                                    ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)]),
+    "rwkvtts_tokenizer_create": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)]),
+    "rwkvtts_tokenizer_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "rwkvtts_tokenizer_encode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p,
+                                                ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]),
+    "rwkvtts_tokenizer_decode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                                ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]),
+    "rwkvtts_tokenizer_vocab_size": (ctypes.c_int64, [ctypes.c_void_p]),
     "rwkvtts_mel": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                                    ctypes.POINTER(ctypes.c_int)]),
 }
