@@ -76,6 +76,13 @@ struct GemmArgs {
   int n_tinfo;         // 0: per-segment lookup
   const bf16_t* tw;
   int64_t x_mix_stride;
+  // XCD-aware 1-D grid (set by the launcher for single-row-group launches): workgroups that
+  // share a K-slice -- hence the same X slice / key slabs -- run on one XCD (blocks b and b + 8
+  // share one), so each XCD's L2 fetches its slices' activations once instead of all eight
+  // fetching every slice. xmap 0: grid (tiles, k_split, row groups).
+  int xmap;
+  int ntiles;          // column tiles
+  int tiles_per_xcd;   // k_split < 8: tiles of one split per XCD (ceil(ntiles * k_split / 8))
   uint32_t tinfo[128];
 };
 
@@ -100,6 +107,7 @@ struct WkvArgs {
   int n_slots;         // state slots (bounds the speculative slot = segment index)
   int n_seg;           // segments in this step 
   int perm;            // state block layout (wkv_perm_layout): 0 row-major, 1 k_wkv4, 2 k_wkv6
+  int xmap;            // k_wkv4 / k_wkv6: 1-D grid, head h's workgroups on one XCD (H % 8 == 0)
   int f16;             // fp16 model: LoRA-up rows and the z planes are f16
   uint64_t* stamps;    // debug: 8 s_memtime stamps per workgroup (null in production)
   int exp;             // debug experiment bits (0 in production)

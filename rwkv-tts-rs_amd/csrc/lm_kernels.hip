@@ -374,6 +374,7 @@ __global__ __launch_bounds__(256) void k_ln1024(LnMixArgs a) {
 template <int MT, int KSTEPS, int XMODE, bool F16>
 __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ uint32_t s_rexp[MT * 16];  // f16 relu^2 rows: bits of the row maximum if >= 2^15
   constexpr int KS = KSTEPS * 32;      // K slice
   constexpr int LD = KS + 8;           // LDS row stride (elements): +16 B breaks bank aliasing
   constexpr int ROWS = MT * 16;
@@ -450,14 +451,33 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
 #pragma unroll
         for (int u = 0; u < PER; ++u) x[u] += t[pp][u];
     }
+    // f16 model: per-row power-of-two range scaling of relu^2 (see k_gemm2)
+    if constexpr (F16) {
+      if (threadIdx.x < ROWS) s_rexp[threadIdx.x] = 0u;
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        const int r = (threadIdx.x + u * 256) / (KS / 4);
+        float m = 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) m = fmaxf(m, x[u][e] > 0.f ? x[u][e] * x[u][e] : 0.f);
+        if (m >= 32768.f) atomicMax(&s_rexp[r], as_u32(m));
+      }
+      __syncthreads();
+    }
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int c = threadIdx.x + u * 256;
       const int r = c / (KS / 4), k4 = (c % (KS / 4)) * 4;
       uint16_t h[4], l[4];
+      float sc = 1.f;
+      if constexpr (F16) {
+        const uint32_t mb = s_rexp[r];
+        if (mb) sc = as_f32((uint32_t)(127 - (int)((mb >> 23) & 0xFF) + 127 + 14) << 23);
+      }
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float y = x[u][e] > 0.f ? x[u][e] * x[u][e] : 0.f;
+        const float y = (x[u][e] > 0.f ? x[u][e] * x[u][e] : 0.f) * sc;
         h[e] = f32_to_w16(y, F16);
         l[e] = f32_to_w16(y - w16_to_f32(h[e], F16), F16);
       }
@@ -500,7 +520,12 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int row = row0 + m * 16 + 4 * g + j;
-        if (row < a.M) a.out[split * a.split_stride + (int64_t)row * a.ldo + sg.col_off + col] = acc[m][j];
+        float v = acc[m][j];
+        if constexpr (F16 && XMODE == kXRelu2) {
+          const uint32_t mb = s_rexp[m * 16 + 4 * g + j];
+          if (mb) v *= as_f32((uint32_t)((int)((mb >> 23) & 0xFF) - 127 - 14 + 127) << 23);
+        }
+        if (row < a.M) a.out[split * a.split_stride + (int64_t)row * a.ldo + sg.col_off + col] = v;
       }
   }
   if (gst) gst[3] = __builtin_amdgcn_s_memtime();
@@ -518,6 +543,7 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
 template <int MT, int KSTEPS, int XMODE, bool F16, int NX, int MS>
 __global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ uint32_t s_rexp[MT * 16];  // f16 relu^2 rows: bits of the row maximum if >= 2^15
   constexpr int KS = KSTEPS * 32;
   constexpr int LD = KS + 8;
   constexpr int ROWS = MT * 16;
@@ -527,7 +553,18 @@ __global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
   float* e_out = a.out;
   int64_t e_sstride = a.split_stride;
   int e_ldo = a.ldo, e_M = a.M;
-  const int tile = blockIdx.x;
+  int tile = blockIdx.x, split = blockIdx.y;
+  if (a.xmap) {  // XCD-aware 1-D grid (GemmArgs::xmap)
+    const int b = blockIdx.x, xcd = b & 7, j = b >> 3;
+    if (a.k_split >= 8) {
+      split = xcd + 8 * (j / a.ntiles);
+      tile = j % a.ntiles;
+    } else {
+      split = xcd % a.k_split;
+      tile = (xcd / a.k_split) * a.tiles_per_xcd + j;
+      if (tile >= a.ntiles) return;  // padding workgroup
+    }
+  }
   // MS 0: one segment, read from seg[0] directly. MS 1: several segments, looked up from the
   // tile starts (a second, dependent kernel-argument round trip). MS 2: several segments
   // through the per-tile descriptor table (one round trip, addressed by blockIdx alone).
@@ -561,9 +598,8 @@ __global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int g = lane >> 4, li = lane & 15;
   const int col0 = (tile - tstart) * 64 + wave * 16;
-  const int split = blockIdx.y;
   const int kbeg = split * KS;
-  const int row0 = blockIdx.z * ROWS;
+  const int row0 = a.xmap ? 0 : blockIdx.z * ROWS;
   // X slice (activations of the previous launch, L2-resident) and weight stream (packed
   // fragment blocks, 1 KB per wave instruction). X is requested first: staging waits only for X
   // (vmcnt retires in order) while the weights are still in flight.
@@ -616,16 +652,43 @@ __global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
       *(short8*)(xl + r * LD + k8) = vl[u];
     }
   } else {
+    // relu(k)^2 can exceed the f16 range (65504) on real checkpoints: in the f16 model each row
+    // of this K-slice is staged as relu^2 * 2^-e_r (e_r >= 0 the smallest power of two that
+    // brings the row's maximum under 2^15) and its partial product is scaled back by 2^e_r in
+    // the epilogue. Powers of two are exact, so rows in range (e_r = 0) are bit-unchanged.
+    float4_ y4[PERR];
 #pragma unroll
     for (int u = 0; u < PERR; ++u) {
       float4_ x = xr[0][u];
 #pragma unroll
       for (int p = 1; p < NX; ++p) x += xr[p][u];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) y4[u][e] = x[e] > 0.f ? x[e] * x[e] : 0.f;
+    }
+    if constexpr (F16) {
+      if (threadIdx.x < ROWS) s_rexp[threadIdx.x] = 0u;
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < PERR; ++u) {
+        const int r = (threadIdx.x + u * 256) / (KS / 4);
+        const float m = fmaxf(fmaxf(y4[u][0], y4[u][1]), fmaxf(y4[u][2], y4[u][3]));
+        if (m >= 32768.f) atomicMax(&s_rexp[r], as_u32(m));  // non-negative floats order as uints
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int u = 0; u < PERR; ++u) {
       const int c = threadIdx.x + u * 256;
       const int r = c / (KS / 4), k4 = (c % (KS / 4)) * 4;
-      float y[4];
+      float y[4] = {y4[u][0], y4[u][1], y4[u][2], y4[u][3]};
+      if constexpr (F16) {
+        const uint32_t mb = s_rexp[r];
+        if (mb) {  // 2^-(E - 14) for a row maximum in [2^E, 2^(E+1)), E >= 15; inf stays inf
+          const float sc = as_f32((uint32_t)(127 - (int)((mb >> 23) & 0xFF) + 127 + 14) << 23);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) y[e] = x[e] > 0.f ? x[e] * x[e] : 0.f;
+          for (int e = 0; e < 4; ++e) y[e] *= sc;
+        }
+      }
       uint32_t h0, l0, h1, l1;
       split2<F16>(y[0], y[1], h0, l0);
       split2<F16>(y[2], y[3], h1, l1);
@@ -667,7 +730,12 @@ __global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int row = row0 + m * 16 + 4 * g + j;
-        if (row < e_M) out[(int64_t)row * e_ldo] = acc_h[m][j] + acc_l[m][j];
+        float v = acc_h[m][j] + acc_l[m][j];
+        if constexpr (F16 && XMODE == kXRelu2) {
+          const uint32_t mb = s_rexp[m * 16 + 4 * g + j];
+          if (mb) v *= as_f32((uint32_t)((int)((mb >> 23) & 0xFF) - 127 - 14 + 127) << 23);  // 2^(E - 14)
+        }
+        if (row < e_M) out[(int64_t)row * e_ldo] = v;
       }
   }
   tl_end(a.tl);
@@ -922,7 +990,20 @@ static void launch_gemm_t(const GemmArgs& a, dim3 grid, hipStream_t st) {
   // generic fallback (other slab counts) and the debug-stamp build
   if ((a.xmode == kXPlanes || a.x_nsplit == 4 || a.x_nsplit == 2) && a.stamps == nullptr && a.exp == 0) {
     const int ms = a.nseg > 1 ? (a.n_tinfo > 0 ? 2 : 1) : 0;
-#define G2(F, XM, NX_, MS_) RT_LAUNCH((k_gemm2<MT, KSTEPS, XM, F, NX_, MS_>), grid, dim3(256), lds, st, a)
+    GemmArgs b = a;
+    b.xmap = 0;
+    static const bool no_xmap = getenv("RWKVTTS_NO_XMAP") != nullptr;  // A/B timing switch
+    if (grid.z == 1 && (a.k_split % 8 == 0 || 8 % a.k_split == 0) && !no_xmap) {
+      b.xmap = 1;
+      b.ntiles = (int)grid.x;
+      if (a.k_split >= 8) {
+        grid = dim3(grid.x * a.k_split);
+      } else {
+        b.tiles_per_xcd = (int)((grid.x * a.k_split + 7) / 8);
+        grid = dim3(8 * b.tiles_per_xcd);
+      }
+    }
+#define G2(F, XM, NX_, MS_) RT_LAUNCH((k_gemm2<MT, KSTEPS, XM, F, NX_, MS_>), grid, dim3(256), lds, st, b)
     if (a.f16) {
       if (a.xmode == kXPlanes) { if (ms == 2) G2(true, kXPlanes, 1, 2); else if (ms == 1) G2(true, kXPlanes, 1, 1); else G2(true, kXPlanes, 1, 0); }
       else if (a.x_nsplit == 4) G2(true, kXRelu2, 4, 0);
@@ -1298,12 +1379,18 @@ __global__ __launch_bounds__(128) void k_wkv4(WkvArgs a) {
   __shared__ __attribute__((aligned(16))) float s_vec[5][N];  // w, kk (unnormalised), a, k, r
   __shared__ float s_red[4][2];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, i = t >> 1, hf = t & 1;
-  const int h = blockIdx.y, C = a.C, c = h * N + i;
+  int seg_i = blockIdx.x, h = blockIdx.y;
+  if (a.xmap) {  // 1-D grid: head h's workgroups share one XCD (its LoRA-up rows stay in one L2)
+    const int b = blockIdx.x, xcd = b & 7, j = b >> 3;
+    h = xcd + 8 * (j / a.n_seg);
+    seg_i = j % a.n_seg;
+  }
+  const int C = a.C, c = h * N + i;
   tl_begin(a.tl);
   bf16_t* e_zhi = a.z_hi;
   bf16_t* e_zlo = a.z_lo;
   int e_ldz = a.ldz;
-  const int4 sg = a.segs[blockIdx.x];
+  const int4 sg = a.segs[seg_i];
   // ---- head-only loads: half of channel c's LoRA-up rows + parameters
   uint4 lw[18];  // 8 bf16 per entry: w 0..3 | a 4..7 | v 8..9 | g 10..17
   {  // packed per head by launch_pack_lora4: entry u of thread t at uint4 index u * 128 + t
@@ -1314,7 +1401,7 @@ __global__ __launch_bounds__(128) void k_wkv4(WkvArgs a) {
   const float w0 = a.w0[c], a0 = a.a0[c], v0 = a.v0[c], kkc = a.k_k[c], kac = a.k_a[c];
   const float rkc = a.r_k[c], lnw = a.lnx_w[c], lnb = a.lnx_b[c];
   // ---- segment-dependent loads, speculated for slot = row = segment index (decode layout)
-  const int spec = blockIdx.x < a.n_slots ? blockIdx.x : 0;
+  const int spec = seg_i < a.n_slots ? seg_i : 0;
   // state block layout (engine.hip perm_index): this thread's q-th float4 at index q * 128 + t
   const int64_t soff = a.layer_off + (int64_t)h * N * N + (int64_t)t * 4;
   float4_ S4[8];
@@ -1485,9 +1572,15 @@ __global__ __launch_bounds__(256) void k_wkv6(WkvArgs a) {
   __shared__ __attribute__((aligned(16))) float s_vec[5][N];  // w, kk (unnormalised), a, k, r
   __shared__ float s_red[4][4];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, i = t >> 2, qq = t & 3;
-  const int h = blockIdx.y, C = a.C, c = h * N + i;
+  int seg_i = blockIdx.x, h = blockIdx.y;
+  if (a.xmap) {  // 1-D grid: head h's workgroups share one XCD (its LoRA-up rows stay in one L2)
+    const int b = blockIdx.x, xcd = b & 7, j = b >> 3;
+    h = xcd + 8 * (j / a.n_seg);
+    seg_i = j % a.n_seg;
+  }
+  const int C = a.C, c = h * N + i;
   tl_begin(a.tl);
-  const int4 sg = a.segs[blockIdx.x];
+  const int4 sg = a.segs[seg_i];
   uint4 lw[9];  // 8 bf16 per entry: w 0..1 | a 2..3 | v 4 | g 5..8
   {
     const uint4* pl = (const uint4*)(a.lup + (int64_t)h * 9 * 256 * 8);
@@ -1496,7 +1589,7 @@ __global__ __launch_bounds__(256) void k_wkv6(WkvArgs a) {
   }
   const float w0 = a.w0[c], a0 = a.a0[c], v0 = a.v0[c], kkc = a.k_k[c], kac = a.k_a[c];
   const float rkc = a.r_k[c], lnw = a.lnx_w[c], lnb = a.lnx_b[c];
-  const int spec = blockIdx.x < a.n_slots ? blockIdx.x : 0;
+  const int spec = seg_i < a.n_slots ? seg_i : 0;
   const int64_t soff = a.layer_off + (int64_t)h * N * N + (int64_t)t * 4;
   float4_ S4[4];
   auto load_state = [&](int slot) {
@@ -1658,12 +1751,17 @@ int wkv_perm_layout(int Dw, int Da, int Dv, int Dg, int n_part, int max_slots, i
 int launch_wkv(const WkvArgs& a, int n_seg, int H, hipStream_t st) {
   const dim3 grid(n_seg, H);
   if (a.Dw == 64 && a.Da == 64 && a.Dv == 32 && a.Dg == 128 && a.n_part == 4 && (a.perm == 1 || a.perm == 2)) {
+    static const bool no_xmap = getenv("RWKVTTS_NO_XMAP") != nullptr;  // A/B timing switch
+    WkvArgs b = a;
+    b.xmap = (H % 8 == 0 && !no_xmap) ? 1 : 0;
+    b.n_seg = n_seg;
+    const dim3 g = b.xmap ? dim3(n_seg * H) : grid;
     if (a.perm == 2) {
-      if (a.f16) RT_LAUNCH((k_wkv6<true>), grid, dim3(256), 0, st, a);
-      else RT_LAUNCH((k_wkv6<false>), grid, dim3(256), 0, st, a);
+      if (a.f16) RT_LAUNCH((k_wkv6<true>), g, dim3(256), 0, st, b);
+      else RT_LAUNCH((k_wkv6<false>), g, dim3(256), 0, st, b);
     } else {
-      if (a.f16) RT_LAUNCH((k_wkv4<true>), grid, dim3(128), 0, st, a);
-      else RT_LAUNCH((k_wkv4<false>), grid, dim3(128), 0, st, a);
+      if (a.f16) RT_LAUNCH((k_wkv4<true>), g, dim3(128), 0, st, b);
+      else RT_LAUNCH((k_wkv4<false>), g, dim3(128), 0, st, b);
     }
     return n_seg * H;
   }

@@ -1,0 +1,47 @@
+"""fp16 models whose FFN activations leave the f16 range (relu(k)^2 > 65504, as real RWKV
+checkpoints do -- the reason ChatRWKV rescales in fp16). The GPU stages relu^2 as per-row
+power-of-two-scaled f16 planes (lm_kernels.hip k_gemm2 / k_gemm); the oracle computes in f32.
+Without the scaling the logits are inf / NaN."""
+import numpy as np
+import pytest
+
+import rwkvtts
+from rwkvtts import weights as W
+from helpers import PROPS, synth_text
+
+pytestmark = pytest.mark.gpu
+
+
+def _hot_ffn_blob(dims, layer, factor):
+    blob = W.synth_blob(dims, seed=31, dtype=rwkvtts._ffi.DTYPE_F16)
+    lay, _ = W.layout(dims)
+    for (l, t, off, r, c, m) in lay:
+        if l == layer and t == W.L_FFN_K:
+            a = blob[off:off + r * c * 2].view(np.float16)
+            a[:] = (a.astype(np.float32) * factor).astype(np.float16)
+    return blob
+
+
+@pytest.mark.parametrize("dims_name", ["mid", "tiny"])
+def test_f16_ffn_overflow_range(dims_name):
+    dims = {"mid": W.DIMS_MID, "tiny": W.DIMS_TINY}[dims_name]
+    blob = _hot_ffn_blob(dims, layer=0, factor=600.0)
+    import oracle
+    om = oracle.Model(blob)
+    rt = rwkvtts.SharedRwkvRuntime(blob, max_slots=4, token_chunk_size=64, use_graphs=False)
+    try:
+        toks = PROPS + [rwkvtts.TAG_2] + synth_text(3) + [rwkvtts.TAG_0]
+        st = om.new_state()
+        ref = [om.forward(st, t, 8193) for t in toks]
+        rt.reset_slot(0)
+        _, out = rt.infer(rwkvtts.RnnInput([rwkvtts.RnnInputBatch(list(toks), rwkvtts.RnnOption.Full)], 64),
+                          head_rows=8193)
+        got = out[0]
+        assert np.isfinite(got).all()
+        ref = np.stack(ref)
+        scale = max(1.0, float(np.abs(ref).max()))
+        assert np.abs(got - ref).max() < 2e-3 * scale, (np.abs(got - ref).max(), scale)
+        # the layer really produced out-of-range activations: some |k| > 256 (k^2 > 65504)
+        assert om is not None
+    finally:
+        rt.close()
