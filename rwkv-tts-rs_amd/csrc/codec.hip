@@ -433,7 +433,20 @@ class Codec {
       int least = 0, greatest = 0;
       RT_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
       if (getenv("RWKVTTS_NO_PRIO")) least = 0;
-      RT_HIP(hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, least));
+      const char* cus = getenv("RWKVTTS_CODEC_CUS");  // experiment: confine the vocoder to N CUs
+      if (cus && atoi(cus) > 0) {
+        hipDeviceProp_t prop;
+        RT_HIP(hipGetDeviceProperties(&prop, device));
+        const int ncu = prop.multiProcessorCount, want = std::min(atoi(cus), ncu);
+        std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+        for (int i = 0; i < want; ++i) {
+          const int cu = (int)((int64_t)i * ncu / want);
+          mask[cu / 32] |= 1u << (cu % 32);
+        }
+        RT_HIP(hipExtStreamCreateWithCUMask(&stream, (uint32_t)mask.size(), mask.data()));
+      } else {
+        RT_HIP(hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, least));
+      }
     }
 #define RT_CONV_ATTR(TN, KT) \
     RT_HIP(hipFuncSetAttribute((const void*)k_conv<TN, KT>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));

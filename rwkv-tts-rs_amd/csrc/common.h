@@ -95,6 +95,23 @@ __device__ inline void split2(float a, float b, uint32_t& hi, uint32_t& lo) {
 
 inline int64_t align_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
 
+// Write-through (sc1) vector stores: the line leaves the XCD's L2 at once instead of staying
+// dirty until the end-of-kernel write-back, which the NEXT launch waits for (MI355X_MICROARCH.md
+// price list, row boundary: + B / 6 TB/s for B dirty bytes). Buffer stores with cpol sc1.
+__device__ inline __amdgpu_buffer_rsrc_t wt_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ inline void store_wt(__amdgpu_buffer_rsrc_t r, int off_bytes, float4_ v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_, v), r, off_bytes, 0, 16);
+}
+__device__ inline void store_wt(__amdgpu_buffer_rsrc_t r, int off_bytes, uint2 v) {
+  typedef unsigned u32x2_ __attribute__((ext_vector_type(2)));
+  __builtin_amdgcn_raw_buffer_store_b64((u32x2_){v.x, v.y}, r, off_bytes, 0, 16);
+}
+__device__ inline void store_wt(__amdgpu_buffer_rsrc_t r, int off_bytes, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, off_bytes, 0, 16);
+}
+
 // Debug timeline (RWKVTTS_TIMELINE): start of the launch's first workgroup and end of its last
 // one in s_memrealtime ticks (100 MHz, one clock for every CU); ends are max-reduced over 64
 // slots to keep the atomics off one address. Slot layout per launch: [0] start, [2..65] ends.

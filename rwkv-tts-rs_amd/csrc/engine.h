@@ -97,6 +97,11 @@ class Engine {
   void state_permute(const float* std_block, float* dev_block);
   void state_unpermute(const float* dev_block, float* std_block);
   int state_perm_ = 0;  // WKV state block layout (wkv_perm_layout; engine.hip perm_index)
+  // XCD-aware grids per launch class: bit 0 rkv, 1 Wo, 2 ffn key, 3 ffn value, 4 head, 5 wkv
+  int xmap_mask_ = 0x28;  // measured (timeline A/B): value GEMM and WKV gain, rkv loses
+  // write-through (sc1) output stores per launch class, same bit order as xmap_mask_, plus
+  // bit 6 ln_att, bit 7 ln_ffn
+  int wt_mask_ = 0xFF;
   int device_ = 0;
   int f16_ = 0;  // fp16 matrices (else bf16): MFMA f16 and f16 activation planes
   hipStream_t stream_ = nullptr;

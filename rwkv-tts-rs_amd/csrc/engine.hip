@@ -91,6 +91,8 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
   RT_CHECK(splitA_ <= kMaxParts, RWKVTTS_EUNSUPPORTED, "n_embd too large for the WKV partial sum (raise kMaxParts)");
   state_perm_ = wkv_perm_layout(dims.d_decay, dims.d_aaa, dims.d_mv, dims.d_gate, splitA_, S_, desc.wkv_variant);
   if (const char* ex = getenv("RWKVTTS_DEBUG_EXP")) dbg_exp_ = atoi(ex);
+  if (const char* xm = getenv("RWKVTTS_XMAP_MASK")) xmap_mask_ = (int)strtol(xm, nullptr, 0);
+  if (const char* wm = getenv("RWKVTTS_WT_MASK")) wt_mask_ = (int)strtol(wm, nullptr, 0);
   if (const char* gp = getenv("RWKVTTS_GEMM_STAMPS")) {
     dbg_gstamp_path_ = gp;
     RT_OK(alloc(&dbg_gstamps_, 2 * 4096 * 4));
@@ -402,6 +404,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     m.rows = d_rows_;
     m.row_map = nullptr;
     m.inplace = inplace ? 1 : 0;
+    m.wt = (wt_mask_ >> 6) & 1;
     m.tl = tl_next("ln_att");
     prof_begin(&ev);
     if (!(dbg_exp_ & 0x10000)) launch_ln_mix(m, R, stream_);
@@ -425,6 +428,8 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     g.K = C; g.M = R; g.k_split = splitA_; g.kslice = C / splitA_;
     gemm_tile_table(g, RC);
     g.xmode = kXPlanes; g.out = partA_; g.split_stride = (int64_t)Rmax_ * ldA_; g.ldo = ldA_;
+    g.allow_xmap = xmap_mask_ & 1;
+    g.wt = wt_mask_ & 1;
     prof_begin(&ev);
     g.stamps = (l == 5 && dbg_gstamps_) ? dbg_gstamps_ : nullptr;
     g.exp = dbg_exp_ >> 8;
@@ -443,6 +448,8 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     k.v_first = vfirst_; k.ldv = C; k.z_hi = z_hi_; k.z_lo = z_lo_; k.ldz = C;
     k.segs = d_segs_; k.layer = l; k.C = C; k.n_slots = S_; k.n_seg = n_seg;
     k.perm = state_perm_;
+    k.allow_xmap = (xmap_mask_ >> 5) & 1;
+    k.wt = (wt_mask_ >> 5) & 1;
     k.Dw = dims.d_decay; k.Da = dims.d_aaa; k.Dv = dims.d_mv; k.Dg = dims.d_gate;
     k.stamps = (l == 5) ? dbg_stamps_ : nullptr;
     k.exp = dbg_exp_;
@@ -457,6 +464,8 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     go.seg[0] = {w.wo, z_hi_, z_lo_, C, C, 0, 0};
     go.K = C; go.M = R; go.k_split = splitO_; go.kslice = C / splitO_;
     go.xmode = kXPlanes; go.out = partO_; go.split_stride = RC; go.ldo = C;
+    go.allow_xmap = (xmap_mask_ >> 1) & 1;
+    go.wt = (wt_mask_ >> 1) & 1;
     prof_begin(&ev);
     go.exp = dbg_exp_ >> 8;
     go.tl = tl_next("gemm_wo");
@@ -475,6 +484,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     f.x_hi = xf_hi_;
     f.x_lo = xf_lo_;
     f.shift = ffn_sh_;
+    f.wt = (wt_mask_ >> 7) & 1;
     f.tl = tl_next("ln_ffn");
     prof_begin(&ev);
     if (!(dbg_exp_ & 0x10000)) launch_ln_mix(f, R, stream_);
@@ -485,6 +495,8 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     gk.seg[0] = {w.ffn_k, xf_hi_, xf_lo_, C, F, 0, 0};
     gk.K = C; gk.M = R; gk.k_split = splitK_; gk.kslice = C / splitK_;
     gk.xmode = kXPlanes; gk.out = partK_; gk.split_stride = (int64_t)Rmax_ * F; gk.ldo = F;
+    gk.allow_xmap = (xmap_mask_ >> 2) & 1;
+    gk.wt = (wt_mask_ >> 2) & 1;
     prof_begin(&ev);
     gk.exp = dbg_exp_ >> 8;
     gk.tl = tl_next("gemm_key");
@@ -498,6 +510,8 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     gv.xmode = kXRelu2; gv.x_part = partK_; gv.x_nsplit = splitK_; gv.x_ld = F;
     gv.x_part_stride = (int64_t)Rmax_ * F;
     gv.out = partF_; gv.split_stride = RC; gv.ldo = C;
+    gv.allow_xmap = (xmap_mask_ >> 3) & 1;
+    gv.wt = (wt_mask_ >> 3) & 1;
     prof_begin(&ev);
     gv.stamps = (l == 5 && dbg_gstamps_) ? dbg_gstamps_ + 4096 * 4 : nullptr;
     gv.exp = dbg_exp_ >> 8;
@@ -534,6 +548,8 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     gh.seg[0] = {head_, xo_hi_, xo_lo_, C, head_rows, 0, 0};
     gh.K = C; gh.M = n_lg; gh.k_split = splitH_; gh.kslice = C / splitH_;
     gh.xmode = kXPlanes; gh.out = logits_; gh.split_stride = (int64_t)Rmax_ * Vpad_; gh.ldo = Vpad_;
+    gh.allow_xmap = (xmap_mask_ >> 4) & 1;
+    gh.wt = (wt_mask_ >> 4) & 1;
     prof_begin(&ev);
     gh.exp = dbg_exp_ >> 8;
     gh.tl = tl_next("gemm_head");

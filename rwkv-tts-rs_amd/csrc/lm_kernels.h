@@ -35,6 +35,7 @@ struct LnMixArgs {
   int n_rows;          // set by the launcher
   int f16;             // planes in f16 (fp16 model) instead of bf16
   unsigned long long* tl;  // debug timeline slot (null in production)
+  int wt;              // k_ln1024: write-through (sc1) plane / residual / shift stores
   int inplace;         // decode step (one row per slot): the shift update overwrites the parity it
                        // read (same thread, read before write) and the parity is not flipped
 };
@@ -81,6 +82,8 @@ struct GemmArgs {
   // share one), so each XCD's L2 fetches its slices' activations once instead of all eight
   // fetching every slice. xmap 0: grid (tiles, k_split, row groups).
   int xmap;
+  int allow_xmap;      // set by the caller: this launch may use the XCD-aware grid
+  int wt;              // k_gemm2: write-through (sc1) output stores (common.h store_wt)
   int ntiles;          // column tiles
   int tiles_per_xcd;   // k_split < 8: tiles of one split per XCD (ceil(ntiles * k_split / 8))
   uint32_t tinfo[128];
@@ -108,6 +111,8 @@ struct WkvArgs {
   int n_seg;           // segments in this step 
   int perm;            // state block layout (wkv_perm_layout): 0 row-major, 1 k_wkv4, 2 k_wkv6
   int xmap;            // k_wkv4 / k_wkv6: 1-D grid, head h's workgroups on one XCD (H % 8 == 0)
+  int allow_xmap;      // set by the caller
+  int wt;              // k_wkv4 / k_wkv6: write-through (sc1) state stores
   int f16;             // fp16 model: LoRA-up rows and the z planes are f16
   uint64_t* stamps;    // debug: 8 s_memtime stamps per workgroup (null in production)
   int exp;             // debug experiment bits (0 in production)

@@ -320,7 +320,11 @@ __global__ __launch_bounds__(256) void k_ln1024(LnMixArgs a) {
   }
 #pragma unroll
   for (int p = 0; p < NP; ++p) v += t[p];
-  if (e_hout) *(float4_*)(e_hout + (int64_t)row * C + c) = v;
+  const bool wt = a.wt != 0;
+  if (e_hout) {
+    if (wt) store_wt(wt_rsrc(e_hout), (int)(((int64_t)row * C + c) * 4), v);
+    else *(float4_*)(e_hout + (int64_t)row * C + c) = v;
+  }
   auto ln = [&](float4_& x, int slot_base) {
     const float mean = block_sum_1b((x[0] + x[1]) + (x[2] + x[3]), red, slot_base) * (1.0f / C);
     const float4_ d = x - mean;
@@ -333,8 +337,13 @@ __global__ __launch_bounds__(256) void k_ln1024(LnMixArgs a) {
     uint32_t h0, l0, h1, l1;
     split2<F16>(x[0], x[1], h0, l0);
     split2<F16>(x[2], x[3], h1, l1);
-    *(uint2*)(hi + idx) = make_uint2(h0, h1);
-    *(uint2*)(lo + idx) = make_uint2(l0, l1);
+    if (wt) {
+      store_wt(wt_rsrc(hi), (int)(idx * 2), make_uint2(h0, h1));
+      store_wt(wt_rsrc(lo), (int)(idx * 2), make_uint2(l0, l1));
+    } else {
+      *(uint2*)(hi + idx) = make_uint2(h0, h1);
+      *(uint2*)(lo + idx) = make_uint2(l0, l1);
+    }
   };
   if constexpr (MODE == 0) {
     store(v, e_xhi, e_xlo, (int64_t)out_row * e_ldx + c);
@@ -353,8 +362,11 @@ __global__ __launch_bounds__(256) void k_ln1024(LnMixArgs a) {
       const float4_ x = v + (pv - v) * mu[m];
       store(x, e_xhi + m * e_mix, e_xlo + m * e_mix, (int64_t)out_row * e_ldx + c);
     }
-    if (flags & kRowLast)
-      *(float4_*)(e_shift + (((int64_t)(e_inpl ? par : par ^ 1) * e_S + slot) * e_L + e_layer) * C + c) = v;
+    if (flags & kRowLast) {
+      float* sp = e_shift + (((int64_t)(e_inpl ? par : par ^ 1) * e_S + slot) * e_L + e_layer) * C;
+      if (wt) store_wt(wt_rsrc(sp), c * 4, v);
+      else *(float4_*)(sp + c) = v;
+    }
   }
   tl_end(a.tl);
 }
@@ -723,19 +735,47 @@ __global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
   }
   // 5) store (D layout: col = lane&15, row = 4*(lane>>4) + j)
   const int col = col0 + li;
-  if (col < Nn) {
+  auto result = [&](int m, int j) {
+    float v = acc_h[m][j] + acc_l[m][j];
+    if constexpr (F16 && XMODE == kXRelu2) {
+      const uint32_t mb = s_rexp[m * 16 + 4 * g + j];
+      if (mb) v *= as_f32((uint32_t)((int)((mb >> 23) & 0xFF) - 127 - 14 + 127) << 23);  // 2^(E - 14)
+    }
+    return v;
+  };
+  if (a.wt) {
+    // write-through: the tile is staged in LDS so every lane stores whole 16-byte pieces (a
+    // 4-byte sc1 store is one fabric write each)
+    constexpr int LDT = 68;
+    float* st = (float*)smem;
+    __syncthreads();  // every wave is done reading its X fragments
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) st[(m * 16 + 4 * g + j) * LDT + wave * 16 + li] = result(m, j);
+    __syncthreads();
+    const int tcol = (tile - tstart) * 64;  // first column of this tile within the segment
+    const auto rs = wt_rsrc(e_out);
+#pragma unroll
+    for (int q = threadIdx.x; q < ROWS * 16; q += 256) {
+      const int r = q >> 4, c4 = (q & 15) * 4, row = row0 + r;
+      if (row >= e_M || tcol + c4 >= Nn) continue;
+      const int64_t o = (int64_t)split * e_sstride + col_off + tcol + c4 + (int64_t)row * e_ldo;
+      const float4_ v = *(const float4_*)(st + r * LDT + c4);
+      if (tcol + c4 + 4 <= Nn && (o & 3) == 0) {
+        store_wt(rs, (int)(o * 4), v);
+      } else {
+        for (int e = 0; e < 4 && tcol + c4 + e < Nn; ++e) store_wt(rs, (int)((o + e) * 4), v[e]);
+      }
+    }
+  } else if (col < Nn) {
     float* out = e_out + split * e_sstride + col_off + col;
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int row = row0 + m * 16 + 4 * g + j;
-        float v = acc_h[m][j] + acc_l[m][j];
-        if constexpr (F16 && XMODE == kXRelu2) {
-          const uint32_t mb = s_rexp[m * 16 + 4 * g + j];
-          if (mb) v *= as_f32((uint32_t)((int)((mb >> 23) & 0xFF) - 127 - 14 + 127) << 23);  // 2^(E - 14)
-        }
-        if (row < e_M) out[(int64_t)row * e_ldo] = v;
+        if (row < e_M) out[(int64_t)row * e_ldo] = result(m, j);
       }
   }
   tl_end(a.tl);
@@ -993,7 +1033,7 @@ static void launch_gemm_t(const GemmArgs& a, dim3 grid, hipStream_t st) {
     GemmArgs b = a;
     b.xmap = 0;
     static const bool no_xmap = getenv("RWKVTTS_NO_XMAP") != nullptr;  // A/B timing switch
-    if (grid.z == 1 && (a.k_split % 8 == 0 || 8 % a.k_split == 0) && !no_xmap) {
+    if (grid.z == 1 && a.allow_xmap && (a.k_split % 8 == 0 || 8 % a.k_split == 0) && !no_xmap) {
       b.xmap = 1;
       b.ntiles = (int)grid.x;
       if (a.k_split >= 8) {
@@ -1387,17 +1427,21 @@ __global__ __launch_bounds__(128) void k_wkv4(WkvArgs a) {
   }
   const int C = a.C, c = h * N + i;
   tl_begin(a.tl);
+  // debug phase stamps (RWKVTTS_WKV_STAMPS, layer 5 only; null in production): [0] realtime
+  // start, [1..6] core clock at phase ends, [7] realtime end
+  uint64_t* stp = (a.stamps && t == 0) ? a.stamps + ((int64_t)h * a.n_seg + seg_i) * 8 : nullptr;
+  if (stp) { stp[0] = __builtin_amdgcn_s_memrealtime(); stp[1] = __builtin_amdgcn_s_memtime(); }
   bf16_t* e_zhi = a.z_hi;
   bf16_t* e_zlo = a.z_lo;
   int e_ldz = a.ldz;
   const int4 sg = a.segs[seg_i];
-  // ---- head-only loads: half of channel c's LoRA-up rows + parameters
   uint4 lw[18];  // 8 bf16 per entry: w 0..3 | a 4..7 | v 8..9 | g 10..17
   {  // packed per head by launch_pack_lora4: entry u of thread t at uint4 index u * 128 + t
     const uint4* pl = (const uint4*)(a.lup + (int64_t)h * 18 * 128 * 8);
 #pragma unroll
     for (int u = 0; u < 18; ++u) lw[u] = pl[u * 128 + t];
   }
+  // ---- head-only loads: half of channel c's LoRA-up rows + parameters
   const float w0 = a.w0[c], a0 = a.a0[c], v0 = a.v0[c], kkc = a.k_k[c], kac = a.k_a[c];
   const float rkc = a.r_k[c], lnw = a.lnx_w[c], lnb = a.lnx_b[c];
   // ---- segment-dependent loads, speculated for slot = row = segment index (decode layout)
@@ -1410,7 +1454,6 @@ __global__ __launch_bounds__(128) void k_wkv4(WkvArgs a) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) S4[q] = Sp[q * 128];
   };
-  load_state(spec);
   const bool hid_thread = t < DALL / 4;
   float4_ hp[NP];
   float rp[NP], kp[NP], vp[NP], vf = 0.f;
@@ -1427,9 +1470,13 @@ __global__ __launch_bounds__(128) void k_wkv4(WkvArgs a) {
     vf = a.layer > 0 ? a.v_first[(int64_t)row * a.ldv + c] : 0.f;
   };
   load_parts(spec);
+  // the state goes out last (vmcnt retires in issue order): the LoRA / mixing phase starts
+  // while it is still in flight (measured: the LoRA-up rows first, then the partials, is best
+  // here; k_wkv6 prefers partials first)
+  load_state(spec);
   const int slot = sg.x, r_begin = sg.y, n_rows = sg.z;
-  if (slot != spec) load_state(slot);
   if (r_begin != spec) load_parts(r_begin);
+  if (slot != spec) load_state(slot);
   float4_* Srow = (float4_*)(a.state + (int64_t)slot * a.slot_stride + soff);
   for (int rr = 0; rr < n_rows; ++rr) {
     const int row = r_begin + rr;
@@ -1459,6 +1506,7 @@ __global__ __launch_bounds__(128) void k_wkv4(WkvArgs a) {
       v += vp[p];
     }
     __syncthreads();
+    if (stp && rr == 0) stp[2] = __builtin_amdgcn_s_memtime() + (uint64_t)(r != r);
     // ---- LoRA up on packed pairs: this thread's half of channel c's four dot products
     float2_ l0 = {0.f, 0.f}, l1 = {0.f, 0.f}, l2 = {0.f, 0.f}, l3 = {0.f, 0.f};
     auto dot = [&](float2_ acc, const uint4 q, const float* hsrc) {
@@ -1502,6 +1550,7 @@ __global__ __launch_bounds__(128) void k_wkv4(WkvArgs a) {
       s_vec[0][i] = w; s_vec[1][i] = kk; s_vec[2][i] = av; s_vec[3][i] = k; s_vec[4][i] = r;
     }
     __syncthreads();
+    if (stp && rr == 0) stp[3] = __builtin_amdgcn_s_memtime();
     const float inv = __builtin_amdgcn_rcpf(fmaxf(sqrtf(s_red[0][0] + s_red[0][1]), 1e-12f));
     const float bonus = s_red[1][0] + s_red[1][1];
     // ---- state half-row update on packed pairs: S = S*w - sa*(kk*inv*a) + v*k ; y = S.r
@@ -1534,9 +1583,16 @@ __global__ __launch_bounds__(128) void k_wkv4(WkvArgs a) {
         y2 += sv * (float2_){rq[e], rq[e + 1]};
       }
     }
+    if (stp && rr == 0) stp[4] = __builtin_amdgcn_s_memtime() + (uint64_t)(y2[0] != y2[0]);
     if (rr + 1 == n_rows) {  // the segment's final state: stored before the GroupNorm tail
+      if (a.wt) {
+        const auto rs = wt_rsrc(a.state + (int64_t)slot * a.slot_stride + a.layer_off + (int64_t)h * N * N);
 #pragma unroll
-      for (int q = 0; q < 8; ++q) Srow[q * 128] = S4[q];
+        for (int q = 0; q < 8; ++q) store_wt(rs, (q * 128 + t) * 16, S4[q]);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) Srow[q * 128] = S4[q];
+      }
     }
     float y = y2[0] + y2[1];
     y += dpp_mov<0xB1>(y);
@@ -1546,6 +1602,7 @@ __global__ __launch_bounds__(128) void k_wkv4(WkvArgs a) {
       if (lane == 0) { s_red[2][wave] = s1; s_red[3][wave] = s2; }
     }
     __syncthreads();
+    if (stp && rr == 0) stp[5] = __builtin_amdgcn_s_memtime();
     const float mean = (s_red[2][0] + s_red[2][1]) * (1.0f / N);
     const float var = fmaxf((s_red[3][0] + s_red[3][1]) * (1.0f / N) - mean * mean, 0.f);
     if (hf == 0) {
@@ -1554,6 +1611,7 @@ __global__ __launch_bounds__(128) void k_wkv4(WkvArgs a) {
     }
     if (rr + 1 < n_rows) __syncthreads();
   }
+  if (stp) { stp[6] = __builtin_amdgcn_s_memtime(); stp[7] = __builtin_amdgcn_s_memrealtime(); }
   tl_end(a.tl);
 }
 
@@ -1581,12 +1639,6 @@ __global__ __launch_bounds__(256) void k_wkv6(WkvArgs a) {
   const int C = a.C, c = h * N + i;
   tl_begin(a.tl);
   const int4 sg = a.segs[seg_i];
-  uint4 lw[9];  // 8 bf16 per entry: w 0..1 | a 2..3 | v 4 | g 5..8
-  {
-    const uint4* pl = (const uint4*)(a.lup + (int64_t)h * 9 * 256 * 8);
-#pragma unroll
-    for (int u = 0; u < 9; ++u) lw[u] = pl[u * 256 + t];
-  }
   const float w0 = a.w0[c], a0 = a.a0[c], v0 = a.v0[c], kkc = a.k_k[c], kac = a.k_a[c];
   const float rkc = a.r_k[c], lnw = a.lnx_w[c], lnb = a.lnx_b[c];
   const int spec = seg_i < a.n_slots ? seg_i : 0;
@@ -1597,7 +1649,6 @@ __global__ __launch_bounds__(256) void k_wkv6(WkvArgs a) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) S4[q] = Sp[q * 256];
   };
-  load_state(spec);
   const bool hid_thread = t < DALL / 4;
   float4_ hp[NP];
   float rp[NP], kp[NP], vp[NP], vf = 0.f;
@@ -1613,10 +1664,17 @@ __global__ __launch_bounds__(256) void k_wkv6(WkvArgs a) {
     }
     vf = a.layer > 0 ? a.v_first[(int64_t)row * a.ldv + c] : 0.f;
   };
+  // issue order = need order (vmcnt retires in order): partials (hidden nonlinearity), then the
+  // LoRA-up rows (LoRA / mixing phase), then the state (update phase)
+  uint4 lw[9];  // 8 bf16 per entry: w 0..1 | a 2..3 | v 4 | g 5..8
+  const uint4* pl = (const uint4*)(a.lup + (int64_t)h * 9 * 256 * 8);
   load_parts(spec);
+#pragma unroll
+  for (int u = 0; u < 9; ++u) lw[u] = pl[u * 256 + t];
+  load_state(spec);
   const int slot = sg.x, r_begin = sg.y, n_rows = sg.z;
-  if (slot != spec) load_state(slot);
   if (r_begin != spec) load_parts(r_begin);
+  if (slot != spec) load_state(slot);
   float4_* Srow = (float4_*)(a.state + (int64_t)slot * a.slot_stride + soff);
   auto quad_sum = [](float x) {
     x += dpp_mov<0xB1>(x);
@@ -1718,8 +1776,14 @@ __global__ __launch_bounds__(256) void k_wkv6(WkvArgs a) {
       }
     }
     if (rr + 1 == n_rows) {
+      if (a.wt) {
+        const auto rs = wt_rsrc(a.state + (int64_t)slot * a.slot_stride + a.layer_off + (int64_t)h * N * N);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) Srow[q * 256] = S4[q];
+        for (int q = 0; q < 4; ++q) store_wt(rs, (q * 256 + t) * 16, S4[q]);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Srow[q * 256] = S4[q];
+      }
     }
     const float y = quad_sum(y2[0] + y2[1]);
     {
@@ -1744,16 +1808,18 @@ int wkv_perm_layout(int Dw, int Da, int Dv, int Dg, int n_part, int max_slots, i
   if (!(Dw == 64 && Da == 64 && Dv == 32 && Dg == 128 && n_part == 4)) return 0;
   if (const char* e = getenv("RWKVTTS_WKV_LAYOUT")) variant = atoi(e);  // A/B timing override
   if (variant == 1 || variant == 2) return variant;
-  // auto, measured per decode step: k_wkv6 1 % faster at one slot (16 workgroups on an idle
-  // chip), k_wkv4 1 % faster at 32 slots (512 workgroups)
-  return max_slots <= 8 ? 2 : 1;
+  // auto: k_wkv6 (measured, timeline of a graph-replayed 32-slot step: 4.85 vs 5.33 us per
+  // launch once its loads are issued in need order and the XCD-aware grid keeps a head's
+  // LoRA-up rows in one L2; 1 % faster at one slot as well)
+  (void)max_slots;
+  return 2;
 }
 int launch_wkv(const WkvArgs& a, int n_seg, int H, hipStream_t st) {
   const dim3 grid(n_seg, H);
   if (a.Dw == 64 && a.Da == 64 && a.Dv == 32 && a.Dg == 128 && a.n_part == 4 && (a.perm == 1 || a.perm == 2)) {
     static const bool no_xmap = getenv("RWKVTTS_NO_XMAP") != nullptr;  // A/B timing switch
     WkvArgs b = a;
-    b.xmap = (H % 8 == 0 && !no_xmap) ? 1 : 0;
+    b.xmap = (H % 8 == 0 && a.allow_xmap && !no_xmap) ? 1 : 0;
     b.n_seg = n_seg;
     const dim3 g = b.xmap ? dim3(n_seg * H) : grid;
     if (a.perm == 2) {
