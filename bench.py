@@ -66,23 +66,26 @@ def pmc_traffic(kernel):
 
 
 def algorithmic_bytes(d, R, head_rows):
-    """Per-kernel algorithmic HBM bytes of one decode step with R rows."""
+    """Per-kernel algorithmic HBM bytes of one decode step with R rows, SURVEY §8d's model (not
+    this implementation's intermediates): weights read once, the recurrent state read and
+    written once (WKV state H*N*N f32 and the two token-shift vectors C f32 per row and layer),
+    plus the embedding rows and the logits of the head rows. Activation planes and split-K
+    partial slabs are implementation traffic: they appear in the PMC `traffic`, not here."""
     C, F, L = d["n_embd"], d["n_ffn"], d["n_layer"]
     H, N = C // 64, 64
     Dt = d["d_decay"] + d["d_aaa"] + d["d_mv"] + d["d_gate"]
-    act2 = 2 * 2  # bf16 hi + lo planes
     per = {
-        "gemm_rkv": 3 * C * C * 2 + 3 * R * C * act2 + 3 * R * C * 4,
-        "gemm_lora": Dt * C * 2 + 4 * R * C * act2 + R * Dt * 4,
-        "wkv": R * H * N * N * 4 * 2 + C * Dt * 2 + R * (3 * C + Dt) * 4 + R * C * act2,
-        "gemm_wo": C * C * 2 + R * C * act2 + R * C * 4,
-        "gemm_ffn_key": F * C * 2 + R * C * act2 + R * F * act2,
-        "gemm_ffn_value": C * F * 2 + R * F * act2 + R * C * 4,
-        "ln_mix_att": R * C * 4 * 2 + 6 * R * C * act2 + 2 * R * C * 4,
-        "ln_mix_ffn": R * C * 4 * 2 + R * C * act2 + 2 * R * C * 4,
+        "gemm_rkv_lora": (3 * C * C + Dt * C) * 2,
+        "wkv": R * H * N * N * 4 * 2 + C * Dt * 2,
+        "gemm_wo": C * C * 2,
+        "gemm_ffn_key": F * C * 2,
+        "gemm_ffn_value": C * F * 2,
+        "ln_mix_att": R * C * 4 * 2,
+        "ln_mix_ffn": R * C * 4 * 2,
     }
     per_step = {k: v * L for k, v in per.items()}
-    per_step["gemm_head"] = head_rows * C * 2 + R * C * act2 + R * head_rows * 4
+    per_step["gemm_head"] = head_rows * C * 2 + R * head_rows * 4
+    per_step["embed"] = R * C * 2
     return per, per_step
 
 

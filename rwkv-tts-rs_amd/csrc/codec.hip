@@ -327,20 +327,35 @@ __global__ __launch_bounds__(128) void k_dw_ln(const float* x, float* y, bf16_t*
   }
 }
 
-// final conv7 (C -> 1) over the snake-activated planes -> tanh; 128 samples per workgroup,
-// the input window staged in LDS as f32 (hi + lo) with row stride C + 1 (conflict-free walks).
-__global__ __launch_bounds__(128) void k_conv_out(const bf16_t* xh, const bf16_t* xl, int64_t x_bs, int C,
+// final conv7 (C -> 1) over the snake-activated planes -> tanh. 256 samples per workgroup of 256
+// threads: the input window (262 rows) is staged once into LDS as f32 (hi + lo) with 16-byte
+// global loads (8 channels per load and plane; C % 8 == 0) at row stride C + 1 (conflict-free
+// walks); each thread then walks its 7 x C window against the weights (scalar operands).
+constexpr int kOutT = 256;
+__global__ __launch_bounds__(256) void k_conv_out(const bf16_t* xh, const bf16_t* xl, int64_t x_bs, int C,
                                                   int tin_mul, const int* ntok, const float* w,
                                                   const float* b, float* pcm, int64_t p_bs) {
   extern __shared__ float s_x[];
-  const int req = blockIdx.y, T = ntok[req] * tin_mul, t0 = blockIdx.x * 128;
+  const int req = blockIdx.y, T = ntok[req] * tin_mul, t0 = blockIdx.x * kOutT;
   if (t0 >= T) return;
-  const int LDX = C + 1, rows = 128 + 6;
+  const int LDX = C + 1, rows = kOutT + 6, c8n = C / 8;
   const int64_t xo = req * x_bs;
-  for (int i = threadIdx.x; i < rows * C; i += 128) {
-    const int r = i / C, c = i % C, p = t0 - 3 + r;
-    const int64_t o = xo + (int64_t)p * C + c;
-    s_x[r * LDX + c] = (p >= 0 && p < T) ? bf16_to_f32(xh[o]) + bf16_to_f32(xl[o]) : 0.0f;
+  for (int i = threadIdx.x; i < rows * c8n; i += 256) {
+    const int r = i / c8n, c8 = (i - r * c8n) * 8, p = t0 - 3 + r;
+    float* dst = s_x + r * LDX + c8;
+    if (p >= 0 && p < T) {
+      const int64_t o = xo + (int64_t)p * C + c8;
+      const uint4 h = *(const uint4*)(xh + o), l = *(const uint4*)(xl + o);
+      const uint32_t hw[4] = {h.x, h.y, h.z, h.w}, lw[4] = {l.x, l.y, l.z, l.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        dst[2 * e] = as_f32(hw[e] << 16) + as_f32(lw[e] << 16);
+        dst[2 * e + 1] = as_f32(hw[e] & 0xFFFF0000u) + as_f32(lw[e] & 0xFFFF0000u);
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dst[e] = 0.0f;
+    }
   }
   __syncthreads();
   const int t = t0 + threadIdx.x;
@@ -454,6 +469,7 @@ class Codec {
     RT_CONV_ATTR(64, 1) RT_CONV_ATTR(64, 3) RT_CONV_ATTR(64, 7)
     RT_CONV_ATTR(96, 1)
 #undef RT_CONV_ATTR
+    RT_HIP(hipFuncSetAttribute((const void*)k_conv_out, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     // zero page: out-of-range window rows read zeros at channel offsets up to the largest Ci
     RT_HIP(hipMalloc(&zeros, 16384));
     RT_HIP(hipMemset(zeros, 0, 16384));
@@ -731,8 +747,8 @@ class Codec {
       }
     }
     pbeg();
-    const size_t shm = (size_t)(128 + 6) * (C + 1) * sizeof(float);
-    k_conv_out<<<dim3((unsigned)((Tmax * (int64_t)mul + 127) / 128), n), 128, shm, stream>>>(
+    const size_t shm = (size_t)(kOutT + 6) * (C + 1) * sizeof(float);
+    k_conv_out<<<dim3((unsigned)((Tmax * (int64_t)mul + kOutT - 1) / kOutT), n), 256, shm, stream>>>(
         pp[cur].h, pp[cur].l, bs, C, mul, d_ntok, F(0, 0, CD_COUT_W), F(0, 0, CD_COUT_B), pcm,
         (int64_t)Tmax * RWKVTTS_HOP);
     RT_HIP(hipGetLastError());

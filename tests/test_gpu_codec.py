@@ -74,3 +74,20 @@ def test_full_dims_raf_tokens_vs_oracle(oracle_mod):
         _check(c.decode_audio(g, sem), oracle_mod.codec_decode(codec.make_codec_dims(d), w, sem, g, threads=16))
     finally:
         c.close()
+
+
+def test_full_dims_batch_of_32_vs_oracle(oracle_mod):
+    """The bench's launch shape: 32 utterances in ONE batched decode at the full dims (ragged
+    lengths of a few frames each), every utterance against the oracle."""
+    d = codec.CODEC_DIMS_FULL
+    w = codec.synth_codec_blob(d)
+    c = codec.BiCodecDetokenizer(w, d)
+    rs = np.random.default_rng(32)
+    items = [(rs.integers(0, 4096, 32), rs.integers(0, 8192, 2 + (i % 5))) for i in range(32)]
+    try:
+        outs = c.decode_audio_batch(items)
+        cd = codec.make_codec_dims(d)
+        for (g, s), pcm in zip(items, outs):
+            _check(pcm, oracle_mod.codec_decode(cd, w, s, g, threads=16))
+    finally:
+        c.close()
