@@ -77,16 +77,16 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
   Rmax_ = (int)align_up(std::max(chunk_, S_), 64);
   use_graphs_ = desc.use_graphs != 0;
   // split-K so that every GEMM slice is 128/256/512 deep and the grids fill the 256 CUs
-  auto pick = [](int K, int want) {
-    int ks = std::min(want, K);
+  auto pick = [](int K, int want) {  // K slices of 128 / 256 / 512 (the GEMM kernels' shapes)
+    int ks = std::max(128, std::min(std::min(want, 512), K));
     while (ks > 128 && K % ks) ks >>= 1;
     return K / ks;
   };
   splitA_ = pick(C, 256);   // r,k,v,LoRA-down: 53 col tiles x 4
-  splitO_ = pick(C, 128);   // Wo: 16 col tiles x 8
+  splitO_ = pick(C, getenv("RWKVTTS_WO_KS") ? atoi(getenv("RWKVTTS_WO_KS")) : 128);   // Wo: 16 col tiles x 8
   splitK_ = pick(C, getenv("RWKVTTS_KEY_KS") ? atoi(getenv("RWKVTTS_KEY_KS")) : 256);  // ffn key: 64 col tiles x 4
   splitF_ = pick(F, 256);   // ffn value: 16 col tiles x 16
-  splitH_ = pick(C, 512);   // head: 129 col tiles x 2
+  splitH_ = pick(C, getenv("RWKVTTS_HEAD_KS") ? atoi(getenv("RWKVTTS_HEAD_KS")) : 512);   // head: 129 col tiles x 2
   RT_CHECK(C % 128 == 0 && F % 128 == 0, RWKVTTS_EUNSUPPORTED, "K dims must be multiples of 128");
   RT_CHECK(splitA_ <= kMaxParts, RWKVTTS_EUNSUPPORTED, "n_embd too large for the WKV partial sum (raise kMaxParts)");
   state_perm_ = wkv_perm_layout(dims.d_decay, dims.d_aaa, dims.d_mv, dims.d_gate, splitA_, S_, desc.wkv_variant);
