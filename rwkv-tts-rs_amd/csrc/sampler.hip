@@ -365,8 +365,14 @@ __device__ inline void sum_sim_elem(uint32_t b, int E, uint32_t& T0, uint32_t& T
 
 constexpr int kNoBinade = 1 << 20;  // sub_e of a sub-chunk whose simulation failed
 
-template <int NT>
-__device__ float exact_seq_sum(const SampleSmem& sm, int n, uint64_t* stamps = nullptr) {
+struct NoOther {
+  __device__ void operator()() const {}
+};
+
+// `other` runs on waves 1.. while wave 0 walks the chunk maps (the walk is serial; the other
+// waves would idle). It may not use workgroup barriers.
+template <int NT, typename Other = NoOther>
+__device__ float exact_seq_sum(const SampleSmem& sm, int n, uint64_t* stamps = nullptr, const Other& other = Other()) {
   constexpr int NS = NT / 64;  // sub-chunks per chunk (64 chunks, one per lane of wave 0)
   constexpr int NE = NT >= 1024 ? 64 : 128;  // serial-add register batch
   const int tid = threadIdx.x;
@@ -531,6 +537,8 @@ __device__ float exact_seq_sum(const SampleSmem& sm, int n, uint64_t* stamps = n
       sm.fred[16] = s;
       if (stamps) stamps[14] = nfast;
     }
+  } else {
+    other();
   }
   __syncthreads();
   STAMP(13);
@@ -559,6 +567,156 @@ __device__ inline uint64_t pkey(float p, int i) {
   return ((uint64_t)__builtin_bit_cast(uint32_t, p) << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)i);
 }
 
+constexpr int kFastK = 256;     // largest top-k of the fast path
+constexpr int kFastCap = 1024;  // candidate capacity (sm.keys[0, kFastCap)); ranked keys at 2048
+static_assert(kSampleMaxSorted >= 2048 + kFastCap, "fast-path key regions");
+
+// The fast path's candidates are exactly a superset of the top-k by (p desc, index asc):
+// at least k elements have e >= L, so the k-th largest p is >= P = RN(L / S) (division rounds
+// monotonically). An element left out has e < T = RN(L (1 - 2^-19)) < L (1 - 2^-20), so
+// e / S < (L / S)(1 - 2^-20) and, with L / S normal (ulp <= 2^-23 of it), RN(e / S) <= P - 8 ulp < P:
+// it can be neither in the top k nor tied with its last member.
+__device__ inline bool sample_fast_ok(float sum, float L, int nc, int top_k) {
+  if (!(sum > 0.0f) || !(L > 0.0f) || nc < top_k || nc > kFastCap) return false;
+  const float P = L / sum;
+  return P >= 0x1p-126f && P <= 1.0f;
+}
+
+__device__ inline float draw_r(const uint32_t* key, uint64_t draw, bool fixed42) {
+  if (!fixed42) return draw_f32(key, draw);
+  uint32_t k42[8];
+  uint64_t st = 42;
+  const uint64_t MUL = 6364136223846793005ull, INC = 11634580456473284103ull;
+  for (int i = 0; i < 8; ++i) {
+    st = st * MUL + INC;
+    const uint32_t xs = (uint32_t)(((st >> 18) ^ st) >> 27);
+    const uint32_t rot = (uint32_t)(st >> 59);
+    k42[i] = (xs >> rot) | (xs << ((32 - rot) & 31));
+  }
+  return draw_f32(k42, 0);
+}
+
+// Steps (2)-(6) of rwkv_sampler.rs:55-211 restricted to the candidates (temperature 1):
+// p = e / S for the nc candidates, top-k by rank, top-p over the k sorted survivors (:108-153,
+// cutoff, zeroing below it, the equal-to-cutoff adjustment with the index-order survivor sum),
+// multinomial over the survivors in index order (:174-207). Every other element has p = 0 after
+// top-k and adds exactly nothing to any sequential sum, so results equal the full path's.
+template <int NT>
+__device__ __attribute__((always_inline)) int sample_fast(const SampleSmem& sm, int nc, float sum, float top_p,
+                                                          int top_k, const uint32_t* key, uint64_t draw,
+                                                          bool fixed42, float* dbg, uint64_t* stamps) {
+  const int tid = threadIdx.x;
+  uint64_t* pk = sm.keys + 2048;
+  for (int c = tid; c < nc; c += NT) {
+    const uint64_t ce = sm.keys[c];
+    pk[c] = pkey(__builtin_bit_cast(float, (uint32_t)(ce >> 32)) / sum, (int)(uint32_t)ce);
+  }
+  __syncthreads();
+  STAMP(4);
+  // top-k: rank among the candidates (keys unique), the k best land sorted in keys[0, k)
+  for (int c = tid; c < nc; c += NT) {
+    const uint64_t kc = pk[c];
+    int rank = 0;
+    for (int j = 0; j < nc; ++j) rank += pk[j] > kc ? 1 : 0;
+    if (rank < top_k) sm.keys[rank] = kc;
+  }
+  __syncthreads();
+  STAMP(5);
+  // top-p over the sorted survivors (all p >= P > 0): wave 0, sequential cumulative
+  if (tid < 64) {
+    int m = top_k, found = 0, ceq = 0;
+    float cutoff = 0.0f;
+    if (top_p < 1.0f) {
+      float cum = 0.0f;
+      for (int q0 = 0; q0 < top_k && !found; q0 += 64) {
+        const bool in = q0 + tid < top_k;
+        const float pv = in ? __builtin_bit_cast(float, (uint32_t)(sm.keys[q0 + tid] >> 32)) : 0.0f;
+        float tot;
+        const float pre = prefix64(cum, pv, &tot);
+        const uint64_t hit = __ballot(in && pre >= top_p);
+        if (hit) {
+          found = 1;
+          cutoff = readlane_f(pv, __builtin_ctzll(hit));
+        }
+        cum = tot;
+      }
+      if (found) {  // survivors p >= cutoff: a prefix of the sorted order
+        m = 0;
+        for (int q0 = 0; q0 < top_k; q0 += 64) {
+          const bool in = q0 + tid < top_k;
+          const float pv = in ? __builtin_bit_cast(float, (uint32_t)(sm.keys[q0 + tid] >> 32)) : 0.0f;
+          m += __popcll(__ballot(in && pv >= cutoff));
+          ceq += __popcll(__ballot(in && pv == cutoff));
+        }
+      }
+    }
+    if (tid == 0) {
+      sm.ired[2] = found;
+      sm.ired[3] = ceq;
+      sm.ired[6] = m;
+      sm.fred[17] = cutoff;
+    }
+  }
+  __syncthreads();
+  const int m = sm.ired[6];
+  // survivors into index order: list[rank by index] = index, p at its index
+  for (int t = tid; t < m; t += NT) {
+    const uint64_t kt = sm.keys[t];
+    const uint32_t lt = (uint32_t)kt;  // ~index: larger means a smaller index
+    int r = 0;
+    for (int j = 0; j < m; ++j) r += (uint32_t)sm.keys[j] > lt ? 1 : 0;
+    const int it = (int)(0xFFFFFFFFu - lt);
+    sm.list[r] = it;
+    sm.p[it] = __builtin_bit_cast(float, (uint32_t)(kt >> 32));
+  }
+  __syncthreads();
+  STAMP(7);
+  if (tid < 64) {
+    const int found = sm.ired[2], ceq = sm.ired[3];
+    const float cutoff = sm.fred[17];
+    bool adj_on = false;
+    float adj = 0.0f;
+    if (top_p < 1.0f && found && top_p > 0.0f) {
+      float s2 = 0.0f;  // index-order sequential sum of the survivors (:129)
+      for (int q0 = 0; q0 < m; q0 += 64) {
+        const float v = q0 + tid < m ? sm.p[sm.list[q0 + tid]] : 0.0f;
+        const int cnt = min(64, m - q0);
+        for (int i = 0; i < cnt; ++i) s2 += readlane_f(v, i);
+      }
+      if (s2 < top_p && ceq > 0) {
+        adj = (top_p - s2) / (float)ceq;
+        adj_on = true;
+      }
+    }
+    const float r = draw_r(key, draw, fixed42);
+    int ret = -1;
+    if (r <= 0.0f) {
+      ret = 0;  // cum at index 0 is >= 0 >= r
+    } else {
+      float cum = 0.0f;
+      for (int q0 = 0; q0 < m && ret < 0; q0 += 64) {
+        const bool in = q0 + tid < m;
+        const int idx_l = in ? sm.list[q0 + tid] : 0;
+        float v = in ? sm.p[idx_l] : 0.0f;
+        if (adj_on && in && v == cutoff) v = cutoff + adj;
+        float tot;
+        const float pre = prefix64(cum, v, &tot);
+        const uint64_t hit = __ballot(in && r <= pre);
+        if (hit) ret = readlane_i(idx_l, __builtin_ctzll(hit));
+        cum = tot;
+      }
+      if (ret < 0) ret = sm.list[m - 1];  // highest index with p > 0 (:183-189)
+    }
+    if (tid == 0) {
+      sm.ired[5] = ret;
+      if (dbg) { dbg[0] = sum; dbg[1] = r; }
+    }
+  }
+  __syncthreads();
+  STAMP(9);
+  return sm.ired[5];
+}
+
 // The sampler. p holds the (masked) logits on entry. Returns the index in every thread.
 // status: 0 ok, RWKVTTS_EUNSUPPORTED for the documented limitation.
 template <int NT>
@@ -574,10 +732,72 @@ __device__ __attribute__((always_inline)) int sample_block(const SampleSmem& sm,
   for (int i = tid; i < n; i += NT) mx = fmaxf(mx, sm.p[i]);
   mx = block_max<NT>(mx, sm.fred);
   for (int i = tid; i < n; i += NT) sm.p[i] = glibc_expf(sm.p[i] - mx);
+  // Fast path (top-k <= kFastK, no temperature step): while wave 0 walks the exact sum, the
+  // other waves collect the top-k candidates on the unnormalised e = exp(l - max), so that after
+  // the sum only the candidates are divided, ranked and sampled. See sample_fast_ok below.
+  static_assert(NT <= 512, "fred[8 + wave] per candidate wave");
+  const bool want_fast = top_k > 0 && top_k < n && top_k <= kFastK && !(temperature != 1.0f && temperature > 0.0f);
+  if (tid == 0) {
+    sm.ired[30] = 0;  // sub-group arrival counter of the candidate waves
+    sm.ired[31] = 0;  // candidate count
+    sm.fred[20] = 0.0f;
+  }
   __syncthreads();
   STAMP(2);
-  const float sum = exact_seq_sum<NT>(sm, n, stamps);
+  auto collect = [&]() {
+    if (!want_fast) return;
+    constexpr int NC = NT - 64, NWC = NT / 64 - 1;
+    const int ct = tid - 64, lane = tid & 63;
+    // lower bound L of the k-th largest e: min over the NWC waves of the ceil(k/NWC)-th largest
+    // thread-local maximum (each wave holds that many disjoint elements >= L)
+    float lm = -1.0f;
+    for (int i = ct; i < n; i += NC) lm = fmaxf(lm, sm.p[i]);
+    const int kw = (top_k + NWC - 1) / NWC;
+    int gt = 0, ge = 0;
+#pragma unroll 16
+    for (int j = 0; j < 64; ++j) {
+      const float o = readlane_f(lm, j);
+      gt += o > lm ? 1 : 0;
+      ge += o >= lm ? 1 : 0;
+    }
+    const uint64_t selm = __ballot(gt < kw && kw <= ge);
+    const float vw = readlane_f(lm, __builtin_ctzll(selm));
+    if (lane == 0) {
+      sm.fred[8 + (tid >> 6)] = vw;
+      __hip_atomic_fetch_add(&sm.ired[30], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    // sub-group barrier of the candidate waves (wave 0 is busy in the walk; all waves of the
+    // workgroup are resident, so the spin terminates)
+    while (__hip_atomic_load(&sm.ired[30], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < NWC)
+      __builtin_amdgcn_s_sleep(1);
+    float L = sm.fred[9];
+#pragma unroll
+    for (int w = 2; w < NT / 64; ++w) L = fminf(L, sm.fred[8 + w]);
+    if (!(L > 0.0f)) return;  // no usable bound: the general path runs
+    if (tid == 64) sm.fred[20] = L;
+    // candidates: e >= T = L (1 - 2^-19) (see sample_fast_ok), appended as (e bits, index)
+    const float T = L * (1.0f - 0x1p-19f);
+    for (int i0 = 0; i0 < n; i0 += NC) {
+      const int i = i0 + ct;
+      const float v = i < n ? sm.p[i] : 0.0f;
+      const bool c = i < n && v >= T;
+      const uint64_t bm = __ballot(c);
+      if (bm) {
+        int base = 0;
+        if (lane == 0) base = atomicAdd(&sm.ired[31], __popcll(bm));
+        base = __builtin_amdgcn_readfirstlane(base);
+        const int off = base + __popcll(bm & ((1ull << lane) - 1ull));
+        if (c && off < kFastCap) sm.keys[off] = ((uint64_t)__builtin_bit_cast(uint32_t, v) << 32) | (uint32_t)i;
+      }
+    }
+  };
+  const float sum = exact_seq_sum<NT>(sm, n, stamps, collect);
   STAMP(3);
+  if (want_fast) {
+    const int nc = sm.ired[31];
+    const float L = sm.fred[20];
+    if (sample_fast_ok(sum, L, nc, top_k)) return sample_fast<NT>(sm, nc, sum, top_p, top_k, key, draw, fixed42, dbg, stamps);
+  }
   if (sum > 0.0f)
     for (int i = tid; i < n; i += NT) sm.p[i] = sm.p[i] / sum;
   __syncthreads();
@@ -786,18 +1006,7 @@ __device__ __attribute__((always_inline)) int sample_block(const SampleSmem& sm,
   STAMP(8);
   // (6) multinomial (:174-207): wave 0, cumulative in index order from lanes
   if (tid < 64) {
-    uint32_t k42[8];
-    if (fixed42) {
-      uint64_t st = 42;
-      const uint64_t MUL = 6364136223846793005ull, INC = 11634580456473284103ull;
-      for (int i = 0; i < 8; ++i) {
-        st = st * MUL + INC;
-        const uint32_t xs = (uint32_t)(((st >> 18) ^ st) >> 27);
-        const uint32_t rot = (uint32_t)(st >> 59);
-        k42[i] = (xs >> rot) | (xs << ((32 - rot) & 31));
-      }
-    }
-    const float r = fixed42 ? draw_f32(k42, 0) : draw_f32(key, draw);
+    const float r = draw_r(key, draw, fixed42);
     int ret = -1;
     if (r <= sm.p[0]) {
       ret = 0;

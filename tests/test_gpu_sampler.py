@@ -44,6 +44,13 @@ CASES = [  # (n, temperature, top_p, top_k)
     (3000, 1.0, 0.3, 0),
     (16384, 1.0, 1.0, 0),     # plain multinomial over a long row
     (77923 // 8, 1.0, 0.9, 64),
+    # candidate fast path (top-k <= 256, T = 1) edges and its fallbacks
+    (8193, 1.0, 0.0, 80),     # top_p <= 0: survivors are the ties of the maximum
+    (8193, 1.0, -1.0, 7),
+    (4096, 1.0, 0.02, 256),   # largest fast k
+    (4096, 1.0, 0.95, 257),   # first k past the fast path
+    (300, 1.0, 0.95, 299),    # k = n - 1
+    (17, 1.0, 0.9, 3),        # fewer elements than candidate threads
 ]
 
 
