@@ -209,7 +209,9 @@ typedef struct {
 
 /* Samples n_rows rows of `logits` (host, n_rows x row_len f32) on the GPU; rng[i] == NULL
  * mirrors `rng: &mut None` (fixed StdRng(42) draw). rngs advance by one draw per row.
- * row_len <= 16384 (or top_k in [1, 16384]). out_tokens receives the index per row. */
+ * Any row_len up to 2^24 and every (temperature, top_p, top_k) of the reference is accepted:
+ * rows up to 16384 run in LDS, longer rows (the 77,923-token vocabulary) in a device scratch.
+ * out_tokens receives the index per row. */
 int rwkvtts_sample(rwkvtts_engine* e, const float* logits, int n_rows, int row_len,
                    const rwkvtts_sample_args* args, rwkvtts_rng* const* rngs, int32_t* out_tokens);
 

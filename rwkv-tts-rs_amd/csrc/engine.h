@@ -156,7 +156,10 @@ class Engine {
   SlotCtrl* h_ctrl_ = nullptr;  // pinned mirror
   // sampler API scratch
   float* d_samp_logits_ = nullptr;
-  int samp_cap_ = 0;
+  size_t samp_cap_ = 0;     // logits elements
+  int samp_rows_cap_ = 0;   // rows of d_keys_ / d_draws_ / d_out_
+  void* d_wide_ = nullptr;  // rows longer than kSampleMaxN: per-row p / keys / list scratch
+  size_t wide_cap_ = 0;
   uint32_t* d_keys_ = nullptr;
   uint64_t* d_draws_ = nullptr;
   int32_t* d_out_ = nullptr;

@@ -28,6 +28,8 @@ Engine::~Engine() {
   for (auto& g : graphs_) hipGraphExecDestroy(g.second);
   for (auto& e : pending_prof_) hipEventDestroy(e.second);
   for (void* p : allocs_) hipFree(p);
+  for (void* p : {(void*)d_samp_logits_, (void*)d_keys_, (void*)d_draws_, (void*)d_out_, d_wide_})
+    if (p) hipFree(p);
   if (h_ctrl_) hipHostFree(h_ctrl_);
   if (stream_) hipStreamDestroy(stream_);
 }
@@ -686,19 +688,27 @@ int Engine::infer(const rwkvtts_input* in, int n, int head_rows, float* logits, 
 int Engine::sample(const float* logits, int n_rows, int row_len, const rwkvtts_sample_args* args,
                    rwkvtts_rng* const* rngs, int32_t* out, float* dbg_host) {
   RT_HIP(hipSetDevice(device_));
-  RT_CHECK(n_rows > 0 && row_len >= 0 && row_len <= kSampleMaxN, RWKVTTS_EINVAL,
-           "sample: row_len must be <= 16384");
+  RT_CHECK(n_rows > 0 && row_len >= 0 && row_len <= kSampleMaxRowLen, RWKVTTS_EINVAL,
+           "sample: row_len must be <= 2^24");
   const size_t need = (size_t)n_rows * std::max(row_len, 1);
-  if ((int)need > samp_cap_) {
+  if (need > samp_cap_) {
     if (d_samp_logits_) hipFree(d_samp_logits_);
-    if (d_keys_) hipFree(d_keys_);
-    if (d_draws_) hipFree(d_draws_);
-    if (d_out_) hipFree(d_out_);
+    d_samp_logits_ = nullptr;
+    samp_cap_ = 0;
     RT_HIP(hipMalloc(&d_samp_logits_, need * 4));
+    samp_cap_ = need;
+  }
+  if (n_rows > samp_rows_cap_) {
+    for (void* p : {(void*)d_keys_, (void*)d_draws_, (void*)d_out_})
+      if (p) hipFree(p);
+    d_keys_ = nullptr;
+    d_draws_ = nullptr;
+    d_out_ = nullptr;
+    samp_rows_cap_ = 0;
     RT_HIP(hipMalloc(&d_keys_, (size_t)n_rows * 32 + 256));
     RT_HIP(hipMalloc(&d_draws_, (size_t)n_rows * 8 + 256));
     RT_HIP(hipMalloc(&d_out_, (size_t)n_rows * 4 + 256));
-    samp_cap_ = (int)need;
+    samp_rows_cap_ = n_rows;
   }
   std::vector<uint32_t> keys((size_t)n_rows * 8, 0);
   std::vector<uint64_t> draws(n_rows, 0);
@@ -727,6 +737,18 @@ int Engine::sample(const float* logits, int n_rows, int row_len, const rwkvtts_s
   a.keys = all_null ? nullptr : d_keys_;
   a.draws = all_null ? nullptr : d_draws_;
   a.out = d_out_;
+  if (row_len > kSampleMaxN) {  // long rows: per-row global scratch for p, sort keys and list
+    const size_t stride = wide_scratch_bytes(row_len), bytes = stride * (size_t)n_rows;
+    if (bytes > wide_cap_) {
+      if (d_wide_) hipFree(d_wide_);
+      d_wide_ = nullptr;
+      wide_cap_ = 0;
+      RT_HIP(hipMalloc(&d_wide_, bytes));
+      wide_cap_ = bytes;
+    }
+    a.scratch = (char*)d_wide_;
+    a.scratch_stride = stride;
+  }
   a.dbg = nullptr;
   float* d_dbg = nullptr;
   if (dbg_host) {
@@ -745,7 +767,7 @@ int Engine::sample(const float* logits, int n_rows, int row_len, const rwkvtts_s
   RT_HIP(hipMemcpyAsync(out, d_out_, (size_t)n_rows * 4, hipMemcpyDeviceToHost, stream_));
   RT_HIP(hipStreamSynchronize(stream_));
   for (int i = 0; i < n_rows; ++i) {
-    RT_CHECK(out[i] >= 0, out[i], "sample: top-p over more than 4096 candidates is unsupported");
+    RT_CHECK(out[i] >= 0, out[i], "sample: device sampler failed");
     if (rngs && rngs[i]) rngs[i]->draw_index++;
   }
   return RWKVTTS_OK;

@@ -5,8 +5,9 @@
 
 namespace rwkvtts {
 
-constexpr int kSampleMaxN = 16384;       // row length held in LDS
-constexpr int kSampleMaxSorted = 4096;   // survivors sortable for top-p
+constexpr int kSampleMaxN = 16384;       // row length held in LDS (longer rows: global scratch)
+constexpr int kSampleMaxSorted = 4096;   // survivors sortable for top-p in LDS
+constexpr int kSampleMaxRowLen = 1 << 24;  // generic sampler API row limit
 
 enum SlotPhase : int32_t { kPhGlobal = 0, kPhGFeed = 1, kPhSemantic = 2, kPhDone = 3 };
 
@@ -45,6 +46,8 @@ struct SampleRowArgs {
   int32_t* out;             // [rows]
   float* dbg;               // optional [rows][2]: softmax sum, r
   uint64_t* stamps;         // optional [rows][16]: s_memtime at phase boundaries (diagnostics)
+  char* scratch;            // n > kSampleMaxN: [rows][scratch_stride] bytes (wide_scratch_bytes(n))
+  size_t scratch_stride;
 };
 
 struct AdvanceArgs {
@@ -59,6 +62,7 @@ struct AdvanceArgs {
   unsigned long long* tl;  // debug timeline slot (null in production)
 };
 
+size_t wide_scratch_bytes(int n);
 void launch_sample_rows(const SampleRowArgs& a, int rows, hipStream_t st);
 int launch_advance(const AdvanceArgs& a, hipStream_t st);
 

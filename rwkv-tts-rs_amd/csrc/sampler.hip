@@ -12,8 +12,10 @@
 //    order-independent and runs block-parallel;
 //  * stable descending sort == sort on the key (p bits, ~index).
 //  * rand 0.8 StdRng draw k == ChaCha12(key, block k/16)[k%16]; f32 = (u32 >> 8) * 2^-24.
-// Limitation (generic API only): top-p over more than 4096 positive probabilities (top_k == 0
-// or > 4096) is rejected; temperature != 1 uses a double-precision powf (not glibc's).
+// Rows up to kSampleMaxN run with the row in LDS; longer rows (the full 77,923-token vocabulary)
+// run the same code with the row, sort keys and index list in a global scratch (k_sample_rows_wide),
+// so every top-k / top-p combination of the reference is accepted. temperature != 1 uses a
+// double-precision powf (not glibc's).
 #include "sampler.h"
 #include "exact_math.h"
 
@@ -200,8 +202,8 @@ __device__ inline float prefix64(float s, float v, float* total) {
 // fred[0..NW) / ired[8..8+2 NW): block reductions; fred[16..20) / ired[0..8): named results.
 struct SampleSmem {
   float* p;           // [n] logits -> e -> probabilities
-  uint64_t* keys;     // [kSampleMaxSorted] sort keys (p bits << 32 | ~index)
-  int* list;          // [kSampleMaxSorted] positive indices in index order
+  uint64_t* keys;     // [cap rounded up to a power of two] sort keys (p bits << 32 | ~index)
+  int* list;          // [cap] positive indices in index order
   int* scan;          // [8] block-scan wave totals
   double* dscan;      // [8]
   uint32_t* sub_t;    // [NT][2] sub-chunk parity maps of the exact-sum emulation
@@ -211,6 +213,7 @@ struct SampleSmem {
   int* chunk_ok;      // [64]
   float* fred;        // [32]
   int* ired;          // [48]
+  int cap;            // keys / list capacity (kSampleMaxSorted in LDS, the row length in scratch)
 };
 
 __device__ inline int wave_sum_i(int v) {
@@ -293,7 +296,7 @@ __device__ int compact_positive(const SampleSmem& sm, int n) {
   int off = block_excl_scan<NT>(cnt, sm.scan, &tot);
   for (int i = b; i < e; ++i)
     if (sm.p[i] > 0.0f) {
-      if (off < kSampleMaxSorted) sm.list[off] = i;
+      if (off < sm.cap) sm.list[off] = i;
       ++off;
     }
   __syncthreads();
@@ -305,7 +308,7 @@ __device__ int compact_positive(const SampleSmem& sm, int n) {
 __device__ float wave_sum_positive(const SampleSmem& sm, int n, int npos) {
   const int lane = threadIdx.x & 63;
   float s = 0.0f;
-  if (npos <= kSampleMaxSorted) {
+  if (npos <= sm.cap) {
     for (int q0 = 0; q0 < npos; q0 += 64) {
       const float v = (q0 + lane < npos) ? sm.p[sm.list[q0 + lane]] : 0.0f;
       const int cnt = min(64, npos - q0);
@@ -837,7 +840,7 @@ __device__ __attribute__((always_inline)) int sample_block(const SampleSmem& sm,
       for (int i = b; i < e; ++i) cnt += sm.p[i] >= L;
       int tot;
       int off = block_excl_scan<NT>(cnt, sm.scan, &tot);
-      if (tot <= kSampleMaxSorted) {
+      if (tot <= sm.cap) {
         for (int i = b; i < e; ++i)
           if (sm.p[i] >= L) sm.keys[off++] = pkey(sm.p[i], i);
         if (tot <= NT) {
@@ -915,7 +918,7 @@ __device__ __attribute__((always_inline)) int sample_block(const SampleSmem& sm,
   if (top_p < 1.0f) {
     if (n_sorted < 0 || n_sorted > npos) {
       // survivors not yet sorted (or fewer positives than k): sort the positive ones
-      if (npos > kSampleMaxSorted) {
+      if (npos > sm.cap) {
         *status = RWKVTTS_EUNSUPPORTED;
         return 0;
       }
@@ -1011,7 +1014,7 @@ __device__ __attribute__((always_inline)) int sample_block(const SampleSmem& sm,
     if (r <= sm.p[0]) {
       ret = 0;
     } else {
-      const bool listed = npos <= kSampleMaxSorted;
+      const bool listed = npos <= sm.cap;
       const int cnt_all = listed ? npos : n;
       float cum = 0.0f;
       int last_pos = -1;
@@ -1041,14 +1044,15 @@ __device__ __attribute__((always_inline)) int sample_block(const SampleSmem& sm,
 }
 
 template <int NT>
-__device__ SampleSmem carve(char* base, int n) {
+__device__ SampleSmem carve(char* base, int n, bool sorted_in_lds = true) {
   SampleSmem sm;
   const int npad = (n + 3) & ~3;
+  const int ns = sorted_in_lds ? kSampleMaxSorted : 0;
   char* q = base;
   sm.p = (float*)q; q += (size_t)npad * 4;
-  sm.keys = (uint64_t*)q; q += kSampleMaxSorted * 8;
+  sm.keys = (uint64_t*)q; q += (size_t)ns * 8;
   sm.dscan = (double*)q; q += 16 * 8;
-  sm.list = (int*)q; q += kSampleMaxSorted * 4;
+  sm.list = (int*)q; q += (size_t)ns * 4;
   sm.scan = (int*)q; q += 16 * 4;
   sm.sub_t = (uint32_t*)q; q += 2 * NT * 4;
   sm.sub_e = (int*)q; q += NT * 4;
@@ -1057,6 +1061,7 @@ __device__ SampleSmem carve(char* base, int n) {
   sm.chunk_ok = (int*)q; q += 64 * 4;
   sm.fred = (float*)q; q += 32 * 4;
   sm.ired = (int*)q;
+  sm.cap = kSampleMaxSorted;
   return sm;
 }
 template <int NT>
@@ -1086,7 +1091,51 @@ __global__ __launch_bounds__(kSampleThreads) void k_sample_rows(SampleRowArgs a)
   if (threadIdx.x == 0) a.out[row] = status ? status : id;
 }
 
+// Rows longer than kSampleMaxN: the row (p), its sort keys and index list live in a per-row
+// global scratch region (wide_scratch_bytes), the small scan / reduction arrays in LDS. All of
+// the row's accesses stay inside its own workgroup, whose barriers order them.
+__host__ __device__ inline int wide_keys_len(int n) {
+  int m = 1;
+  while (m < n) m <<= 1;
+  return m;
+}
+size_t wide_scratch_bytes(int n) {
+  const size_t npad = (size_t)((n + 3) & ~3);
+  return (npad * 4 + (size_t)wide_keys_len(n) * 8 + (size_t)n * 4 + 255) & ~(size_t)255;
+}
+
+__global__ __launch_bounds__(kSampleThreads) void k_sample_rows_wide(SampleRowArgs a) {
+  constexpr int NT = kSampleThreads;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int row = blockIdx.x;
+  char* g = a.scratch + (size_t)row * a.scratch_stride;
+  // small arrays in LDS (carve with n = 0 and no keys / list), the row's arrays in scratch
+  SampleSmem sm = carve<NT>(smem, 0, false);
+  sm.p = (float*)g;
+  sm.keys = (uint64_t*)(g + (size_t)((a.n + 3) & ~3) * 4);
+  sm.list = (int*)((char*)sm.keys + (size_t)wide_keys_len(a.n) * 8);
+  sm.cap = a.n;
+  uint64_t* stamps = a.stamps ? a.stamps + row * 16 : nullptr;
+  STAMP(0);
+  const float* lg = a.logits + (int64_t)row * a.ld;
+  for (int i = threadIdx.x; i < a.n; i += NT) sm.p[i] = lg[i];
+  __syncthreads();
+  if (threadIdx.x == 0 && a.forbid >= 0 && a.forbid < a.n) sm.p[a.forbid] = -__builtin_inff();
+  __syncthreads();
+  int status;
+  const int id = sample_block<NT>(sm, a.n, a.temperature, a.top_p, a.top_k,
+                              a.keys ? a.keys + row * 8 : nullptr, a.draws ? a.draws[row] : 0,
+                              a.keys == nullptr, a.dbg ? a.dbg + row * 2 : nullptr, &status, stamps);
+  if (threadIdx.x == 0) a.out[row] = status ? status : id;
+}
+
 void launch_sample_rows(const SampleRowArgs& a, int rows, hipStream_t st) {
+  if (a.n > kSampleMaxN) {
+    // the LDS carve of k_sample_rows_wide holds no row, keys or list
+    const size_t lds = smem_bytes<kSampleThreads>(0) - kSampleMaxSorted * 12;
+    RT_LAUNCH(k_sample_rows_wide, dim3(rows), dim3(kSampleThreads), lds, st, a);
+    return;
+  }
   RT_LAUNCH(k_sample_rows, dim3(rows), dim3(kSampleThreads), smem_bytes<kSampleThreads>(a.n), st, a);
 }
 

@@ -76,6 +76,22 @@ def test_sampler_masked_full_vocab_equivalence(rt, oracle_mod):
     assert dev.tolist() == ref
 
 
+@pytest.mark.parametrize("kind", ["normal", "ties"])
+@pytest.mark.parametrize("case", [(77923, 1.0, 0.85, 0),     # SamplerArgs::default on the full vocabulary
+                                  (77923, 1.0, 0.95, 80),
+                                  (20000, 1.0, 0.3, 5000),   # top-k past the LDS candidate path
+                                  (77923, 1.0, 1.0, 0)])
+def test_sampler_full_vocab_rows(rt, oracle_mod, kind, case):
+    """Rows longer than the LDS row (16384) run from a device scratch: bit-exact for every
+    top-k / top-p combination, including top-p without top-k over ~10^4 positive candidates."""
+    n, T, p, k = case
+    rows = _rows(kind, n, 4, seed=n + k)
+    seeds = [77 + i for i in range(len(rows))]
+    dev = rt.sample(rows, T, p, k, None, [rwkvtts.StdRng.seed_from_u64(s) for s in seeds])
+    ref = [oracle_mod.sample(rows[i], T, p, k, None, oracle_mod.Rng(seeds[i])) for i in range(len(rows))]
+    assert dev.tolist() == ref
+
+
 def test_sampler_rng_stream_advances(rt, oracle_mod):
     rows = _rows("normal", 4096, 1, seed=11)[0]
     dr = rwkvtts.StdRng.seed_from_u64(1042)
