@@ -95,6 +95,7 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
   if (const char* ex = getenv("RWKVTTS_DEBUG_EXP")) dbg_exp_ = atoi(ex);
   if (const char* xm = getenv("RWKVTTS_XMAP_MASK")) xmap_mask_ = (int)strtol(xm, nullptr, 0);
   if (const char* wm = getenv("RWKVTTS_WT_MASK")) wt_mask_ = (int)strtol(wm, nullptr, 0);
+  if (const char* xa = getenv("RWKVTTS_XALIGN_MASK")) xalign_mask_ = (int)strtol(xa, nullptr, 0);
   if (const char* gp = getenv("RWKVTTS_GEMM_STAMPS")) {
     dbg_gstamp_path_ = gp;
     RT_OK(alloc(&dbg_gstamps_, 2 * 4096 * 4));
@@ -431,6 +432,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     gemm_tile_table(g, RC);
     g.xmode = kXPlanes; g.out = partA_; g.split_stride = (int64_t)Rmax_ * ldA_; g.ldo = ldA_;
     g.allow_xmap = xmap_mask_ & 1;
+    g.xalign = (xalign_mask_ & 1) ? 1 : 0;  // r / k / v tile h (head h) on the XCD of WKV head h
     g.wt = wt_mask_ & 1;
     prof_begin(&ev);
     g.stamps = (l == 5 && dbg_gstamps_) ? dbg_gstamps_ : nullptr;
@@ -498,6 +500,8 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     gk.K = C; gk.M = R; gk.k_split = splitK_; gk.kslice = C / splitK_;
     gk.xmode = kXPlanes; gk.out = partK_; gk.split_stride = (int64_t)Rmax_ * F; gk.ldo = F;
     gk.allow_xmap = (xmap_mask_ >> 2) & 1;
+    // key tiles of value K-slice s on the XCD that runs slice s (value xmap: split = xcd + 8 j)
+    if ((xalign_mask_ >> 2) & 1) gk.xalign = std::max(1, (F / splitF_) / 64);
     gk.wt = (wt_mask_ >> 2) & 1;
     prof_begin(&ev);
     gk.exp = dbg_exp_ >> 8;

@@ -86,6 +86,10 @@ struct GemmArgs {
   int wt;              // k_gemm2: write-through (sc1) output stores (common.h store_wt)
   int ntiles;          // column tiles
   int tiles_per_xcd;   // k_split < 8: tiles of one split per XCD (ceil(ntiles * k_split / 8))
+  // xmap 2 (consumer-aligned): every split of column tile t runs on XCD (t / xalign) % 8, the
+  // XCD whose workgroups consume those columns next (the value GEMM's K-slice, the WKV head), so
+  // the consumer reads the partial slabs from its own L2. Set xalign > 0 to request it.
+  int xalign;
   uint32_t tinfo[128];
 };
 

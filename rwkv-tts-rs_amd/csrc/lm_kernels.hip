@@ -566,7 +566,13 @@ __global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
   int64_t e_sstride = a.split_stride;
   int e_ldo = a.ldo, e_M = a.M;
   int tile = blockIdx.x, split = blockIdx.y;
-  if (a.xmap) {  // XCD-aware 1-D grid (GemmArgs::xmap)
+  if (a.xmap == 2) {  // consumer-aligned 1-D grid (GemmArgs::xalign)
+    const int b = blockIdx.x, xcd = b & 7, j = b >> 3;
+    split = j % a.k_split;
+    const int lt = j / a.k_split;
+    tile = (xcd + 8 * (lt / a.xalign)) * a.xalign + lt % a.xalign;
+    if (tile >= a.ntiles) return;  // padding workgroup
+  } else if (a.xmap) {  // XCD-aware 1-D grid (GemmArgs::xmap)
     const int b = blockIdx.x, xcd = b & 7, j = b >> 3;
     if (a.k_split >= 8) {
       split = xcd + 8 * (j / a.ntiles);
@@ -1033,7 +1039,12 @@ static void launch_gemm_t(const GemmArgs& a, dim3 grid, hipStream_t st) {
     GemmArgs b = a;
     b.xmap = 0;
     static const bool no_xmap = getenv("RWKVTTS_NO_XMAP") != nullptr;  // A/B timing switch
-    if (grid.z == 1 && a.allow_xmap && (a.k_split % 8 == 0 || 8 % a.k_split == 0) && !no_xmap) {
+    if (grid.z == 1 && a.xalign > 0 && !no_xmap) {
+      b.xmap = 2;
+      b.ntiles = (int)grid.x;
+      const int groups = ((int)grid.x + a.xalign - 1) / a.xalign;
+      grid = dim3(8 * ((groups + 7) / 8) * a.xalign * a.k_split);
+    } else if (grid.z == 1 && a.allow_xmap && (a.k_split % 8 == 0 || 8 % a.k_split == 0) && !no_xmap) {
       b.xmap = 1;
       b.ntiles = (int)grid.x;
       if (a.k_split >= 8) {
