@@ -65,6 +65,23 @@ def pmc_traffic(kernel):
     return k[key]["traffic_bytes"], os.path.relpath(files[-1], ROOT)
 
 
+def mfma_counters(part="codec"):
+    """Aggregate MFMA utilisation of the vocoder (or LM) kernels from the newest committed counter
+    summary (profiles/rNN_mfma_<part>.txt, made by tools/pmc_mfma.sh + tools/mfma_summary.py:
+    SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x per-XCD GRBM_GUI_ACTIVE))."""
+    import glob
+    import re
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_mfma_{part}.txt")))
+    if not files:
+        return None
+    for line in open(files[-1]):
+        m = re.match(r"TOTAL mfma_util ([0-9.]+) over ([0-9.]+) ms .* ([0-9.]+) TFLOP/s executed", line)
+        if m:
+            return {"util": float(m.group(1)), "executed_tflops": float(m.group(3)),
+                    "source": os.path.relpath(files[-1], ROOT)}
+    return None
+
+
 def algorithmic_bytes(d, R, head_rows):
     """Per-kernel algorithmic HBM bytes of one decode step with R rows, SURVEY §8d's model (not
     this implementation's intermediates): weights read once, the recurrent state read and
@@ -249,6 +266,7 @@ def main():
                       "achieved": round(sum(cfl.values()) / (vtot * 1e-3) / 1e12, 1),
                       "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                       "frac": round(sum(cfl.values()) / (vtot * 1e-3) / 1e12 / MFMA_BF16_PEAK_TFLOPS, 4),
+                      "mfma_counters": mfma_counters("codec"),
                       "kernels": vk}
         # whole decode step (graph-replayed timing from the timed region)
         if dec_steps:

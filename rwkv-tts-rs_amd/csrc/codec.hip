@@ -48,6 +48,10 @@ struct ConvArgs {
   int64_t y_bs;
   const int* ntok;     // tokens per utterance; input length = ntok * tin_mul
   const bf16_t* zeros; // >= 16 zero bytes (source of out-of-range window rows)
+  // XCD-aware 1-D grid (xmap = 1): the gy column tiles of time tile x run back to back on one XCD
+  // (blocks b and b + 8 share one), so the input window they all read is fetched into that XCD's
+  // L2 once instead of once per column tile
+  int xmap, gx, gy;
 };
 
 __device__ inline float snake(float v, float a) {
@@ -89,10 +93,17 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int req = blockIdx.z;
   const int Tin = a.ntok[req] * a.tin_mul;
-  const int q0 = blockIdx.x * TM;
+  int bx = blockIdx.x, by = blockIdx.y;
+  if (a.xmap) {
+    const int k = blockIdx.x >> 3;
+    by = k % a.gy;
+    bx = (blockIdx.x & 7) + 8 * (k / a.gy);
+    if (bx >= a.gx) return;
+  }
+  const int q0 = bx * TM;
   if (q0 >= Tin) return;
   const int ncot = a.Co / TN;
-  const int phase = blockIdx.y / ncot, co0 = (blockIdx.y % ncot) * TN;
+  const int phase = by / ncot, co0 = (by % ncot) * TN;
   int ntaps, k0, kstep, pbase, pstep, ostr;
   if (a.mode == 0) {
     ntaps = a.K; k0 = 0; kstep = 1; pbase = -a.pad; pstep = a.dil; ostr = 1;
@@ -572,6 +583,16 @@ class Codec {
     a.y_alpha = o.alpha; a.y_bs = o.y_bs >= 0 ? o.y_bs : bs; a.ntok = d_ntok; a.zeros = zeros;
     const int phases = mode == 1 ? s : 1;
     dim3 grid((unsigned)((Tmax * (int64_t)tin_mul + kConvTM - 1) / kConvTM), (unsigned)(phases * (Co / TN)), (unsigned)n);
+    // XCD-aware order for the long-time-axis residual convs (conv7 at >= 32 time tiles: -4 %);
+    // the short prenet / conv_in / convT launches keep the default order (2x slower remapped)
+    static const int xm = getenv("RWKVTTS_CODEC_XMAP") ? atoi(getenv("RWKVTTS_CODEC_XMAP")) : 1;
+    a.xmap = 0;
+    if (xm && grid.y > 1 && mode == 0 && K == 7 && grid.x >= 32) {
+      a.xmap = 1;
+      a.gx = (int)grid.x;
+      a.gy = (int)grid.y;
+      grid = dim3((unsigned)(8 * ((grid.x + 7) / 8) * grid.y), 1, (unsigned)n);
+    }
     pbeg();
     const int KT = ntaps_max <= 1 ? 1 : (ntaps_max <= 3 ? 3 : 7);
     if (TN == 96) k_conv<96, 1><<<grid, 256, shm, stream>>>(a);

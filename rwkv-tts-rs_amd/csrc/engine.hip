@@ -84,10 +84,10 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
     while (ks > 128 && K % ks) ks >>= 1;
     return K / ks;
   };
-  splitA_ = pick(C, 256);   // r,k,v,LoRA-down: 53 col tiles x 4
+  splitA_ = pick(C, getenv("RWKVTTS_RKV_KS") ? atoi(getenv("RWKVTTS_RKV_KS")) : 256);   // r,k,v,LoRA-down: 53 col tiles x 4
   splitO_ = pick(C, getenv("RWKVTTS_WO_KS") ? atoi(getenv("RWKVTTS_WO_KS")) : 128);   // Wo: 16 col tiles x 8
   splitK_ = pick(C, getenv("RWKVTTS_KEY_KS") ? atoi(getenv("RWKVTTS_KEY_KS")) : 256);  // ffn key: 64 col tiles x 4
-  splitF_ = pick(F, 256);   // ffn value: 16 col tiles x 16
+  splitF_ = pick(F, getenv("RWKVTTS_VAL_KS") ? atoi(getenv("RWKVTTS_VAL_KS")) : 256);   // ffn value: 16 col tiles x 16
   splitH_ = pick(C, getenv("RWKVTTS_HEAD_KS") ? atoi(getenv("RWKVTTS_HEAD_KS")) : 512);   // head: 129 col tiles x 2
   RT_CHECK(C % 128 == 0 && F % 128 == 0, RWKVTTS_EUNSUPPORTED, "K dims must be multiples of 128");
   RT_CHECK(splitA_ <= kMaxParts, RWKVTTS_EUNSUPPORTED, "n_embd too large for the WKV partial sum (raise kMaxParts)");
