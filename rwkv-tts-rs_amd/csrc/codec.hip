@@ -190,6 +190,22 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
   // row = 4 * (lane >> 4) + j -> q), staged through this wave's LDS tile [32][TN + 4] f32;
   // (2) read back row-contiguous so each lane moves 16 B of f32 (residual, y) and 8 B per
   // plane, with the output Snake applied once per element.
+  // TN = 96 (the pointwise conv of the last stage, memory-bound): residual rows (f32,
+  // row-contiguous, this lane's epilogue elements) are requested now, before any store -- res may
+  // alias y, and loads issued after a store to y cannot be hoisted above it (every element is read
+  // and then written by the same lane, so the early read is the same value). 1.2x on that launch;
+  // at TN 32 / 64 the 8-16 extra float4 registers cost more occupancy than they save.
+  const int64_t yoff = req * a.y_bs;
+  constexpr int NIT = TN / 8;
+  constexpr bool kPreRes = TN == 96;
+  float4_ rv[kPreRes ? NIT : 1];
+#pragma unroll
+  for (int it = 0; it < (kPreRes ? NIT : 0); ++it) {
+    const int idx = lane + 64 * it, r = idx / (TN / 4), c4 = (idx % (TN / 4)) * 4;
+    const int q = q0 + wave * 32 + r;
+    rv[it] = (float4_){0.f, 0.f, 0.f, 0.f};
+    if (a.res && q < Tin) rv[it] = *(const float4_*)(a.res + yoff + (int64_t)(q * ostr + phase) * a.Co + co0 + c4);
+  }
   __syncthreads();  // every wave is done with the chunk buffers
   constexpr int LDE = TN + 4;
   float* sE = (float*)lds + wave * 32 * LDE;
@@ -207,15 +223,17 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
         sE[(m * 16 + 4 * g + j) * LDE + n * 16 + li] = v * gm;
       }
   }
-  const int64_t yoff = req * a.y_bs;
 #pragma unroll
-  for (int it = 0; it < TN / 8; ++it) {
+  for (int it = 0; it < NIT; ++it) {
     const int idx = lane + 64 * it, r = idx / (TN / 4), c4 = (idx % (TN / 4)) * 4;
     const int q = q0 + wave * 32 + r;
     if (q >= Tin) continue;
     float4_ v = *(const float4_*)(sE + r * LDE + c4);
     const int64_t o = yoff + (int64_t)(q * ostr + phase) * a.Co + co0 + c4;
-    if (a.res) v += *(const float4_*)(a.res + o);
+    if (a.res) {
+      if constexpr (kPreRes) v += rv[it];
+      else v += *(const float4_*)(a.res + o);
+    }
     if (a.y) *(float4_*)(a.y + o) = v;
     if (a.yh) {
       uint16_t h[4], l[4];
