@@ -154,7 +154,18 @@ typedef struct {
   int32_t use_graphs;       /* capture decode steps in hipGraphs */
   int32_t wkv_variant;      /* 0 auto; 1 k_wkv4 (2 waves per (slot, head)); 2 k_wkv6 (4 waves).
                                0.4B LoRA ranks only; both are tested against the oracle */
+  /* web-rwkv ModelBuilder::quant(HashMap<layer, Quant>) as the server builds it from
+   * --quant-layers / --quant-type (bin/server.rs:1029-1071, src/shared_runtime.rs:156-160):
+   * layers [0, quant_layers) store their r / k / v / o and FFN key / value matrices quantised
+   * (the LoRA matrices, embedding and head stay 16-bit). RWKVTTS_QUANT_NONE when 0 layers. */
+  int32_t quant_layers;
+  int32_t quant_type;       /* RWKVTTS_QUANT_* */
 } rwkvtts_engine_desc;
+
+#define RWKVTTS_QUANT_NONE 0
+#define RWKVTTS_QUANT_INT8 1 /* 128-element blocks along K: f16 (min, max), u8 q; w = min + q/255 (max - min) */
+#define RWKVTTS_QUANT_NF4 2  /* 64-element blocks along K: f16 absmax, 4-bit NormalFloat index; w = nf4[q] absmax */
+#define RWKVTTS_QUANT_SF4 3  /* rejected (RWKVTTS_EUNSUPPORTED): its code table is not available offline */
 
 /* weights: packed blob (header included). blob_on_device != 0: `weights` is a device pointer
  * on desc->device (e.g. a buffer filled by an RCCL broadcast); it is copied. */

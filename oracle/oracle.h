@@ -55,6 +55,9 @@ float oracle_expf(float x); /* = glibc expf */
 typedef struct oracle_model oracle_model;
 oracle_model* oracle_model_load(const void* blob, size_t bytes);
 void oracle_model_free(oracle_model* m);
+/* web-rwkv Quant restated (rwkv7.c): layers [0, quant_layers) use dequantised r / k / v / o / FFN
+ * matrices; quant_type 1 Int8, 2 NF4 (0: none). 0 ok, -1 invalid. */
+int oracle_model_quantize(oracle_model* m, int quant_layers, int quant_type);
 int64_t oracle_state_floats(const oracle_model* m);
 /* one token; state updated in place; logits (head_rows, may be NULL) of this token */
 void oracle_forward_token(const oracle_model* m, float* state, uint32_t token, float* logits,

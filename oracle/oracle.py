@@ -59,6 +59,8 @@ def lib():
         L.oracle_model_load.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
         L.oracle_model_load.restype = ctypes.c_void_p
         L.oracle_model_free.argtypes = [ctypes.c_void_p]
+        L.oracle_model_quantize.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+        L.oracle_model_quantize.restype = ctypes.c_int
         L.oracle_state_floats.argtypes = [ctypes.c_void_p]
         L.oracle_state_floats.restype = ctypes.c_int64
         L.oracle_forward_token.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int]
@@ -121,7 +123,7 @@ def expf(x):
 class Model:
     """RWKV-7 x070 f32 forward (web-rwkv Bundle<f32> arithmetic restated)."""
 
-    def __init__(self, blob: np.ndarray, threads: int = 0):
+    def __init__(self, blob: np.ndarray, threads: int = 0, quant_layers: int = 0, quant_type: int = 0):
         b = np.ascontiguousarray(blob)
         self._blob = b
         self.h = lib().oracle_model_load(b.ctypes.data_as(ctypes.c_void_p), b.nbytes)
@@ -129,6 +131,9 @@ class Model:
             raise ValueError("bad weight blob")
         if threads:
             lib().oracle_set_threads(threads)
+        if quant_layers and quant_type:  # web-rwkv Quant restated (rwkv7.c): 1 Int8, 2 NF4
+            if lib().oracle_model_quantize(self.h, int(quant_layers), int(quant_type)) != 0:
+                raise ValueError("bad quantisation config")
 
     def __del__(self):
         try:

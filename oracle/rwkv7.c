@@ -28,6 +28,7 @@ struct oracle_model {
   int dtype;
   uint8_t* blob;
   size_t bytes;
+  float** qf; /* [n_layer][6] dequantised r, k, v, o, ffn key, ffn value (NULL: 16-bit) */
 };
 
 static inline float bf16_to_f32(uint16_t h) {
@@ -66,6 +67,102 @@ static inline float mat_at(const oracle_model* m, const uint16_t* w, int64_t i) 
 static int g_threads = 0;
 void oracle_set_threads(int n) { g_threads = n; }
 
+/* ---- quantised matrices: web-rwkv 0.10.16 Quant::{Int8, NF4} (ModelBuilder::quant, set from the
+ * server's --quant-layers / --quant-type, bin/server.rs:1029-1071). The crate is not vendored,
+ * so this restates its published block quantisers (parity unpinned):
+ *   Int8: blocks of 128 consecutive elements of a row (along K); mn = f16(min), mx = f16(max);
+ *     q = floor(fma(clamp((x - mn) / (mx - mn), 0, 1), 255, 0.5)) (0 when mx == mn);
+ *     w = fma(q / 255, mx - mn, mn)                         (unpack4x8unorm(q) = q / 255)
+ *   NF4: blocks of 64; s = f16(max |x|); q = #{i < 15 : x / s > (t[i] + t[i+1]) / 2}
+ *     (7 when s == 0); w = t[q] * s, t = the NormalFloat-4 table.
+ * f16(.) is round-to-nearest-even. */
+static uint16_t f32_to_f16_rne(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  const uint32_t sign = (u >> 16) & 0x8000u;
+  const uint32_t a = u & 0x7fffffffu;
+  if (a >= 0x7f800000u) return (uint16_t)(sign | (a > 0x7f800000u ? 0x7e00u : 0x7c00u));
+  if (a >= 0x477ff000u) return (uint16_t)(sign | 0x7c00u); /* rounds to >= 65520: inf */
+  if (a < 0x38800000u) {                                     /* f16 subnormal or zero */
+    const int e = (int)(a >> 23);
+    if (e < 102) return (uint16_t)sign;
+    const uint32_t m = (a & 0x7fffffu) | 0x800000u;
+    const int sh = 126 - e; /* value = m * 2^(e - 150); f16 unit 2^-24 */
+    uint32_t q = m >> sh, r = m & ((1u << sh) - 1u), half = 1u << (sh - 1);
+    if (r > half || (r == half && (q & 1u))) ++q;
+    return (uint16_t)(sign | q);
+  }
+  uint32_t q = ((a >> 13) - (112u << 10)), r = a & 0x1fffu;
+  if (r > 0x1000u || (r == 0x1000u && (q & 1u))) ++q;
+  return (uint16_t)(sign | q);
+}
+static const float kNF4[16] = {
+    -1.0f, -0.6961928009986877f, -0.5250730514526367f, -0.39491748809814453f, -0.28444138169288635f,
+    -0.18477343022823334f, -0.09105003625154495f, 0.0f, 0.07958029955625534f, 0.16093020141124725f,
+    0.24611230194568634f, 0.33791524171829224f, 0.44070982933044434f, 0.5626170039176941f,
+    0.7229568362236023f, 1.0f};
+
+/* dequantised copy of a [N][K] matrix (2-byte blob storage) */
+static float* quant_matrix(const oracle_model* m, const uint16_t* W, int N, int K, int qt) {
+  float* out = (float*)malloc((size_t)N * K * sizeof(float));
+  const int BS = qt == 1 ? 128 : 64;
+  for (int n = 0; n < N; ++n)
+    for (int k0 = 0; k0 < K; k0 += BS) {
+      const uint16_t* src = W + (size_t)n * K + k0;
+      float* dst = out + (size_t)n * K + k0;
+      if (qt == 1) {
+        float lo = mat_at(m, src, 0), hi = lo;
+        for (int i = 1; i < BS; ++i) {
+          const float x = mat_at(m, src, i);
+          lo = fminf(lo, x);
+          hi = fmaxf(hi, x);
+        }
+        const float mn = f16_to_f32(f32_to_f16_rne(lo)), mx = f16_to_f32(f32_to_f16_rne(hi)), d = mx - mn;
+        for (int i = 0; i < BS; ++i) {
+          unsigned q = 0;
+          if (mx != mn) {
+            float v = (mat_at(m, src, i) - mn) / d;
+            v = fminf(fmaxf(v, 0.0f), 1.0f);
+            q = (unsigned)floorf(fmaf(v, 255.0f, 0.5f));
+          }
+          dst[i] = fmaf((float)q / 255.0f, d, mn);
+        }
+      } else {
+        float am = 0.0f;
+        for (int i = 0; i < BS; ++i) am = fmaxf(am, fabsf(mat_at(m, src, i)));
+        const float sc = f16_to_f32(f32_to_f16_rne(am));
+        for (int i = 0; i < BS; ++i) {
+          unsigned q = 7;
+          if (sc != 0.0f) {
+            const float v = mat_at(m, src, i) / sc;
+            q = 0;
+            for (int t = 0; t < 15; ++t) q += v > 0.5f * (kNF4[t] + kNF4[t + 1]) ? 1u : 0u;
+          }
+          dst[i] = kNF4[q] * sc;
+        }
+      }
+    }
+  return out;
+}
+
+static const int kQuantT[6] = {RWKVTTS_L_WR, RWKVTTS_L_WK, RWKVTTS_L_WV, RWKVTTS_L_WO, RWKVTTS_L_FFN_K,
+                               RWKVTTS_L_FFN_V};
+
+int oracle_model_quantize(oracle_model* m, int quant_layers, int quant_type) {
+  if (quant_type < 0 || quant_type > 2 || quant_layers < 0) return -1;
+  if (quant_type == 0 || quant_layers == 0) return 0;
+  const int L = m->d.n_layer, C = m->d.n_embd, F = m->d.n_ffn;
+  if (C % 128 || F % 128) return -1;
+  if (!m->qf) m->qf = (float**)calloc((size_t)L * 6, sizeof(float*));
+  for (int l = 0; l < L && l < quant_layers; ++l)
+    for (int j = 0; j < 6; ++j) {
+      const int N = j == 4 ? F : C, K = j == 5 ? F : C;
+      free(m->qf[l * 6 + j]);
+      m->qf[l * 6 + j] = quant_matrix(m, (const uint16_t*)T(m, l, kQuantT[j]), N, K, quant_type);
+    }
+  return 0;
+}
+
 /* y[rows] = W[rows][cols] x[cols] */
 static void matvec(const oracle_model* m, const void* W, int rows, int cols, const float* x,
                    float* y) {
@@ -81,6 +178,28 @@ static void matvec(const oracle_model* m, const void* W, int rows, int cols, con
       for (int c = 0; c < cols; ++c) acc += bf16_to_f32(row[c]) * x[c];
     else
       for (int c = 0; c < cols; ++c) acc += f16_to_f32(row[c]) * x[c];
+    y[r] = acc;
+  }
+}
+
+/* matrix t of layer l: the dequantised copy when the layer is quantised */
+static void matvec_l(const oracle_model* m, int l, int t, int rows, int cols, const float* x, float* y) {
+  const float* q = NULL;
+  if (m->qf)
+    for (int j = 0; j < 6; ++j)
+      if (kQuantT[j] == t) q = m->qf[l * 6 + j];
+  if (!q) {
+    matvec(m, T(m, l, t), rows, cols, x, y);
+    return;
+  }
+#ifdef _OPENMP
+  int nt = g_threads > 0 ? g_threads : omp_get_max_threads();
+#pragma omp parallel for schedule(static) num_threads(nt) if ((int64_t)rows * cols >= (1 << 18))
+#endif
+  for (int r = 0; r < rows; ++r) {
+    const float* row = q + (int64_t)r * cols;
+    float acc = 0.0f;
+    for (int c = 0; c < cols; ++c) acc += row[c] * x[c];
     y[r] = acc;
   }
 }
@@ -117,6 +236,10 @@ oracle_model* oracle_model_load(const void* blob, size_t bytes) {
 
 void oracle_model_free(oracle_model* m) {
   if (!m) return;
+  if (m->qf) {
+    for (int i = 0; i < m->d.n_layer * 6; ++i) free(m->qf[i]);
+    free(m->qf);
+  }
   free(m->blob);
   free(m);
 }
@@ -171,9 +294,9 @@ void oracle_forward_token(const oracle_model* m, float* state, uint32_t token, f
     memcpy(att_shift, xx, sizeof(float) * C);
     float *xr = mix[0], *xw = mix[1], *xk = mix[2], *xv = mix[3], *xa = mix[4], *xg = mix[5];
 
-    matvec(m, T(m, l, RWKVTTS_L_WR), C, C, xr, r);
-    matvec(m, T(m, l, RWKVTTS_L_WK), C, C, xk, k);
-    matvec(m, T(m, l, RWKVTTS_L_WV), C, C, xv, v);
+    matvec_l(m, l, RWKVTTS_L_WR, C, C, xr, r);
+    matvec_l(m, l, RWKVTTS_L_WK, C, C, xk, k);
+    matvec_l(m, l, RWKVTTS_L_WV, C, C, xv, v);
 
     /* w = exp(-e^-0.5 * sigmoid(w0 + W2 tanh(W1 xw))) */
     matvec(m, T(m, l, RWKVTTS_L_W1T), Dw, C, xw, hid);
@@ -265,7 +388,7 @@ void oracle_forward_token(const oracle_model* m, float* state, uint32_t token, f
         }
       }
     }
-    matvec(m, T(m, l, RWKVTTS_L_WO), C, C, tmp, y);
+    matvec_l(m, l, RWKVTTS_L_WO, C, C, tmp, y);
     for (int c = 0; c < C; ++c) x[c] += y[c];
 
     /* ---- channel mix ---- */
@@ -275,12 +398,12 @@ void oracle_forward_token(const oracle_model* m, float* state, uint32_t token, f
       for (int c = 0; c < C; ++c) tmp[c] = xx[c] + (ffn_shift[c] - xx[c]) * mu[c];
     }
     memcpy(ffn_shift, xx, sizeof(float) * C);
-    matvec(m, T(m, l, RWKVTTS_L_FFN_K), F, C, tmp, kf);
+    matvec_l(m, l, RWKVTTS_L_FFN_K, F, C, tmp, kf);
     for (int i = 0; i < F; ++i) {
       float t = kf[i] > 0.0f ? kf[i] : 0.0f;
       kf[i] = t * t;
     }
-    matvec(m, T(m, l, RWKVTTS_L_FFN_V), C, F, kf, y);
+    matvec_l(m, l, RWKVTTS_L_FFN_V, C, F, kf, y);
     for (int c = 0; c < C; ++c) x[c] += y[c];
   }
 

@@ -17,6 +17,12 @@ struct LayerW {
   const float *w0, *a0, *v0, *k_k, *k_a, *r_k, *lnx_w, *lnx_b, *ffn_xk;
   const bf16_t *wr, *wk, *wv, *wo, *w1t, *a1t, *v1t, *g1t, *w2t, *a2t, *v2t, *g2t, *ffn_k, *ffn_v;
   const bf16_t* lup;  // LoRA-up rows repacked for k_wkv
+  // RWKVTTS_QUANT_* of this layer's r / k / v / o / FFN matrices (0: 16-bit fragments) and their
+  // codes / scales (launch_quant_pack layout; r, k, v back to back as the rkv launch's tiles 0..)
+  int quant = 0;
+  const uint8_t *q_rkv = nullptr, *q_o = nullptr, *q_fk = nullptr, *q_fv = nullptr;
+  const void *s_rkv = nullptr, *s_o = nullptr, *s_fk = nullptr, *s_fv = nullptr;
+  int qs_rkv = 0, qs_o = 0, qs_fk = 0, qs_fv = 0;  // f16 models: GemmArgs::q_shift per launch
 };
 
 // One forward step description (host side).

@@ -152,6 +152,59 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
     RT_HIP(hipGetLastError());
     w.lup = dst;
   }
+  // quantised layers (web-rwkv ModelBuilder::quant, bin/server.rs:1029-1071): codes + scales of
+  // the r / k / v / o / FFN matrices from the blob's row-major 16-bit copies
+  {
+    const int qt = desc.quant_type, ql = std::min(std::max(desc.quant_layers, 0), (int)dims.n_layer);
+    RT_CHECK(qt >= RWKVTTS_QUANT_NONE && qt <= RWKVTTS_QUANT_SF4, RWKVTTS_EINVAL, "unknown quant_type");
+    RT_CHECK(!(qt == RWKVTTS_QUANT_SF4 && ql > 0), RWKVTTS_EUNSUPPORTED,
+             "quant_type sf4: its code table is not available (web-rwkv not vendored)");
+    if (qt != RWKVTTS_QUANT_NONE && ql > 0) {
+      RT_CHECK(C % kQ8Block == 0 && F % kQ8Block == 0, RWKVTTS_EUNSUPPORTED, "quantisation needs K % 128 == 0");
+      const size_t cb_cc = quant_code_bytes(qt, C, C), sb_cc = quant_scale_bytes(qt, C, C);
+      const size_t cb_fc = quant_code_bytes(qt, F, C), sb_fc = quant_scale_bytes(qt, F, C);
+      const size_t per_layer = 4 * cb_cc + 2 * cb_fc + 4 * sb_cc + 2 * sb_fc;
+      uint8_t* qbuf = nullptr;
+      RT_OK(alloc(&qbuf, per_layer * ql));
+      RT_HIP(hipDeviceSynchronize());  // alloc's memset runs on the null stream
+      for (int l = 0; l < ql; ++l) {
+        LayerW& w = L_[l];
+        uint8_t* q = qbuf + per_layer * l;
+        uint8_t* sc = q + 4 * cb_cc + 2 * cb_fc;
+        w.quant = qt;
+        w.q_rkv = q; w.s_rkv = sc;
+        for (int j = 0; j < 3; ++j)
+          launch_quant_pack((const uint16_t*)(j == 0 ? w.wr : j == 1 ? w.wk : w.wv), C, C, f16_, qt,
+                            q + j * cb_cc, sc + j * sb_cc, stream_);
+        w.q_o = q + 3 * cb_cc; w.s_o = sc + 3 * sb_cc;
+        launch_quant_pack((const uint16_t*)w.wo, C, C, f16_, qt, (uint8_t*)w.q_o, (void*)w.s_o, stream_);
+        w.q_fk = q + 4 * cb_cc; w.s_fk = sc + 4 * sb_cc;
+        launch_quant_pack((const uint16_t*)w.ffn_k, F, C, f16_, qt, (uint8_t*)w.q_fk, (void*)w.s_fk, stream_);
+        w.q_fv = q + 4 * cb_cc + cb_fc; w.s_fv = sc + 4 * sb_cc + sb_fc;
+        launch_quant_pack((const uint16_t*)w.ffn_v, C, F, f16_, qt, (uint8_t*)w.q_fv, (void*)w.s_fv, stream_);
+      }
+      RT_HIP(hipGetLastError());
+      RT_HIP(hipStreamSynchronize(stream_));
+      // f16 models: per launch, the shift that brings the largest dequantised |w| to ~2^14
+      // (int8: max(|min|, |max|) of the blocks; nf4: the largest block absmax)
+      auto shift_of = [&](const void* scales, size_t bytes) -> int {
+        std::vector<uint16_t> h(bytes / 2);
+        if (hipMemcpy(h.data(), scales, bytes, hipMemcpyDeviceToHost) != hipSuccess) return 0;
+        float mx = 0.0f;
+        for (uint16_t v : h) mx = std::max(mx, std::fabs(f16_to_f32(v)));
+        if (!(mx > 0.0f) || !std::isfinite(mx)) return 0;
+        return std::max(0, std::min(24, 14 - (int)std::ceil(std::log2(mx))));
+      };
+      if (f16_)
+        for (int l = 0; l < ql; ++l) {
+          LayerW& w = L_[l];
+          w.qs_rkv = shift_of(w.s_rkv, 3 * sb_cc);
+          w.qs_o = shift_of(w.s_o, sb_cc);
+          w.qs_fk = shift_of(w.s_fk, sb_fc);
+          w.qs_fv = shift_of(w.s_fv, sb_fc);
+        }
+    }
+  }
   // GEMM matrices -> MFMA fragment blocks (k_gemm streams each wave's weights as contiguous 1 KB
   // blocks); the blob's row-major copies stay for the embedding gather and the oracle layout
   {
@@ -430,6 +483,11 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     seg(6, w.g1t, 5, dims.d_gate, 3 * C + dims.d_decay + dims.d_aaa + dims.d_mv);
     g.K = C; g.M = R; g.k_split = splitA_; g.kslice = C / splitA_;
     gemm_tile_table(g, RC);
+    if (w.quant) {  // r, k, v (tiles of segments 0-2) quantised; the LoRA-down tiles stay 16-bit
+      RT_CHECK(g.n_tinfo > 0, RWKVTTS_EUNSUPPORTED, "quantised rkv launch needs the per-tile table");
+      g.q_fmt = w.quant; g.qw = w.q_rkv; g.qs = w.s_rkv; g.q_shift = w.qs_rkv;
+      for (int t = 0; t < 3 * C / 64; ++t) g.tinfo[t] |= 1u << 31;
+    }
     g.xmode = kXPlanes; g.out = partA_; g.split_stride = (int64_t)Rmax_ * ldA_; g.ldo = ldA_;
     g.allow_xmap = xmap_mask_ & 1;
     g.xalign = (xalign_mask_ & 1) ? 1 : 0;  // r / k / v tile h (head h) on the XCD of WKV head h
@@ -469,6 +527,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     go.K = C; go.M = R; go.k_split = splitO_; go.kslice = C / splitO_;
     go.xmode = kXPlanes; go.out = partO_; go.split_stride = RC; go.ldo = C;
     go.allow_xmap = (xmap_mask_ >> 1) & 1;
+    if (w.quant) { go.q_fmt = w.quant; go.qw = w.q_o; go.qs = w.s_o; go.q_shift = w.qs_o; }
     go.wt = (wt_mask_ >> 1) & 1;
     prof_begin(&ev);
     go.exp = dbg_exp_ >> 8;
@@ -500,6 +559,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     gk.K = C; gk.M = R; gk.k_split = splitK_; gk.kslice = C / splitK_;
     gk.xmode = kXPlanes; gk.out = partK_; gk.split_stride = (int64_t)Rmax_ * F; gk.ldo = F;
     gk.allow_xmap = (xmap_mask_ >> 2) & 1;
+    if (w.quant) { gk.q_fmt = w.quant; gk.qw = w.q_fk; gk.qs = w.s_fk; gk.q_shift = w.qs_fk; }
     // key tiles of value K-slice s on the XCD that runs slice s (value xmap: split = xcd + 8 j)
     if ((xalign_mask_ >> 2) & 1) gk.xalign = std::max(1, (F / splitF_) / 64);
     gk.wt = (wt_mask_ >> 2) & 1;
@@ -517,6 +577,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     gv.x_part_stride = (int64_t)Rmax_ * F;
     gv.out = partF_; gv.split_stride = RC; gv.ldo = C;
     gv.allow_xmap = (xmap_mask_ >> 3) & 1;
+    if (w.quant) { gv.q_fmt = w.quant; gv.qw = w.q_fv; gv.qs = w.s_fv; gv.q_shift = w.qs_fv; }
     gv.wt = (wt_mask_ >> 3) & 1;
     prof_begin(&ev);
     gv.stamps = (l == 5 && dbg_gstamps_) ? dbg_gstamps_ + 4096 * 4 : nullptr;

@@ -90,6 +90,17 @@ struct GemmArgs {
   // XCD whose workgroups consume those columns next (the value GEMM's K-slice, the WKV head), so
   // the consumer reads the partial slabs from its own L2. Set xalign > 0 to request it.
   int xalign;
+  // quantised weights (RWKVTTS_QUANT_INT8 / NF4): q_fmt != 0 -> the launch (MS 0) or its tiles
+  // whose tinfo bit 31 is set (MS 2) read codes / scales (launch_quant_pack layout, column tiles
+  // of 64 back to back) instead of 16-bit fragments, dequantise in registers and split the weight
+  // into hi + lo 16-bit planes (three MFMAs per product: ~f32 dequantised weights)
+  int q_fmt;
+  const uint8_t* qw;
+  const void* qs;
+  // f16 models: the dequantised weights are split as w * 2^q_shift (brought up to ~2^14 at the
+  // matrix's largest |w|) so that the lo half stays a normal f16 number; the product is scaled
+  // back by 2^-q_shift in the epilogue (powers of two: exact)
+  int q_shift;
   uint32_t tinfo[128];
 };
 
@@ -142,6 +153,16 @@ int wkv_perm_layout(int Dw, int Da, int Dv, int Dg, int n_part, int max_slots, i
 // Repack a GEMM matrix W [N][K] (K % 32 == 0) into MFMA fragment blocks (k_gemm's layout):
 // out holds ceil(N/16)*16*K elements.
 void launch_pack_frag(const bf16_t* W, int N, int K, bf16_t* out, hipStream_t st);
+
+// Quantised matrices (RWKVTTS_QUANT_*, web-rwkv Quant restated): W [N][K] 16-bit -> codes in
+// launch_pack_frag's fragment order (block (nb, kb) = 16 columns x 32 k, lane 16 g + li holding
+// k = 32 kb + 8 g .. + 8 of column 16 nb + li: 8 bytes (int8) or 4 bytes (nf4, low nibble first))
+// and per-(column, K-block) scales: int8 [N][K / 128] u32 = f16 min | f16 max << 16; nf4
+// [N][K / 64] u16 = f16 absmax.
+constexpr int kQ8Block = 128, kQ4Block = 64;
+inline size_t quant_code_bytes(int qt, int N, int K) { return (size_t)N * K / (qt == 1 ? 1 : 2); }
+inline size_t quant_scale_bytes(int qt, int N, int K) { return qt == 1 ? (size_t)N * (K / kQ8Block) * 4 : (size_t)N * (K / kQ4Block) * 2; }
+void launch_quant_pack(const uint16_t* W, int N, int K, int f16, int qt, uint8_t* codes, void* scales, hipStream_t st);
 // Repack one layer's LoRA-up rows (0.4B ranks 64/64/32/128) into k_wkv4's coalesced order.
 void launch_pack_lora4(const bf16_t* w2t, const bf16_t* a2t, const bf16_t* v2t, const bf16_t* g2t, int C,
                        bf16_t* out, hipStream_t st);

@@ -25,6 +25,13 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 // Cross-lane sums on DPP moves (no LDS round trip, unlike __shfl_xor's ds_bpermute). Each step
 // pairs every lane with a partner holding the other half of its group and both add in the same
 // order, so every lane of a group ends with the identical sum.
+// NormalFloat-4 code table (RWKVTTS_QUANT_NF4; quant_pack below, k_gemm2 dequantisation)
+__device__ __constant__ float kNF4[16] = {
+    -1.0f, -0.6961928009986877f, -0.5250730514526367f, -0.39491748809814453f, -0.28444138169288635f,
+    -0.18477343022823334f, -0.09105003625154495f, 0.0f, 0.07958029955625534f, 0.16093020141124725f,
+    0.24611230194568634f, 0.33791524171829224f, 0.44070982933044434f, 0.5626170039176941f,
+    0.7229568362236023f, 1.0f};
+
 template <int CTRL>
 __device__ inline float dpp_mov(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
@@ -552,10 +559,11 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
 //    latency; in kXRelu2 mode all NX key slabs are in flight at once;
 //  * hi and lo products accumulate in separate MFMA chains (2*MT independent accumulators).
 // ------------------------------------------------------------------------------------
-template <int MT, int KSTEPS, int XMODE, bool F16, int NX, int MS>
+template <int MT, int KSTEPS, int XMODE, bool F16, int NX, int MS, bool QW = false>
 __global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ uint32_t s_rexp[MT * 16];  // f16 relu^2 rows: bits of the row maximum if >= 2^15
+  __shared__ float s_qlut[QW ? 256 + 16 : 1];  // QW: q / 255 (int8), then the NF4 table
   constexpr int KS = KSTEPS * 32;
   constexpr int LD = KS + 8;
   constexpr int ROWS = MT * 16;
@@ -603,14 +611,17 @@ __global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
         ldx = a.seg[j].ldx; Nn = a.seg[j].N; col_off = a.seg[j].col_off; tstart = a.seg[j].tile_start;
       }
   }
+  int qf = 0;  // QW: this tile's weight format (0: 16-bit fragments)
+  if constexpr (QW && MS != 2) qf = a.q_fmt;
   if constexpr (MS == 2) {
     const uint32_t ti = a.tinfo[tile];
+    if constexpr (QW) qf = (ti >> 31) ? a.q_fmt : 0;
     const int mix = ti & 7;
     Wm = a.tw + (int64_t)tile * 64 * a.K;
     Xhi += mix * a.x_mix_stride;
     Xlo += mix * a.x_mix_stride;
     Nn = (ti >> 3) & 127;      // valid columns of this tile (the tile is its own segment)
-    col_off = (int)(ti >> 10);
+    col_off = (int)((ti >> 10) & 0x1FFFFFu);
     tstart = tile;
   }
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -631,6 +642,14 @@ __global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
   if (nb >= nblk) nb = nblk - 1;
   const bf16_t* wp = Wm + (((int64_t)nb * (a.K >> 5) + (kbeg >> 5)) * 64 + lane) * 8;
   short8 b[KSTEPS];
+  // quantised tiles: codes in the same fragment order (column tiles back to back from the
+  // launch's first quantised tile), one scale word per (column, K-block) and step
+  uint2 bq8[QW ? KSTEPS : 1];
+  uint32_t bq4[QW ? KSTEPS : 1], qsc[QW ? KSTEPS : 1];
+  if constexpr (QW) {
+    if (threadIdx.x < 256) s_qlut[threadIdx.x] = (float)threadIdx.x / 255.0f;
+    if (threadIdx.x < 16) s_qlut[256 + threadIdx.x] = kNF4[threadIdx.x];
+  }
   auto load_x = [&]() {
   if constexpr (XMODE == kXPlanes) {
 #pragma unroll
@@ -655,6 +674,33 @@ __global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
   }
   };
   auto load_w = [&]() {
+    if constexpr (QW) {
+      if (qf) {
+        const int nbq = MS == 2 ? tile * 4 + wave : nb;
+        const int64_t ncol = (int64_t)nbq * 16 + li;
+        const int64_t cb = (((int64_t)nbq * (a.K >> 5) + (kbeg >> 5)) * 64 + lane);
+        if (qf == 1) {
+          typedef uint32_t u32x2q __attribute__((ext_vector_type(2)));
+          const u32x2q* qp = (const u32x2q*)(a.qw + cb * 8);
+#pragma unroll
+          for (int t = 0; t < KSTEPS; ++t) {
+            const u32x2q v = __builtin_nontemporal_load(qp + t * 64);
+            bq8[t] = make_uint2(v.x, v.y);
+          }
+#pragma unroll
+          for (int t = 0; t < KSTEPS; ++t)
+            qsc[t] = ((const uint32_t*)a.qs)[ncol * (a.K / kQ8Block) + ((kbeg + 32 * t) / kQ8Block)];
+        } else {
+          const uint32_t* qp = (const uint32_t*)(a.qw + cb * 4);
+#pragma unroll
+          for (int t = 0; t < KSTEPS; ++t) bq4[t] = __builtin_nontemporal_load(qp + t * 64);
+#pragma unroll
+          for (int t = 0; t < KSTEPS; ++t)
+            qsc[t] = ((const uint16_t*)a.qs)[ncol * (a.K / kQ4Block) + ((kbeg + 32 * t) / kQ4Block)];
+        }
+        return;
+      }
+    }
 #pragma unroll
   for (int t = 0; t < KSTEPS; ++t) b[t] = __builtin_nontemporal_load((const short8*)(wp + t * 512));
   };
@@ -719,6 +765,55 @@ __global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
   float4_ acc_h[MT], acc_l[MT];
 #pragma unroll
   for (int m = 0; m < MT; ++m) acc_h[m] = acc_l[m] = (float4_){0.f, 0.f, 0.f, 0.f};
+  if constexpr (QW) {
+    if (qf) {
+      // dequantise 8 weights per step, split w = hi + lo, three MFMAs per product (x_hi w_hi,
+      // x_lo w_hi, x_hi w_lo): the dequantised weights enter at ~2^-16 relative
+#pragma unroll
+      for (int t = 0; t < KSTEPS; ++t) {
+        float w[8];
+        if (qf == 1) {
+          const float mn = h16_to_f32((uint16_t)(qsc[t] & 0xFFFFu)), mx = h16_to_f32((uint16_t)(qsc[t] >> 16));
+          const float d = mx - mn;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const uint32_t q = ((e < 4 ? bq8[t].x : bq8[t].y) >> (8 * (e & 3))) & 255u;
+            w[e] = fmaf(s_qlut[q], d, mn);
+          }
+        } else {
+          const float sc = h16_to_f32((uint16_t)qsc[t]);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) w[e] = s_qlut[256 + ((bq4[t] >> (4 * e)) & 15u)] * sc;
+        }
+        if constexpr (F16) {
+          const float up = __builtin_amdgcn_ldexpf(1.0f, a.q_shift);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) w[e] *= up;
+        }
+        uint32_t hh[4], ll[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) split2<F16>(w[2 * e], w[2 * e + 1], hh[e], ll[e]);
+        const short8 bh = __builtin_bit_cast(short8, (u32x4_){hh[0], hh[1], hh[2], hh[3]});
+        const short8 bl = __builtin_bit_cast(short8, (u32x4_){ll[0], ll[1], ll[2], ll[3]});
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          const int o = (m * 16 + li) * LD + t * 32 + g * 8;
+          const short8 ah = *(const short8*)(xh + o);
+          const short8 al = *(const short8*)(xl + o);
+          if constexpr (F16) {
+            acc_h[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, ah), __builtin_bit_cast(f16x8, bh), acc_h[m], 0, 0, 0);
+            acc_l[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, al), __builtin_bit_cast(f16x8, bh), acc_l[m], 0, 0, 0);
+            acc_l[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, ah), __builtin_bit_cast(f16x8, bl), acc_l[m], 0, 0, 0);
+          } else {
+            acc_h[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ah), __builtin_bit_cast(bf16x8, bh), acc_h[m], 0, 0, 0);
+            acc_l[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, al), __builtin_bit_cast(bf16x8, bh), acc_l[m], 0, 0, 0);
+            acc_l[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ah), __builtin_bit_cast(bf16x8, bl), acc_l[m], 0, 0, 0);
+          }
+        }
+      }
+    }
+  }
+  if (!qf) {
 #pragma unroll
   for (int t = 0; t < KSTEPS; ++t) {
 #pragma unroll
@@ -739,10 +834,14 @@ __global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
       }
     }
   }
+  }
   // 5) store (D layout: col = lane&15, row = 4*(lane>>4) + j)
   const int col = col0 + li;
   auto result = [&](int m, int j) {
     float v = acc_h[m][j] + acc_l[m][j];
+    if constexpr (F16 && QW) {
+      if (qf) v *= __builtin_amdgcn_ldexpf(1.0f, -a.q_shift);
+    }
     if constexpr (F16 && XMODE == kXRelu2) {
       const uint32_t mb = s_rexp[m * 16 + 4 * g + j];
       if (mb) v *= as_f32((uint32_t)((int)((mb >> 23) & 0xFF) - 127 - 14 + 127) << 23);  // 2^(E - 14)
@@ -1034,7 +1133,9 @@ static void launch_gemm_t(const GemmArgs& a, dim3 grid, hipStream_t st) {
   const size_t lds = (size_t)MT * 16 * (KSTEPS * 32 + 8) * 2 * 2;
   // k_gemm2 (fragment-packed weights, per-tile descriptors) covers the 0.4B shapes; k_gemm is the
   // generic fallback (other slab counts) and the debug-stamp build
-  if ((a.xmode == kXPlanes || a.x_nsplit == 4 || a.x_nsplit == 2) && a.stamps == nullptr && a.exp == 0) {
+  // (quantised weights exist only in k_gemm2: debug stamps / experiments are ignored for them)
+  const bool nx_ok = a.x_nsplit == 4 || a.x_nsplit == 2 || (a.x_nsplit == 1 && a.q_fmt);
+  if ((a.xmode == kXPlanes || nx_ok) && ((a.stamps == nullptr && a.exp == 0) || a.q_fmt)) {
     const int ms = a.nseg > 1 ? (a.n_tinfo > 0 ? 2 : 1) : 0;
     GemmArgs b = a;
     b.xmap = 0;
@@ -1054,15 +1155,21 @@ static void launch_gemm_t(const GemmArgs& a, dim3 grid, hipStream_t st) {
         grid = dim3(8 * b.tiles_per_xcd);
       }
     }
-#define G2(F, XM, NX_, MS_) RT_LAUNCH((k_gemm2<MT, KSTEPS, XM, F, NX_, MS_>), grid, dim3(256), lds, st, b)
+#define G2(F, XM, NX_, MS_)                                                               \
+  do {                                                                                    \
+    if (b.q_fmt) RT_LAUNCH((k_gemm2<MT, KSTEPS, XM, F, NX_, MS_, true>), grid, dim3(256), lds, st, b); \
+    else RT_LAUNCH((k_gemm2<MT, KSTEPS, XM, F, NX_, MS_>), grid, dim3(256), lds, st, b);  \
+  } while (0)
     if (a.f16) {
       if (a.xmode == kXPlanes) { if (ms == 2) G2(true, kXPlanes, 1, 2); else if (ms == 1) G2(true, kXPlanes, 1, 1); else G2(true, kXPlanes, 1, 0); }
       else if (a.x_nsplit == 4) G2(true, kXRelu2, 4, 0);
-      else G2(true, kXRelu2, 2, 0);
+      else if (a.x_nsplit == 2) G2(true, kXRelu2, 2, 0);
+      else G2(true, kXRelu2, 1, 0);
     } else {
       if (a.xmode == kXPlanes) { if (ms == 2) G2(false, kXPlanes, 1, 2); else if (ms == 1) G2(false, kXPlanes, 1, 1); else G2(false, kXPlanes, 1, 0); }
       else if (a.x_nsplit == 4) G2(false, kXRelu2, 4, 0);
-      else G2(false, kXRelu2, 2, 0);
+      else if (a.x_nsplit == 2) G2(false, kXRelu2, 2, 0);
+      else G2(false, kXRelu2, 1, 0);
     }
 #undef G2
     return;
@@ -1137,6 +1244,72 @@ __global__ void k_pack_frag(const bf16_t* W, int N, int K, bf16_t* out) {
 
 void launch_pack_frag(const bf16_t* W, int N, int K, bf16_t* out, hipStream_t st) {
   RT_LAUNCH(k_pack_frag, dim3(4096), dim3(256), 0, st, W, N, K, out);
+}
+
+// ------------------------------------------------------------------------------------
+// quant_pack: web-rwkv 0.10.16's Quant::Int8 / Quant::NF4 matrix quantisation, restated (the
+// crate is not vendored: parity unpinned; the oracle restates the same rules independently,
+// oracle/rwkv7.c). One thread per (column n, K-block):
+//  Int8 (128 k): mn = f16(min), mx = f16(max); q = floor(fma(clamp((x - mn) / (mx - mn), 0, 1),
+//    255, 0.5)) (0 when mx == mn); dequantised w = fma(q / 255, mx - mn, mn).
+//  NF4 (64 k): s = f16(max |x|); q = #{i < 15 : x / s > (t[i] + t[i+1]) / 2} (7 when s == 0);
+//    dequantised w = t[q] * s, t = the NormalFloat-4 code table.
+// ------------------------------------------------------------------------------------
+__device__ inline float f16_round(float x) { return (float)(_Float16)x; }
+// byte offset of element (n, k) in the fragment order, for e-byte lanes (int8: 8 per lane)
+__device__ inline int64_t frag_elem(int n, int k, int K) {
+  const int nb = n >> 4, li = n & 15, kb = k >> 5, g = (k >> 3) & 3, e = k & 7;
+  return (((int64_t)nb * (K >> 5) + kb) * 64 + 16 * g + li) * 8 + e;
+}
+template <int QT>
+__global__ void k_quant_pack(const uint16_t* W, int N, int K, int f16, uint8_t* codes, void* scales) {
+  constexpr int BS = QT == 1 ? kQ8Block : kQ4Block;
+  const int nkb = K / BS;
+  const int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= (int64_t)N * nkb) return;
+  const int n = (int)(id / nkb), kb = (int)(id % nkb);
+  const uint16_t* row = W + (int64_t)n * K + kb * BS;
+  auto at = [&](int i) { return f16 ? h16_to_f32(row[i]) : bf16_to_f32(row[i]); };
+  if constexpr (QT == 1) {
+    float lo = at(0), hi = at(0);
+    for (int i = 1; i < BS; ++i) { lo = fminf(lo, at(i)); hi = fmaxf(hi, at(i)); }
+    const float mn = f16_round(lo), mx = f16_round(hi), d = mx - mn;
+    for (int i = 0; i < BS; ++i) {
+      uint32_t q = 0;
+      if (mx != mn) {
+        const float v = fminf(fmaxf((at(i) - mn) / d, 0.0f), 1.0f);
+        q = (uint32_t)floorf(fmaf(v, 255.0f, 0.5f));
+      }
+      codes[frag_elem(n, kb * BS + i, K)] = (uint8_t)q;
+    }
+    ((uint32_t*)scales)[id] = (uint32_t)f32_to_h16(mn) | ((uint32_t)f32_to_h16(mx) << 16);
+  } else {
+    float am = 0.0f;
+    for (int i = 0; i < BS; ++i) am = fmaxf(am, fabsf(at(i)));
+    const float sc = f16_round(am);
+    for (int i = 0; i < BS; i += 2) {
+      uint32_t q2[2];
+      for (int u = 0; u < 2; ++u) {
+        uint32_t q = 7;
+        if (sc != 0.0f) {
+          const float v = at(i + u) / sc;
+          q = 0;
+          for (int t = 0; t < 15; ++t) q += v > 0.5f * (kNF4[t] + kNF4[t + 1]) ? 1u : 0u;
+        }
+        q2[u] = q;
+      }
+      // nibble pair (k, k + 1) = byte (frag_elem / 2): low nibble the even k
+      codes[frag_elem(n, kb * BS + i, K) >> 1] = (uint8_t)(q2[0] | (q2[1] << 4));
+    }
+    ((uint16_t*)scales)[id] = f32_to_h16(sc);
+  }
+}
+
+void launch_quant_pack(const uint16_t* W, int N, int K, int f16, int qt, uint8_t* codes, void* scales, hipStream_t st) {
+  const int64_t n = (int64_t)N * (K / (qt == 1 ? kQ8Block : kQ4Block));
+  const dim3 grid((unsigned)((n + 255) / 256));
+  if (qt == 1) hipLaunchKernelGGL(k_quant_pack<1>, grid, dim3(256), 0, st, W, N, K, f16, codes, scales);
+  else hipLaunchKernelGGL(k_quant_pack<2>, grid, dim3(256), 0, st, W, N, K, f16, codes, scales);
 }
 
 __global__ void k_pack_lora(const bf16_t* w2t, const bf16_t* a2t, const bf16_t* v2t, const bf16_t* g2t, int C,

@@ -34,7 +34,11 @@ class Dims(ctypes.Structure):
 class EngineDesc(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("max_slots", ctypes.c_int32),
                 ("token_chunk_size", ctypes.c_int32), ("use_graphs", ctypes.c_int32),
-                ("wkv_variant", ctypes.c_int32)]
+                ("wkv_variant", ctypes.c_int32), ("quant_layers", ctypes.c_int32),
+                ("quant_type", ctypes.c_int32)]
+
+
+QUANT_NONE, QUANT_INT8, QUANT_NF4, QUANT_SF4 = 0, 1, 2, 3
 
 
 class Input(ctypes.Structure):
@@ -172,6 +176,7 @@ def lib():
 
 class RwkvTtsError(RuntimeError):
     def __init__(self, rc, where):
+        self.code = rc
         msg = lib().rwkvtts_last_error()
         super().__init__(f"{where} failed ({rc}): {msg.decode() if msg else ''}")
         self.rc = rc

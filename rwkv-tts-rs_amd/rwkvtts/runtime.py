@@ -125,16 +125,38 @@ def _unpack_results(res, sem_bufs):
     return out, status
 
 
+def parse_quant_type(s) -> int:
+    """bin/server.rs:1029-1056 (parse_quant_type): none / int8 / nf4 / sf4, case-insensitive;
+    anything else is an error. SF4 parses but the engine rejects it (table not available)."""
+    if isinstance(s, int):
+        return s
+    t = {"none": _ffi.QUANT_NONE, "int8": _ffi.QUANT_INT8, "nf4": _ffi.QUANT_NF4, "sf4": _ffi.QUANT_SF4}.get(str(s).lower())
+    if t is None:
+        raise ValueError(f"unsupported quant type: {s}. supported: none, int8, nf4, sf4")
+    return t
+
+
+def quant_config(quant_layers: int, quant_type) -> tuple:
+    """bin/server.rs:1059-1071 (create_quant_config): layers [0, quant_layers) quantised, or none."""
+    t = parse_quant_type(quant_type)
+    if quant_layers <= 0 or t == _ffi.QUANT_NONE:
+        return 0, _ffi.QUANT_NONE
+    return int(quant_layers), t
+
+
 class SharedRwkvRuntime:
-    """One engine per GPU: weights resident in HBM, `max_concurrent_batches` state slots."""
+    """One engine per GPU: weights resident in HBM, `max_concurrent_batches` state slots.
+    quant_layers / quant_type: the server's --quant-layers / --quant-type (web-rwkv Quant)."""
 
     def __init__(self, weights: np.ndarray, device: int = 0, max_slots: int = 10,
                  token_chunk_size: int = 512, use_graphs: bool = True, weights_on_device: bool = False,
-                 device_ptr: Optional[int] = None, wkv_variant: int = 0):
+                 device_ptr: Optional[int] = None, wkv_variant: int = 0, quant_layers: int = 0,
+                 quant_type="none"):
         # the C ABI serialises calls per engine; this lock also keeps Python-side buffers of one
         # call from interleaving with another thread's
         self._lock = threading.RLock()
-        desc = _ffi.EngineDesc(device, max_slots, token_chunk_size, 1 if use_graphs else 0, wkv_variant)
+        ql, qt = quant_config(quant_layers, quant_type)
+        desc = _ffi.EngineDesc(device, max_slots, token_chunk_size, 1 if use_graphs else 0, wkv_variant, ql, qt)
         h = ctypes.c_void_p()
         if device_ptr is not None:
             check(lib().rwkvtts_engine_create(ctypes.byref(desc), ctypes.c_void_p(device_ptr),
@@ -343,7 +365,8 @@ class DynamicBatchManager:
 
     def __init__(self, weights: np.ndarray, config: Optional[DynamicBatchConfig] = None,
                  devices: Sequence[int] = (0,), max_slots: int = 32, token_chunk_size: int = 512,
-                 use_graphs: bool = True, wkv_variant: int = 0, tokenizer=None):
+                 use_graphs: bool = True, wkv_variant: int = 0, tokenizer=None, quant_layers: int = 0,
+                 quant_type="none"):
         self.config = config or DynamicBatchConfig()
         devices = list(devices)
         if not 1 <= len(devices) <= _ffi.MAX_ENGINES:
@@ -352,7 +375,8 @@ class DynamicBatchManager:
         d.n_engines = len(devices)
         for i, dev in enumerate(devices):
             d.devices[i] = dev
-        d.engine = _ffi.EngineDesc(0, max_slots, token_chunk_size, 1 if use_graphs else 0, wkv_variant)
+        ql, qt = quant_config(quant_layers, quant_type)
+        d.engine = _ffi.EngineDesc(0, max_slots, token_chunk_size, 1 if use_graphs else 0, wkv_variant, ql, qt)
         d.max_batch_size = self.config.max_batch_size
         d.collect_timeout_ms = self.config.collect_timeout_ms
         w = np.ascontiguousarray(weights)

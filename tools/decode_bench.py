@@ -2,7 +2,8 @@
 replay. Prints decode ms/step from the engine's own HIP events and a token checksum (a kernel
 change that keeps the arithmetic must keep the checksum). Usage: decode_bench.py [S] [reps].
 Env: DB_B requests (default 32), DB_F16=1 fp16 weights, DB_ZS=1 zero-shot prompts (32 reference
-global tokens + 128 reference semantic tokens per request)."""
+global tokens + 128 reference semantic tokens per request), DB_QUANT=int8|nf4 (every layer quantised,
+the server's --quant-layers 24 --quant-type ...)."""
 import hashlib
 import os
 import sys
@@ -19,7 +20,9 @@ f16 = os.environ.get("DB_F16", "0") == "1"
 B = int(os.environ.get("DB_B", "32"))
 zs = os.environ.get("DB_ZS", "0") == "1"
 blob = W.synth_blob(W.DIMS_04B, seed=20251205, **({"dtype": rwkvtts._ffi.DTYPE_F16} if f16 else {}))
-rt = rwkvtts.SharedRwkvRuntime(blob, max_slots=max(B, 1), token_chunk_size=512, use_graphs=True)
+qt = os.environ.get("DB_QUANT", "none")
+rt = rwkvtts.SharedRwkvRuntime(blob, max_slots=max(B, 1), token_chunk_size=512, use_graphs=True,
+                               quant_layers=W.DIMS_04B["n_layer"] if qt != "none" else 0, quant_type=qt)
 del blob
 import numpy as np  # noqa: E402
 reqs = []
@@ -39,7 +42,7 @@ for r in range(reps):
     st = rt.stats()
     h = hashlib.sha1(repr(out).encode()).hexdigest()[:12]
     us = st['decode_ms'] / max(st['steps'], 1) * 1000
-    print(f"rep {r}: B={B} f16={int(f16)} zs={int(zs)} decode {us:.1f} us/step over {st['steps']} steps "
+    print(f"rep {r}: B={B} f16={int(f16)} zs={int(zs)} quant={qt} decode {us:.1f} us/step over {st['steps']} steps "
           f"({B * 320 / us * 1e6:.0f} samples/s decode-only), "
           f"prefill {st['prefill_ms']:.2f} ms, wall {wall * 1000:.1f} ms, tokens {h}", flush=True)
 rt.close()
