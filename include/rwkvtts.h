@@ -163,7 +163,7 @@ typedef struct {
 } rwkvtts_engine_desc;
 
 #define RWKVTTS_QUANT_NONE 0
-#define RWKVTTS_QUANT_INT8 1 /* 128-element blocks along K: f16 (min, max), u8 q; w = min + q/255 (max - min) */
+#define RWKVTTS_QUANT_INT8 1 /* 128-element blocks along K: f16 (min, max), u8 q; w = min + q (max - min)/255 */
 #define RWKVTTS_QUANT_NF4 2  /* 64-element blocks along K: f16 absmax, 4-bit NormalFloat index; w = nf4[q] absmax */
 #define RWKVTTS_QUANT_SF4 3  /* rejected (RWKVTTS_EUNSUPPORTED): its code table is not available offline */
 

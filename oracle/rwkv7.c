@@ -72,7 +72,7 @@ void oracle_set_threads(int n) { g_threads = n; }
  * so this restates its published block quantisers (parity unpinned):
  *   Int8: blocks of 128 consecutive elements of a row (along K); mn = f16(min), mx = f16(max);
  *     q = floor(fma(clamp((x - mn) / (mx - mn), 0, 1), 255, 0.5)) (0 when mx == mn);
- *     w = fma(q / 255, mx - mn, mn)                         (unpack4x8unorm(q) = q / 255)
+ *     w = fma(q, (mx - mn) / 255, mn)               (min + unpack4x8unorm(q) * (max - min))
  *   NF4: blocks of 64; s = f16(max |x|); q = #{i < 15 : x / s > (t[i] + t[i+1]) / 2}
  *     (7 when s == 0); w = t[q] * s, t = the NormalFloat-4 table.
  * f16(.) is round-to-nearest-even. */
@@ -125,7 +125,7 @@ static float* quant_matrix(const oracle_model* m, const uint16_t* W, int N, int 
             v = fminf(fmaxf(v, 0.0f), 1.0f);
             q = (unsigned)floorf(fmaf(v, 255.0f, 0.5f));
           }
-          dst[i] = fmaf((float)q / 255.0f, d, mn);
+          dst[i] = fmaf((float)q, d / 255.0f, mn);
         }
       } else {
         float am = 0.0f;

@@ -563,7 +563,7 @@ template <int MT, int KSTEPS, int XMODE, bool F16, int NX, int MS, bool QW = fal
 __global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ uint32_t s_rexp[MT * 16];  // f16 relu^2 rows: bits of the row maximum if >= 2^15
-  __shared__ float s_qlut[QW ? 256 + 16 : 1];  // QW: q / 255 (int8), then the NF4 table
+  __shared__ float s_qlut[QW ? 16 : 1];  // QW: the NF4 code table
   constexpr int KS = KSTEPS * 32;
   constexpr int LD = KS + 8;
   constexpr int ROWS = MT * 16;
@@ -647,8 +647,7 @@ __global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
   uint2 bq8[QW ? KSTEPS : 1];
   uint32_t bq4[QW ? KSTEPS : 1], qsc[QW ? KSTEPS : 1];
   if constexpr (QW) {
-    if (threadIdx.x < 256) s_qlut[threadIdx.x] = (float)threadIdx.x / 255.0f;
-    if (threadIdx.x < 16) s_qlut[256 + threadIdx.x] = kNF4[threadIdx.x];
+    if (threadIdx.x < 16) s_qlut[threadIdx.x] = kNF4[threadIdx.x];
   }
   auto load_x = [&]() {
   if constexpr (XMODE == kXPlanes) {
@@ -774,16 +773,16 @@ __global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
         float w[8];
         if (qf == 1) {
           const float mn = h16_to_f32((uint16_t)(qsc[t] & 0xFFFFu)), mx = h16_to_f32((uint16_t)(qsc[t] >> 16));
-          const float d = mx - mn;
+          const float step = (mx - mn) / 255.0f;
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             const uint32_t q = ((e < 4 ? bq8[t].x : bq8[t].y) >> (8 * (e & 3))) & 255u;
-            w[e] = fmaf(s_qlut[q], d, mn);
+            w[e] = fmaf((float)q, step, mn);
           }
         } else {
           const float sc = h16_to_f32((uint16_t)qsc[t]);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) w[e] = s_qlut[256 + ((bq4[t] >> (4 * e)) & 15u)] * sc;
+          for (int e = 0; e < 8; ++e) w[e] = s_qlut[(bq4[t] >> (4 * e)) & 15u] * sc;
         }
         if constexpr (F16) {
           const float up = __builtin_amdgcn_ldexpf(1.0f, a.q_shift);
@@ -1251,7 +1250,7 @@ void launch_pack_frag(const bf16_t* W, int N, int K, bf16_t* out, hipStream_t st
 // crate is not vendored: parity unpinned; the oracle restates the same rules independently,
 // oracle/rwkv7.c). One thread per (column n, K-block):
 //  Int8 (128 k): mn = f16(min), mx = f16(max); q = floor(fma(clamp((x - mn) / (mx - mn), 0, 1),
-//    255, 0.5)) (0 when mx == mn); dequantised w = fma(q / 255, mx - mn, mn).
+//    255, 0.5)) (0 when mx == mn); dequantised w = fma(q, (mx - mn) / 255, mn).
 //  NF4 (64 k): s = f16(max |x|); q = #{i < 15 : x / s > (t[i] + t[i+1]) / 2} (7 when s == 0);
 //    dequantised w = t[q] * s, t = the NormalFloat-4 code table.
 // ------------------------------------------------------------------------------------
