@@ -459,6 +459,7 @@ __device__ float exact_seq_sum(const SampleSmem& sm, int n, uint64_t* stamps = n
       sT1[j] = sm.sub_t[2 * (NS * lane + j) + 1];
       sE[j] = sm.sub_e[NS * lane + j];
     }
+    uint64_t sadd_cyc = 0;  // diagnostics (stamps): cycles in element-wise fallback adds
     // chunk c in order: each sub-chunk by its map when s is in the binade it was simulated for
     // and stays there, otherwise element by element on one lane
     auto add_chunk = [&](float s, int c) -> float {
@@ -485,7 +486,7 @@ __device__ float exact_seq_sum(const SampleSmem& sm, int n, uint64_t* stamps = n
             const uint64_t fb = stamps ? __builtin_amdgcn_s_memtime() : 0;
             if (lane == 0) t = lane_serial_add<NE>(s, sm.p, b1, e1);
             s = readlane_f(t, 0);
-            if (stamps && tid == 0) stamps[15] += __builtin_amdgcn_s_memtime() + (uint64_t)(s != s) - fb;
+            if (stamps) sadd_cyc += __builtin_amdgcn_s_memtime() + (uint64_t)(s != s) - fb;
           }
         }
       }
@@ -538,7 +539,10 @@ __device__ float exact_seq_sum(const SampleSmem& sm, int n, uint64_t* stamps = n
     }
     if (tid == 0) {
       sm.fred[16] = s;
-      if (stamps) stamps[14] = nfast;
+      if (stamps) {
+        stamps[14] = nfast;
+        stamps[15] = sadd_cyc;
+      }
     }
   } else {
     other();
@@ -625,6 +629,7 @@ __device__ __attribute__((always_inline)) int sample_fast(const SampleSmem& sm, 
   }
   __syncthreads();
   STAMP(5);
+  STAMP(6);
   // top-p over the sorted survivors (all p >= P > 0): wave 0, sequential cumulative
   if (tid < 64) {
     int m = top_k, found = 0, ceq = 0;
@@ -674,6 +679,7 @@ __device__ __attribute__((always_inline)) int sample_fast(const SampleSmem& sm, 
   }
   __syncthreads();
   STAMP(7);
+  STAMP(8);
   if (tid < 64) {
     const int found = sm.ired[2], ceq = sm.ired[3];
     const float cutoff = sm.fred[17];
