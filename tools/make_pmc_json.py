@@ -9,10 +9,10 @@ from collections import defaultdict
 
 # (kernel symbol prefix, grid size) of each decode-step launch at 32 rows (0.4B dims)
 DECODE = {
-    "gemm_rkv_lora": ("k_gemm2<2, 8, 0, false, 1, 2>", 54272),
-    "gemm_ffn_key": ("k_gemm2<2, 8, 0, false, 1, 0>", 65536),
-    "gemm_wo": ("k_gemm2<2, 4, 0, false, 1, 0>", 32768),
-    "gemm_ffn_value": ("k_gemm2<2, 8, 1, false, 4, 0>", 65536),
+    "gemm_rkv_lora": ("k_gemm2<2, 8, 0, false, 1, 2, false>", 54272),
+    "gemm_ffn_key": ("k_gemm2<2, 8, 0, false, 1, 0, false>", 65536),
+    "gemm_wo": ("k_gemm2<2, 4, 0, false, 1, 0, false>", 32768),
+    "gemm_ffn_value": ("k_gemm2<2, 8, 1, false, 4, 0, false>", 65536),
     "wkv": ("k_wkv6<false>", 131072),
     "ln_mix_att": ("k_ln1024<false, 1, 6, 16>", 8192),
     "ln_mix_ffn": ("k_ln1024<false, 1, 1, 8>", 8192),
