@@ -9,11 +9,10 @@ decode_audio_batch (a failed item decodes to an empty array there, as the refere
 spawn_blocking tasks return vec![]).
 
 The voice store lookup by voice_id inside the pipeline (`VoiceFeatureManager::new("./raf")`,
-:751) is kept as a RAF-JSON read from `raf_dir` (the server passes the tokens
-directly instead).
+:751) goes through `voices.VoiceFeatureManager` on `raf_dir` (the server passes the
+tokens directly instead).
 """
 import dataclasses
-import json
 import os
 from typing import List, Optional, Sequence
 
@@ -76,10 +75,11 @@ class LightweightTtsPipeline:
         return convert_standard_properties_to_tokens(args.age, args.gender, args.emotion, args.pitch, args.speed)
 
     def _voice_tokens(self, voice_id: str):
-        path = os.path.join(self.raf_dir, f"{voice_id}.raf.json")
-        with open(path, encoding="utf-8") as f:
-            raf = json.load(f)
-        return list(raf["global_tokens"]), list(raf["semantic_tokens"])
+        """VoiceFeatureManager::new(raf_dir).get_voice_tokens (:751-760; checksum verified)."""
+        from .voices import VoiceFeatureManager
+        if getattr(self, "_voices", None) is None:
+            self._voices = VoiceFeatureManager(self.raf_dir)
+        return self._voices.get_voice_tokens(voice_id)
 
     def process_reference_audio(self, ref_audio_path: str):
         if not ref_audio_path or not os.path.exists(ref_audio_path):

@@ -9,7 +9,12 @@
   token is always 7), the voice lookup by voice_id (:481-515, a RAF JSON under `voice_dir`).
 * `handle_tts_json(body, pipeline, voice_dir)` returns (HTTP status, JSON dict) exactly as the
   handler renders them; `create_app` wires it to POST /api/tts with FastAPI when installed.
-The web UI, voice-extraction / storage routes and model download are out of scope.
+* The voice-clone routes (:777-979, routes :1448-1450) over the RAF store (`voices.py`,
+  VoiceFeatureManager): `handle_voice_list`, `handle_voice_delete`, `handle_voice_extract`
+  (multipart voice_name / prompt_text / audio_file; the feature extraction needs the
+  BiCodecTokenize + wav2vec2 encoders, whose graphs are absent: a pipeline may supply
+  `reference_tokenizer`, otherwise the route answers the reference's extraction-failure body).
+The embedded web UI and model download are out of scope.
 """
 import base64
 import json
@@ -75,13 +80,22 @@ def map_pitch(pitch: Optional[str]) -> str:
             "very_high_pitch": "very_high"}.get(pitch, "medium")
 
 
+_MANAGERS = {}
+
+
+def voice_manager(voice_dir: str):
+    """One VoiceFeatureManager per RAF directory (the server's AppState.voice_manager)."""
+    from .voices import VoiceFeatureManager
+    m = _MANAGERS.get(voice_dir)
+    if m is None:
+        m = _MANAGERS[voice_dir] = VoiceFeatureManager(voice_dir)
+    return m
+
+
 def load_voice_feature(voice_dir: str, voice_id: str) -> dict:
-    with open(os.path.join(voice_dir, f"{voice_id}.raf.json"), encoding="utf-8") as f:
-        raf = json.load(f)
-    for k in ("global_tokens", "semantic_tokens"):
-        if k not in raf:
-            raise ValueError(f"voice feature file lacks {k}")
-    return raf
+    """VoiceFeatureManager::load_voice_feature (checksum verified, cached)."""
+    vf = voice_manager(voice_dir).load_voice_feature(voice_id)
+    return dict(vf.__dict__)
 
 
 def handle_tts_json(body, pipeline, voice_dir: str = "assets/raf") -> Tuple[int, dict]:
@@ -124,6 +138,66 @@ def handle_tts_json(body, pipeline, voice_dir: str = "assets/raf") -> Tuple[int,
                  "duration_ms": int(total * 1000), "rtf": calculate_rtf(audio, total)}
 
 
+def handle_voice_list(voice_dir: str = "assets/raf") -> Tuple[int, dict]:
+    """:920-944: {success, voices: [VoiceMetadata]} (an unreadable store: success false, [])."""
+    try:
+        voices = voice_manager(voice_dir).list_voices()
+        return 200, {"success": True, "voices": [dict(v.__dict__) for v in voices]}
+    except (OSError, ValueError, KeyError):
+        return 200, {"success": False, "voices": []}
+
+
+def handle_voice_delete(body, voice_dir: str = "assets/raf") -> Tuple[int, dict]:
+    """:946-979: JSON {voice_id} -> {success, message}."""
+    try:
+        if isinstance(body, (bytes, str)):
+            body = json.loads(body)
+        voice_id = body["voice_id"]
+        if not isinstance(voice_id, str):
+            raise TypeError
+    except (ValueError, KeyError, TypeError):
+        return 200, {"success": False, "message": "请求格式错误"}
+    try:
+        voice_manager(voice_dir).delete_voice(voice_id)
+        return 200, {"success": True, "message": "音色删除成功"}
+    except (OSError, ValueError) as e:
+        return 200, {"success": False, "message": f"删除音色失败: {e}"}
+
+
+def handle_voice_extract(form: Optional[dict], audio_path: Optional[str], pipeline=None,
+                         voice_dir: str = "assets/raf", is_multipart: bool = True) -> Tuple[int, dict]:
+    """:777-918. form: voice_name / prompt_text; audio_path: the uploaded audio_file saved to a
+    temporary path (None: no file). Extraction = pipeline.reference_tokenizer(path) ->
+    (global, semantic) (the BiCodecTokenize encoders), duration / rate from the WAV itself."""
+    def fail(msg):
+        return 200, {"success": False, "message": msg, "voice_id": None}
+    if not is_multipart:
+        return fail("需要上传音频文件")
+    form = form or {}
+    name, prompt = form.get("voice_name") or "", form.get("prompt_text") or ""
+    if not name:
+        return fail("音色名称不能为空")
+    if not prompt:
+        return fail("提示词不能为空")
+    if not audio_path:
+        return fail("未找到音频文件")
+    try:
+        tok = getattr(pipeline, "reference_tokenizer", None)
+        if tok is None:
+            raise RuntimeError("ONNX模型文件不存在: assets/model/BiCodecTokenize.onnx")
+        g, sem = tok(audio_path)
+        from .audio import read_wav
+        x, sr, ch = read_wav(audio_path)
+        duration = (x.size // max(ch, 1)) / float(sr)
+    except Exception as e:  # noqa: BLE001 -- the reference renders every extraction error this way
+        return fail(f"音频特征提取失败: {e}")
+    try:
+        vid = voice_manager(voice_dir).save_voice_feature(name, prompt, list(g), list(sem), duration, sr)
+    except (OSError, ValueError) as e:
+        return fail(f"音色特征提取失败: {e}")
+    return 200, {"success": True, "message": "音色特征提取成功", "voice_id": vid}
+
+
 def create_app(pipeline, voice_dir: str = "assets/raf"):
     """FastAPI app with POST /api/tts (server.rs:1447). Serve with uvicorn."""
     from fastapi import FastAPI, Request
@@ -136,6 +210,41 @@ def create_app(pipeline, voice_dir: str = "assets/raf"):
         import anyio
         body = await request.body()
         code, payload = await anyio.to_thread.run_sync(handle_tts_json, body, pipeline, voice_dir)
+        return JSONResponse(payload, status_code=code)
+
+    @app.get("/api/voice-clone/list")
+    async def api_voice_list():
+        code, payload = handle_voice_list(voice_dir)
+        return JSONResponse(payload, status_code=code)
+
+    @app.post("/api/voice-clone/delete")
+    async def api_voice_delete(request: Request):
+        code, payload = handle_voice_delete(await request.body(), voice_dir)
+        return JSONResponse(payload, status_code=code)
+
+    @app.post("/api/voice-clone/extract")
+    async def api_voice_extract(request: Request):
+        import anyio
+        import tempfile
+        ctype = request.headers.get("content-type", "")
+        if not ctype.startswith("multipart/"):
+            return JSONResponse(handle_voice_extract(None, None, pipeline, voice_dir, is_multipart=False)[1])
+        form = await request.form()
+        fields = {k: v for k, v in form.items() if isinstance(v, str)}
+        up = form.get("audio_file")
+        path = None
+        if up is not None and not isinstance(up, str):
+            ext = os.path.splitext(up.filename or "audio")[1] or ".wav"
+            tmp_dir = os.path.join(voice_dir, "temp", "upload_temp_files")
+            os.makedirs(tmp_dir, exist_ok=True)
+            fd, path = tempfile.mkstemp(suffix=ext, dir=tmp_dir)
+            with os.fdopen(fd, "wb") as f:
+                f.write(await up.read())
+        try:
+            code, payload = await anyio.to_thread.run_sync(handle_voice_extract, fields, path, pipeline, voice_dir)
+        finally:
+            if path and os.path.exists(path):
+                os.remove(path)
         return JSONResponse(payload, status_code=code)
 
     return app

@@ -80,10 +80,9 @@ def test_handler_normal_and_zero_shot(tmp_path):
     assert req.args.seed == 3 and req.args.top_k == 100 and req.args.max_tokens == 8000
     # zero-shot by voice_id: RAF tokens passed, no property tokens
     raf = json.load(open(os.path.join(HERE, "golden", "raf_voice_05d8f5ed.json")))
-    (tmp_path / "v1.raf.json").write_text(json.dumps({"global_tokens": raf["global_tokens"],
-                                                      "semantic_tokens": raf["semantic_tokens"][:9],
-                                                      "prompt_text": "x"}))
-    code, body = SV.handle_tts_json({"text": "hi", "voice_id": "v1"}, pipe, str(tmp_path))
+    vid = SV.voice_manager(str(tmp_path)).save_voice_feature("v1", "x", raf["global_tokens"],
+                                                              raf["semantic_tokens"][:9], 1.5, 16000)
+    code, body = SV.handle_tts_json({"text": "hi", "voice_id": vid}, pipe, str(tmp_path))
     assert code == 200
     req = m.seen[-1]
     assert req.property_tokens == [] and req.ref_global_tokens == raf["global_tokens"]
@@ -111,3 +110,40 @@ def test_fastapi_route():
     app = SV.create_app(LightweightTtsPipeline(FakeManager(), FakeCodec()))
     r = TestClient(app).post("/api/tts", json={"text": "hello"})
     assert r.status_code == 200 and r.json()["success"]
+
+
+def test_fastapi_voice_routes(tmp_path):
+    pytest.importorskip("fastapi")
+    from fastapi.testclient import TestClient
+
+    class Pipe(LightweightTtsPipeline):
+        @staticmethod
+        def reference_tokenizer(path):
+            return list(range(32)), [1, 2]
+    c = TestClient(SV.create_app(Pipe(FakeManager(), FakeCodec()), voice_dir=str(tmp_path)))
+    assert c.get("/api/voice-clone/list").json() == {"success": True, "voices": []}
+    assert c.post("/api/voice-clone/extract", data={"voice_name": "n"}).json()["message"] == "需要上传音频文件"
+    try:  # multipart parsing needs python-multipart (not installed in every image)
+        import multipart  # noqa: F401
+        have_mp = True
+    except ImportError:
+        have_mp = False
+    if have_mp:
+        import io
+        import wave
+        buf = io.BytesIO()
+        with wave.open(buf, "wb") as w:
+            w.setnchannels(1)
+            w.setsampwidth(2)
+            w.setframerate(16000)
+            w.writeframes(b"\x10\x00" * 3200)
+        r = c.post("/api/voice-clone/extract", data={"voice_name": "n", "prompt_text": "p"},
+                   files={"audio_file": ("ref.wav", buf.getvalue(), "audio/wav")}).json()
+        assert r["success"], r
+        vid = r["voice_id"]
+        assert not os.listdir(tmp_path / "temp" / "upload_temp_files")  # upload temp removed
+    else:
+        vid = SV.voice_manager(str(tmp_path)).save_voice_feature("n", "p", list(range(32)), [1, 2], 0.2, 16000)
+    assert [v["id"] for v in c.get("/api/voice-clone/list").json()["voices"]] == [vid]
+    assert c.post("/api/voice-clone/delete", json={"voice_id": vid}).json()["success"]
+    assert c.get("/api/voice-clone/list").json()["voices"] == []
