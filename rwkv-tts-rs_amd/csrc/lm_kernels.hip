@@ -1821,6 +1821,9 @@ __global__ __launch_bounds__(256) void k_wkv6(WkvArgs a) {
   }
   const int C = a.C, c = h * N + i;
   tl_begin(a.tl);
+  // debug phase stamps (as k_wkv4: RWKVTTS_WKV_STAMPS, layer 5 only; null in production)
+  uint64_t* stp = (a.stamps && t == 0) ? a.stamps + ((int64_t)h * a.n_seg + seg_i) * 8 : nullptr;
+  if (stp) { stp[0] = __builtin_amdgcn_s_memrealtime(); stp[1] = __builtin_amdgcn_s_memtime(); }
   const int4 sg = a.segs[seg_i];
   const float w0 = a.w0[c], a0 = a.a0[c], v0 = a.v0[c], kkc = a.k_k[c], kac = a.k_a[c];
   const float rkc = a.r_k[c], lnw = a.lnx_w[c], lnb = a.lnx_b[c];
@@ -1890,6 +1893,7 @@ __global__ __launch_bounds__(256) void k_wkv6(WkvArgs a) {
       v += vp[p];
     }
     __syncthreads();
+    if (stp && rr == 0) stp[2] = __builtin_amdgcn_s_memtime() + (uint64_t)(r != r);
     float2_ l0 = {0.f, 0.f}, l1 = {0.f, 0.f}, l2 = {0.f, 0.f}, l3 = {0.f, 0.f};
     auto dot = [&](float2_ acc, const uint4 q, const float* hsrc) {
       const float4_ h0 = *(const float4_*)hsrc;
@@ -1927,6 +1931,7 @@ __global__ __launch_bounds__(256) void k_wkv6(WkvArgs a) {
       s_vec[0][i] = w; s_vec[1][i] = kk; s_vec[2][i] = av; s_vec[3][i] = k; s_vec[4][i] = r;
     }
     __syncthreads();
+    if (stp && rr == 0) stp[3] = __builtin_amdgcn_s_memtime();
     const float inv =
         __builtin_amdgcn_rcpf(fmaxf(sqrtf((s_red[0][0] + s_red[0][1]) + (s_red[0][2] + s_red[0][3])), 1e-12f));
     const float bonus = (s_red[1][0] + s_red[1][1]) + (s_red[1][2] + s_red[1][3]);
@@ -1968,6 +1973,7 @@ __global__ __launch_bounds__(256) void k_wkv6(WkvArgs a) {
         for (int q = 0; q < 4; ++q) Srow[q * 256] = S4[q];
       }
     }
+    if (stp && rr == 0) stp[4] = __builtin_amdgcn_s_memtime() + (uint64_t)(y2[0] != y2[0]);
     const float y = quad_sum(y2[0] + y2[1]);
     {
       const float s1 = wave_sum(qq == 0 ? y : 0.f);
@@ -1975,6 +1981,7 @@ __global__ __launch_bounds__(256) void k_wkv6(WkvArgs a) {
       if (lane == 0) { s_red[2][wave] = s1; s_red[3][wave] = s2; }
     }
     __syncthreads();
+    if (stp && rr == 0) stp[5] = __builtin_amdgcn_s_memtime();
     const float mean = ((s_red[2][0] + s_red[2][1]) + (s_red[2][2] + s_red[2][3])) * (1.0f / N);
     const float var =
         fmaxf(((s_red[3][0] + s_red[3][1]) + (s_red[3][2] + s_red[3][3])) * (1.0f / N) - mean * mean, 0.f);
@@ -1984,6 +1991,7 @@ __global__ __launch_bounds__(256) void k_wkv6(WkvArgs a) {
     }
     if (rr + 1 < n_rows) __syncthreads();
   }
+  if (stp) { stp[6] = __builtin_amdgcn_s_memtime(); stp[7] = __builtin_amdgcn_s_memrealtime(); }
   tl_end(a.tl);
 }
 

@@ -1,4 +1,4 @@
-"""WKV (k_wkv4) phase breakdown: runs 32 requests through the engine with RWKVTTS_WKV_STAMPS set
+"""WKV (k_wkv6 by default; RWKVTTS_WKV_VARIANT-style env of the engine picks k_wkv4) phase breakdown: runs 32 requests through the engine with RWKVTTS_WKV_STAMPS set
 (layer 5 of the last decode step records per-workgroup stamps) and prints the launch-wide span,
 the workgroup start ramp and mean / max core-clock cycles per phase."""
 import os
