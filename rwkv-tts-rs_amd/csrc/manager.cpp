@@ -240,7 +240,16 @@ class Manager {
       const auto collect_start = Clock::now();
       pending.clear();
       while (true) {
-        const bool got = q_cv_.wait_for(lk, tmo, [&] { return !queue_.empty() || closing_; }) && !queue_.empty();
+        // (a zero collect timeout with nothing pending would spin, as the reference's
+        // timeout(0) does; wait for the first request without a timeout instead -- same batches)
+        const auto ready = [&] { return !queue_.empty() || closing_; };
+        bool got;
+        if (pending.empty() && tmo.count() == 0) {
+          q_cv_.wait(lk, ready);
+          got = !queue_.empty();
+        } else {
+          got = q_cv_.wait_for(lk, tmo, ready) && !queue_.empty();
+        }
         if (got) {
           pending.push_back(queue_.front());
           queue_.pop_front();
