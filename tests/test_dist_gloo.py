@@ -41,8 +41,9 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_gloo_world2_shard_broadcast_reduce():
-    world, port = 2, _free_port()
+@pytest.mark.parametrize("world", [2, 4])
+def test_gloo_shard_broadcast_reduce(world):
+    port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
@@ -54,9 +55,9 @@ def test_gloo_world2_shard_broadcast_reduce():
         assert p.exitcode == 0
     expect = int(np.random.default_rng(7).integers(0, 256, 4096, dtype=np.uint8).astype(np.int64).sum())
     assert all(o[1] == expect for o in out)                     # identical weights everywhere
-    assert out[0][2] == [0, 2, 4, 6, 8] and out[1][2] == [1, 3, 5, 7, 9]
+    assert [o[2] for o in out] == [list(range(r, 10, world)) for r in range(world)]  # round-robin shards
     assert D.unshard([o[3] for o in out]) == [x * x for x in range(10)]
-    assert all(o[4] == 1.5 and o[5] == 10 for o in out)           # max time, summed count
+    assert all(o[4] == 0.5 + (world - 1) and o[5] == 10 for o in out)  # max time, summed count
 
 
 def test_shard_unshard_roundtrip():
