@@ -19,8 +19,11 @@ __host__ __device__ inline uint64_t exp2_tab(int i) {
   return kExp2Tab[i];
 }
 
-// glibc expf for x <= 0 (and NaN / -inf). sysdeps/ieee754/flt-32/e_expf.c algorithm.
-__host__ __device__ inline float glibc_expf(float x) {
+// glibc expf for x <= 0 (and NaN / -inf). sysdeps/ieee754/flt-32/e_expf.c algorithm. `tab`:
+// the 32-entry 2^(i/32) table (exp2_tab) -- on the device a copy in LDS, so that the per-element
+// gather is a conflict-free LDS read instead of a dependent global load.
+template <typename Tab>
+__host__ __device__ inline float glibc_expf_t(float x, const Tab& tab) {
   if (x == -__builtin_inff()) return 0.0f;
   if (x != x) return x + x;
   if (x < -0x1.9fe368p6f) return 0.0f;  // underflow to +0
@@ -34,7 +37,7 @@ __host__ __device__ inline float glibc_expf(float x) {
   const uint64_t ki = __builtin_bit_cast(uint64_t, kd);
   kd -= SHIFT;
   const double r = __builtin_fma(InvLn2N, xd, -kd);
-  uint64_t t = exp2_tab((int)(ki % 32));
+  uint64_t t = tab((int)(ki % 32));
   t += ki << (52 - 5);
   const double s = __builtin_bit_cast(double, t);
   const double zz = __builtin_fma(C0, r, C1);
@@ -42,6 +45,9 @@ __host__ __device__ inline float glibc_expf(float x) {
   y = __builtin_fma(zz, r * r, y);
   y = y * s;
   return (float)y;
+}
+__host__ __device__ inline float glibc_expf(float x) {
+  return glibc_expf_t(x, [](int i) { return exp2_tab(i); });
 }
 
 

@@ -199,7 +199,7 @@ __device__ inline float prefix64(float s, float v, float* total) {
 }
 
 // Shared-memory layout of one sampling workgroup (NT threads, NW = NT / 64 waves).
-// fred[0..NW) / ired[8..8+2 NW): block reductions; fred[16..20) / ired[0..8): named results.
+// fred[0..NW) / ired[8..8+2 NW): block reductions; fred[16..22) / ired[0..8): named results.
 struct SampleSmem {
   float* p;           // [n] logits -> e -> probabilities
   uint64_t* keys;     // [cap rounded up to a power of two] sort keys (p bits << 32 | ~index)
@@ -211,6 +211,8 @@ struct SampleSmem {
   int* chunk_e;       // [64] predicted binade per chunk
   uint32_t* chunk_t;  // [64][2]
   int* chunk_ok;      // [64]
+  int* runs;          // [4 * 128] binade runs of the exact-sum emulation: start, end, map
+  uint64_t* etab;     // [32] glibc expf's 2^(i/32) table
   float* fred;        // [32]
   int* ired;          // [48]
   int cap;            // keys / list capacity (kSampleMaxSorted in LDS, the row length in scratch)
@@ -245,6 +247,10 @@ __device__ inline double dpp_shr(double v) {
   const uint32_t lo = (uint32_t)dpp_shr<N>((int)(uint32_t)u), hi = (uint32_t)dpp_shr<N>((int)(uint32_t)(u >> 32));
   return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
+template <int N>
+__device__ inline uint32_t dpp_shr(uint32_t v) {
+  return (uint32_t)dpp_shr<N>((int)v);
+}
 __device__ inline double readlane_d(double v, int l) {
   const uint64_t u = __builtin_bit_cast(uint64_t, v);
   const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
@@ -252,6 +258,7 @@ __device__ inline double readlane_d(double v, int l) {
   return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
 __device__ inline int readlane_t(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ inline uint32_t readlane_t(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
 __device__ inline double readlane_t(double v, int l) { return readlane_d(v, l); }
 
 // block-wide exclusive scans (NT threads): per wave an inclusive scan of each 16-lane row on DPP
@@ -375,7 +382,7 @@ struct NoOther {
 // `other` runs on waves 1.. while wave 0 walks the chunk maps (the walk is serial; the other
 // waves would idle). It may not use workgroup barriers.
 template <int NT, typename Other = NoOther>
-__device__ float exact_seq_sum(const SampleSmem& sm, int n, uint64_t* stamps = nullptr, const Other& other = Other()) {
+__device__ float exact_seq_sum_chunks(const SampleSmem& sm, int n, uint64_t* stamps = nullptr, const Other& other = Other()) {
   constexpr int NS = NT / 64;  // sub-chunks per chunk (64 chunks, one per lane of wave 0)
   constexpr int NE = NT >= 1024 ? 64 : 128;  // serial-add register batch
   const int tid = threadIdx.x;
@@ -552,6 +559,207 @@ __device__ float exact_seq_sum(const SampleSmem& sm, int n, uint64_t* stamps = n
   return sm.fred[16];
 }
 
+// ---------------------------------------------------------------------------------------
+// The same sum for rows up to kSampleMaxN, by binade runs instead of chunks. With e >= 0 the
+// running f32 sum s_i (before element i) stays within gamma_n <= n 2^-24 (relative) of the exact
+// prefix pre_i (Higham, recursive summation), and pre_i only grows. Element i is SAFE in binade E
+// when pre_i >= 2^E (1 + d) and pre_{i+1} <= 2^(E+1) (1 - d), d = 2^-k >= 2 (n-1) 2^-24: then s_i and
+// s_{i+1} are both in [2^E, 2^(E+1)), so the add is the quantised increment of the parity map
+// above. The safe elements of one binade form ONE contiguous run (pre is monotone), so a run is
+// keyed by E: its map is composed across the threads it spans by a segmented scan, and the walk
+// applies one map per binade (about log2(sum / e_first) of them) and adds only the rest -- the
+// ranges of the threads that hold a binade crossing -- one by one. The walk still
+// checks each run against the real s and adds the run serially if a check fails (never, by the
+// bound; the fallback keeps the result exact regardless).
+// ---------------------------------------------------------------------------------------
+constexpr int kRunEMin = -100, kRuns = 128;  // run table: binades [-100, 27]
+
+struct PMap {  // parity map: from parity p, add T[p] ulps
+  uint32_t t0, t1;
+};
+__device__ inline PMap pcompose(PMap a, PMap b) {  // a, then b
+  const uint32_t n0 = a.t0 + ((a.t0 & 1u) ? b.t1 : b.t0);
+  const uint32_t n1 = a.t1 + (((1u + a.t1) & 1u) ? b.t1 : b.t0);
+  return PMap{min(n0, 0x2000000u), min(n1, 0x2000000u)};
+}
+template <int NT, typename Other = NoOther>
+__device__ float exact_seq_sum_runs(const SampleSmem& sm, int n, uint64_t* stamps = nullptr, const Other& other = Other()) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int* rstart = sm.runs;
+  int* rend = sm.runs + kRuns;
+  uint32_t* rt = (uint32_t*)(sm.runs + 2 * kRuns);  // [kRuns][2]
+  if (tid < kRuns) rend[tid] = -1;
+  // safety band d = 2^-k >= 2 (n - 1) 2^-24 >= 2 gamma_(n-1) (n <= kSampleMaxN = 2^14: k >= 9)
+  int lg = 0;
+  while ((1 << lg) < n - 1) ++lg;
+  const uint64_t dm = 1ull << (52 - (23 - lg));  // d 2^52 (the double fraction field of 1 + d)
+  const int SUB = (n + NT - 1) / NT;
+  const int b = min(n, tid * SUB), e = min(n, b + SUB);
+  double ds = 0.0;
+  for (int i = b; i < e; ++i) ds += (double)sm.p[i];
+  double dtot;
+  double lo = block_excl_scan_t<NT, double>(ds, sm.dscan, &dtot);  // its barriers order rend[] init
+  STAMP(10);
+  // pass 1: a thread whose whole range lies in one binade's safe band (its first and last
+  // prefixes decide it: pre is monotone) composes the map of its range; any other range -- the
+  // few that hold a binade crossing -- is left to the walk, element by element. The safety
+  // tests read only the high words of the doubles: the band edges d 2^52 and 2^52 - 2 d 2^52 have
+  // zero low words (d >= 2^-20), and the upper test is taken strictly (a stricter test only adds
+  // elements to the walk).
+  const uint32_t DM = (uint32_t)(dm >> 32), DMAX = (1u << 20) - 2 * DM;
+  const uint32_t lw = (uint32_t)(__builtin_bit_cast(uint64_t, lo) >> 32);
+  const uint32_t hw = (uint32_t)(__builtin_bit_cast(uint64_t, lo + ds) >> 32);
+  const int E = (int)(lw >> 20) - 1023;  // lo >= 0: no sign bit
+  const bool wsafe = b < e && E >= kRunEMin && E <= kRunEMin + kRuns - 1 && (lw & 0xFFFFFu) >= DM &&
+                     (hw >> 20) == (lw >> 20) && (hw & 0xFFFFFu) < DMAX;
+  PMap T{0u, 0u};
+  if (wsafe) {
+    for (int i = b; i < e; ++i) {
+      // the element's increment in ulps of binade E (safe: sh >= 1), ties to even by parity
+      const uint32_t xb = __builtin_bit_cast(uint32_t, sm.p[i]);
+      const uint32_t ef = (xb >> 23) & 0xFFu;
+      const uint32_t M = (xb & 0x7FFFFFu) | (ef ? 0x800000u : 0u);
+      const int ex = ef ? (int)ef - 150 : -149;
+      const int sh = min((E - 23) - ex, 31);
+      const uint32_t a = M >> sh, r = M & ((1u << sh) - 1u), half = (1u << sh) >> 1;
+      const uint32_t up = r > half ? 1u : 0u, tie = r == half ? 1u : 0u;
+      const uint32_t m0 = a + (up | (tie & a & 1u)), m1 = a + (up | (tie & ~a & 1u));
+      T.t0 += (T.t0 & 1u) ? m1 : m0;
+      T.t1 += ((1u + T.t1) & 1u) ? m1 : m0;
+    }
+  }
+  const int tE = wsafe ? E : kNoBinade;
+  sm.sub_e[tid] = tE;
+  // parity-free maps (no half-ulp tie anywhere: t0 == t1) compose by plain addition
+  const int ties = __syncthreads_or(wsafe && T.t0 != T.t1);
+  STAMP(11);
+  const int prevE = tid > 0 ? sm.sub_e[tid - 1] : kNoBinade;
+  const int nextE = tid + 1 < NT ? sm.sub_e[tid + 1] : kNoBinade;
+  const bool contL = wsafe && prevE == tE, contR = wsafe && nextE == tE;
+  if (wsafe && !contL) rstart[tE - kRunEMin] = b;
+  if (wsafe && !contR) rend[tE - kRunEMin] = e;
+  if (!ties) {
+    // a run's map = (inclusive prefix at its last thread) - (exclusive prefix at its head), in
+    // uint32 arithmetic mod 2^32 (a run adds < 2^24 ulps)
+    uint32_t tot;
+    const uint32_t P = block_excl_scan_t<NT, uint32_t>(wsafe ? T.t0 : 0u, (uint32_t*)sm.scan, &tot);
+    if (wsafe && !contL) rt[2 * (tE - kRunEMin)] = P;
+    __syncthreads();
+    if (wsafe && !contR) {
+      const uint32_t full = P + T.t0 - (contL ? rt[2 * (tE - kRunEMin)] : P);
+      rt[2 * (tE - kRunEMin)] = full;
+      rt[2 * (tE - kRunEMin) + 1] = full;
+    }
+  } else {
+    // segmented exclusive scan over threads of (run head, parity map): carry = the run's map so far
+    bool f = !contL;
+    PMap x = T;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y0 = __shfl_up(x.t0, o), y1 = __shfl_up(x.t1, o);
+      const bool yf = __shfl_up(f ? 1 : 0, o) != 0;
+      if (lane >= o && !f) {
+        x = pcompose(PMap{y0, y1}, x);
+        f = yf;
+      }
+    }
+    // wave totals -> LDS (the double scan's scratch: 8 x (flag, t0, t1) as ints)
+    int* wt = (int*)sm.dscan;
+    if (lane == 63) { wt[3 * w] = f ? 1 : 0; wt[3 * w + 1] = (int)x.t0; wt[3 * w + 2] = (int)x.t1; }
+    uint32_t e0 = __shfl_up(x.t0, 1), e1 = __shfl_up(x.t1, 1);
+    bool ef = __shfl_up(f ? 1 : 0, 1) != 0;
+    if (lane == 0) { e0 = 0u; e1 = 0u; ef = false; }
+    __syncthreads();
+    PMap c{0u, 0u};  // carry into this wave: waves 0 .. w-1 in order
+    for (int k = 0; k < w; ++k) {
+      const PMap kv{(uint32_t)wt[3 * k + 1], (uint32_t)wt[3 * k + 2]};
+      c = wt[3 * k] ? kv : pcompose(c, kv);
+    }
+    const PMap v = ef ? PMap{e0, e1} : pcompose(c, PMap{e0, e1});
+    if (wsafe && !contR) {
+      const PMap full = contL ? pcompose(v, T) : T;
+      rt[2 * (tE - kRunEMin)] = full.t0;
+      rt[2 * (tE - kRunEMin) + 1] = full.t1;
+    }
+  }
+  __syncthreads();
+  STAMP(12);
+  if (tid < 64) {
+    // wave 0 walks the runs in binade order (= element order), adding the unsafe elements
+    // between them on lane 0
+    const int s0 = rstart[lane], e0 = rend[lane], s1 = rstart[lane + 64], e1 = rend[lane + 64];
+    const uint32_t a0 = rt[2 * lane], b0 = rt[2 * lane + 1], a1 = rt[2 * (lane + 64)], b1 = rt[2 * (lane + 64) + 1];
+    uint64_t m0 = __ballot(e0 >= 0), m1 = __ballot(e1 >= 0);
+    float s = 0.0f;
+    int pos = 0;
+    uint64_t sadd = 0;
+    // unsafe elements in order: 64 at a time pulled into the lanes by one LDS read, then added
+    // in order from the registers (no dependent LDS latency per element)
+    auto serial = [&](int from, int to) {
+      if (from >= to) return;
+      const uint64_t t0 = stamps ? __builtin_amdgcn_s_memtime() : 0;
+      for (int q = from; q < to; q += 64) {
+        const float v = q + lane < to ? sm.p[q + lane] : 0.0f;
+        const int cnt = __builtin_amdgcn_readfirstlane(min(64, to - q));
+        int i = 0;
+        for (; i + 4 <= cnt; i += 4) {
+          s += readlane_f(v, i);
+          s += readlane_f(v, i + 1);
+          s += readlane_f(v, i + 2);
+          s += readlane_f(v, i + 3);
+        }
+        for (; i < cnt; ++i) s += readlane_f(v, i);
+      }
+      if (stamps) sadd += __builtin_amdgcn_s_memtime() + (uint64_t)(s != s) - t0;
+    };
+    while (m0 | m1) {
+      const bool hiw = m0 == 0;
+      const uint64_t m = hiw ? m1 : m0;
+      const int l = __builtin_ctzll(m);
+      if (hiw) m1 &= m1 - 1; else m0 &= m0 - 1;
+      const int k = l + (hiw ? 64 : 0);
+      const int rs = readlane_i(hiw ? s1 : s0, l), re = readlane_i(hiw ? e1 : e0, l);
+      const uint32_t T0 = (uint32_t)readlane_i((int)(hiw ? a1 : a0), l);
+      const uint32_t T1 = (uint32_t)readlane_i((int)(hiw ? b1 : b0), l);
+      if (rs < pos) {  // cannot happen (runs are disjoint and ordered); stay exact regardless
+        serial(pos, re);
+        pos = max(pos, re);
+        continue;
+      }
+      serial(pos, rs);
+      s = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, s)));
+      const uint32_t sb = __builtin_bit_cast(uint32_t, s);
+      const int ef = (int)((sb >> 23) & 0xFFu);
+      const uint32_t mm = (sb & 0x7FFFFFu) | 0x800000u;
+      const uint32_t T = (mm & 1u) ? T1 : T0;
+      if (ef != 0 && ef - 127 == k + kRunEMin && mm + T < 0x1000000u)
+        s = __builtin_bit_cast(float, (sb & 0xFF800000u) | ((mm + T) & 0x7FFFFFu));
+      else
+        serial(rs, re);
+      pos = re;
+    }
+    serial(pos, n);
+    if (tid == 0) {
+      sm.fred[16] = s;
+      if (stamps) {
+        stamps[14] = __builtin_amdgcn_s_memtime();
+        stamps[15] = sadd;
+      }
+    }
+  } else {
+    other();
+  }
+  __syncthreads();
+  STAMP(13);
+  return sm.fred[16];
+}
+
+template <int NT, typename Other = NoOther>
+__device__ float exact_seq_sum(const SampleSmem& sm, int n, uint64_t* stamps = nullptr, const Other& other = Other()) {
+  if (n <= kSampleMaxN) return exact_seq_sum_runs<NT>(sm, n, stamps, other);
+  return exact_seq_sum_chunks<NT>(sm, n, stamps, other);
+}
+
 // bitonic sort (descending) of M (power of two) keys in LDS by the whole workgroup
 template <int NT>
 __device__ void bitonic_desc(uint64_t* keys, int M) {
@@ -697,7 +905,7 @@ __device__ __attribute__((always_inline)) int sample_fast(const SampleSmem& sm, 
         adj_on = true;
       }
     }
-    const float r = draw_r(key, draw, fixed42);
+    const float r = sm.fred[21];  // the draw, made by the last wave during the exact sum
     int ret = -1;
     if (r <= 0.0f) {
       ret = 0;  // cum at index 0 is >= 0 >= r
@@ -738,9 +946,22 @@ __device__ __attribute__((always_inline)) int sample_block(const SampleSmem& sm,
   STAMP(1);
   // (2) softmax: max, exp, sequential sum (exact emulation), divide
   float mx = -__builtin_inff();
+  if (tid < 32) sm.etab[tid] = exp2_tab(tid);  // ordered before the reads by block_max's barriers
   for (int i = tid; i < n; i += NT) mx = fmaxf(mx, sm.p[i]);
   mx = block_max<NT>(mx, sm.fred);
-  for (int i = tid; i < n; i += NT) sm.p[i] = glibc_expf(sm.p[i] - mx);
+  {
+    const uint64_t* et = sm.etab;
+    auto tab = [et](int i) { return et[i]; };
+    int i = tid;
+    for (; i + 3 * NT < n; i += 4 * NT) {  // four independent elements per round
+      const float x0 = sm.p[i], x1 = sm.p[i + NT], x2 = sm.p[i + 2 * NT], x3 = sm.p[i + 3 * NT];
+      sm.p[i] = glibc_expf_t(x0 - mx, tab);
+      sm.p[i + NT] = glibc_expf_t(x1 - mx, tab);
+      sm.p[i + 2 * NT] = glibc_expf_t(x2 - mx, tab);
+      sm.p[i + 3 * NT] = glibc_expf_t(x3 - mx, tab);
+    }
+    for (; i < n; i += NT) sm.p[i] = glibc_expf_t(sm.p[i] - mx, tab);
+  }
   // Fast path (top-k <= kFastK, no temperature step): while wave 0 walks the exact sum, the
   // other waves collect the top-k candidates on the unnormalised e = exp(l - max), so that after
   // the sum only the candidates are divided, ranked and sampled. See sample_fast_ok below.
@@ -800,7 +1021,13 @@ __device__ __attribute__((always_inline)) int sample_block(const SampleSmem& sm,
       }
     }
   };
-  const float sum = exact_seq_sum<NT>(sm, n, stamps, collect);
+  // waves 1..: the candidates, then (last wave) the uniform draw of step (6) -- a ChaCha12
+  // block, thousands of cycles on one wave -- both while wave 0 walks the exact sum
+  auto other = [&]() {
+    collect();
+    if (tid == NT - 64) sm.fred[21] = draw_r(key, draw, fixed42);
+  };
+  const float sum = exact_seq_sum<NT>(sm, n, stamps, other);
   STAMP(3);
   if (want_fast) {
     const int nc = sm.ired[31];
@@ -1015,7 +1242,7 @@ __device__ __attribute__((always_inline)) int sample_block(const SampleSmem& sm,
   STAMP(8);
   // (6) multinomial (:174-207): wave 0, cumulative in index order from lanes
   if (tid < 64) {
-    const float r = draw_r(key, draw, fixed42);
+    const float r = sm.fred[21];  // the draw, made by the last wave during the exact sum
     int ret = -1;
     if (r <= sm.p[0]) {
       ret = 0;
@@ -1065,6 +1292,8 @@ __device__ SampleSmem carve(char* base, int n, bool sorted_in_lds = true) {
   sm.chunk_e = (int*)q; q += 64 * 4;
   sm.chunk_t = (uint32_t*)q; q += 128 * 4;
   sm.chunk_ok = (int*)q; q += 64 * 4;
+  sm.runs = (int*)q; q += 4 * kRuns * 4;
+  sm.etab = (uint64_t*)q; q += 32 * 8;
   sm.fred = (float*)q; q += 32 * 4;
   sm.ired = (int*)q;
   sm.cap = kSampleMaxSorted;
@@ -1074,7 +1303,7 @@ template <int NT>
 inline size_t smem_bytes(int n) {
   const int npad = (n + 3) & ~3;
   return (size_t)npad * 4 + kSampleMaxSorted * 8 + 16 * 8 + kSampleMaxSorted * 4 + 16 * 4 + 2 * NT * 4 + NT * 4 +
-         256 + 512 + 256 + 32 * 4 + 48 * 4;
+         256 + 512 + 256 + 4 * kRuns * 4 + 32 * 8 + 32 * 4 + 48 * 4;
 }
 constexpr int kSampleThreads = 512;  // one workgroup per sampled row
 

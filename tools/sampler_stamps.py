@@ -29,5 +29,5 @@ for n, p, k in [(8193, 0.95, 80), (4096, 0.95, 20), (1024, 0.95, 80), (8193, 1.0
           " ".join(f"{nm}={x:.0f}" for nm, x in zip(names, d)))
     s2 = dbg[64:].view(np.uint64).reshape(32, 16).astype(np.int64)
     print("   sum: scan", (s2[:, 10] - s2[:, 2]).mean(), "sim", (s2[:, 11] - s2[:, 10]).mean(), "compose",
-          (s2[:, 12] - s2[:, 11]).mean(), "walk", (s2[:, 13] - s2[:, 12]).mean(), "fast chunks", s2[:, 14].mean(),
+          (s2[:, 12] - s2[:, 11]).mean(), "walk", (s2[:, 13] - s2[:, 12]).mean(), "walk-only", (s2[:, 14] - s2[:, 12]).mean(),
           "serial-add cycles", s2[:, 15].mean())
