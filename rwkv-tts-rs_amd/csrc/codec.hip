@@ -69,7 +69,11 @@ __device__ inline void split_store(bf16_t* h, bf16_t* l, int64_t o, float v) {
   l[o] = f32_to_bf16(v - bf16_to_f32(hb));
 }
 
-constexpr int kConvTM = 128;  // output rows (time) per workgroup
+// output rows (time) per workgroup: 32 per wave. The 7-tap convolutions run 8-wave workgroups
+// (256 rows): their double-buffered chunk window (the 7 taps' weights + the activation window,
+// 92-104 KB at 128 rows) leaves room for one workgroup per CU only, so a 4-wave workgroup would
+// run one wave per SIMD and expose every wait; 8 waves share the same weight tiles.
+constexpr int conv_waves(int KT) { return KT == 7 ? 8 : 4; }
 
 // LDS image of a 32-channel chunk: 64-B rows of four 16-B pieces, piece p of row r stored at
 // slot p ^ ((r >> 1) & 3): the MFMA fragment reads (16 rows x 4 pieces per ds_read_b128 lane
@@ -88,8 +92,8 @@ __device__ inline void glds16(const void* g, void* l) {
 // and the chunk of every tap's weights, then runs ntaps x 2 x NT x 2 MFMAs per wave while the
 // next chunk streams in.
 template <int TN, int KT>
-__global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
-  constexpr int TM = kConvTM, NT = TN / 16;
+__global__ __launch_bounds__(64 * conv_waves(KT), conv_waves(KT) == 8 ? 1 : 2) void k_conv(ConvArgs a) {
+  constexpr int NWV = conv_waves(KT), TM = 32 * NWV, NT = TN / 16;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int req = blockIdx.z;
   const int Tin = a.ntok[req] * a.tin_mul;
@@ -129,7 +133,7 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
   const bf16_t* srcp[MAXB];
 #pragma unroll
   for (int u = 0; u < MAXB; ++u) {
-    const int b = wave + 4 * u;
+    const int b = wave + NWV * u;
     const bf16_t* src = a.zeros;
     if (b < nAblk) {
       const int plane = b >= WRp / 16, row = (b - plane * (WRp / 16)) * 16 + lrow;
@@ -147,7 +151,7 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
     const int c0 = ck * 32;
 #pragma unroll
     for (int u = 0; u < MAXB; ++u) {
-      const int b = wave + 4 * u;
+      const int b = wave + NWV * u;
       if (b < nblk) glds16(srcp[u] + c0, buf + b * 1024);
     }
   };
@@ -496,7 +500,7 @@ class Codec {
     RT_HIP(hipFuncSetAttribute((const void*)k_conv<TN, KT>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     RT_CONV_ATTR(32, 1) RT_CONV_ATTR(32, 3) RT_CONV_ATTR(32, 7)
     RT_CONV_ATTR(64, 1) RT_CONV_ATTR(64, 3) RT_CONV_ATTR(64, 7)
-    RT_CONV_ATTR(96, 1)
+    RT_CONV_ATTR(96, 1) RT_CONV_ATTR(48, 1) RT_CONV_ATTR(48, 3) RT_CONV_ATTR(48, 7)
 #undef RT_CONV_ATTR
     RT_HIP(hipFuncSetAttribute((const void*)k_conv_out, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     // zero page: out-of-range window rows read zeros at channel offsets up to the largest Ci
@@ -586,13 +590,17 @@ class Codec {
   int conv(int n, int Tmax, const std::string& name, Planes x, int64_t bs, int Ci, int tin_mul, const bf16_t* w,
            int K, int Co, int mode, int dil, int pad, int s, const float* bias, const ConvOut& o) {
     RT_CHECK(Ci % 32 == 0 && Co % 32 == 0, RWKVTTS_EINVAL, "codec conv: channels must be multiples of 32");
-    const int TN = (Co % 64 == 0) ? 64 : ((Co % 96 == 0 && K == 1) ? 96 : 32);
+    // column tile: 64, or for the last stage's 96 channels 96 (pointwise) / 48 (taps): 32-wide
+    // tiles read two LDS fragments per four MFMAs
+    const int TN = (Co % 64 == 0) ? 64 : ((Co % 96 == 0 && K == 1) ? 96 : (Co % 48 == 0 ? 48 : 32));
     const int ntaps_max = mode == 1 ? (K + s - 1) / s : K;
     const int span = (ntaps_max - 1) * (mode == 1 ? 1 : dil);
-    const int WRp = (kConvTM + span + 15) & ~15;
+    const int KT = ntaps_max <= 1 ? 1 : (ntaps_max <= 3 ? 3 : 7);
+    const int nwv = TN == 96 ? 4 : conv_waves(KT), TM = 32 * nwv;
+    const int WRp = (TM + span + 15) & ~15;
     const size_t shm = std::max(2 * (size_t)(2 * WRp + ntaps_max * TN) * 64,        // two chunk buffers
-                                (size_t)4 * 32 * (TN + 4) * sizeof(float));          // epilogue tiles
-    RT_CHECK(shm <= 160 * 1024 && (2 * WRp + ntaps_max * TN) / 16 <= 64 && ntaps_max <= 7 && Ci <= 4096,
+                                (size_t)nwv * 32 * (TN + 4) * sizeof(float));        // epilogue tiles
+    RT_CHECK(shm <= 160 * 1024 && (2 * WRp + ntaps_max * TN) / 16 <= 16 * nwv && ntaps_max <= 7 && Ci <= 4096,
              RWKVTTS_EINVAL, "codec conv: tile window too large");
     ConvArgs a;
     a.xh = x.h; a.xl = x.l; a.x_bs = bs; a.Ci = Ci; a.tin_mul = tin_mul; a.w = w; a.K = K; a.Co = Co;
@@ -600,28 +608,33 @@ class Codec {
     a.gamma = o.gamma; a.res = o.res; a.act = o.act; a.y = o.y; a.yh = o.p.h; a.yl = o.p.l;
     a.y_alpha = o.alpha; a.y_bs = o.y_bs >= 0 ? o.y_bs : bs; a.ntok = d_ntok; a.zeros = zeros;
     const int phases = mode == 1 ? s : 1;
-    dim3 grid((unsigned)((Tmax * (int64_t)tin_mul + kConvTM - 1) / kConvTM), (unsigned)(phases * (Co / TN)), (unsigned)n);
+    dim3 grid((unsigned)((Tmax * (int64_t)tin_mul + TM - 1) / TM), (unsigned)(phases * (Co / TN)), (unsigned)n);
     // XCD-aware order for the long-time-axis residual convs (conv7 at >= 32 time tiles: -4 %);
     // the short prenet / conv_in / convT launches keep the default order (2x slower remapped)
     static const int xm = getenv("RWKVTTS_CODEC_XMAP") ? atoi(getenv("RWKVTTS_CODEC_XMAP")) : 1;
     a.xmap = 0;
-    if (xm && grid.y > 1 && mode == 0 && K == 7 && grid.x >= 32) {
+    if (grid.y > 1 && mode == 0 && grid.x >= 32 && (((xm & 1) && K == 7) || ((xm & 2) && K == 1))) {
       a.xmap = 1;
       a.gx = (int)grid.x;
       a.gy = (int)grid.y;
       grid = dim3((unsigned)(8 * ((grid.x + 7) / 8) * grid.y), 1, (unsigned)n);
     }
     pbeg();
-    const int KT = ntaps_max <= 1 ? 1 : (ntaps_max <= 3 ? 3 : 7);
-    if (TN == 96) k_conv<96, 1><<<grid, 256, shm, stream>>>(a);
+    const int nthr = 64 * nwv;
+    if (TN == 96) k_conv<96, 1><<<grid, nthr, shm, stream>>>(a);
+    else if (TN == 48) {
+      if (KT == 1) k_conv<48, 1><<<grid, nthr, shm, stream>>>(a);
+      else if (KT == 3) k_conv<48, 3><<<grid, nthr, shm, stream>>>(a);
+      else k_conv<48, 7><<<grid, nthr, shm, stream>>>(a);
+    }
     else if (TN == 64) {
-      if (KT == 1) k_conv<64, 1><<<grid, 256, shm, stream>>>(a);
-      else if (KT == 3) k_conv<64, 3><<<grid, 256, shm, stream>>>(a);
-      else k_conv<64, 7><<<grid, 256, shm, stream>>>(a);
+      if (KT == 1) k_conv<64, 1><<<grid, nthr, shm, stream>>>(a);
+      else if (KT == 3) k_conv<64, 3><<<grid, nthr, shm, stream>>>(a);
+      else k_conv<64, 7><<<grid, nthr, shm, stream>>>(a);
     } else {
-      if (KT == 1) k_conv<32, 1><<<grid, 256, shm, stream>>>(a);
-      else if (KT == 3) k_conv<32, 3><<<grid, 256, shm, stream>>>(a);
-      else k_conv<32, 7><<<grid, 256, shm, stream>>>(a);
+      if (KT == 1) k_conv<32, 1><<<grid, nthr, shm, stream>>>(a);
+      else if (KT == 3) k_conv<32, 3><<<grid, nthr, shm, stream>>>(a);
+      else k_conv<32, 7><<<grid, nthr, shm, stream>>>(a);
     }
     RT_HIP(hipGetLastError());
     pend(name.c_str());
