@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <chrono>
 #include <deque>
+#include <mutex>
 #include <random>
 
 namespace rwkvtts {
@@ -669,6 +670,10 @@ int Engine::run_step(const StepPlan& p, bool upload) {
     auto key = std::make_pair(R, p.head_rows * 2 + (p.advance ? 1 : 0));
     auto it = graphs_.find(key);
     if (it == graphs_.end()) {
+      // one capture at a time per process: engines owned by different threads (the manager's
+      // workers) never capture / instantiate concurrently
+      static std::mutex capture_mu;
+      std::lock_guard<std::mutex> cap_lock(capture_mu);
       hipGraph_t graph;
       RT_HIP(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
       int rc = launch_forward(R, n_seg, n_lg, p.head_rows, true, p.advance);
@@ -1133,9 +1138,11 @@ int Engine::serve(JobSource& src) {
       r.n_global = c.n_global;
       memcpy(r.global_tokens, c.global_out, sizeof(int32_t) * RWKVTTS_N_GLOBAL);
       r.n_semantic = c.n_sem;
-      if (r.semantic_tokens && c.n_sem > 0)
-        RT_HIP(hipMemcpy(r.semantic_tokens, d_sem_ + (int64_t)a.slot * RWKVTTS_SEMANTIC_LIMIT,
-                         sizeof(int32_t) * c.n_sem, hipMemcpyDeviceToHost));
+      if (r.semantic_tokens && c.n_sem > 0) {  // on the engine's stream: no null-stream sync
+        RT_HIP(hipMemcpyAsync(r.semantic_tokens, d_sem_ + (int64_t)a.slot * RWKVTTS_SEMANTIC_LIMIT,
+                              sizeof(int32_t) * c.n_sem, hipMemcpyDeviceToHost, stream_));
+        RT_HIP(hipStreamSynchronize(stream_));
+      }
       src.finish(a.job);
       free_slots.push_back(a.slot);
       act.erase(act.begin() + i);

@@ -215,12 +215,15 @@ def test_manager_two_engines_concurrent_callers():
     try:
         reqs = [make_request(synth_text(1200 + i), seed=600 + i, max_tokens=10 + i) for i in range(12)]
         got = [None] * 12
-        ths = [threading.Thread(target=lambda i=i: got.__setitem__(
-            i, m.generate_tts(reqs[i].text_tokens, reqs[i].property_tokens, args=reqs[i].args))) for i in range(12)]
+        # generate_tts is wait(submit(request)); a bounded wait turns a stuck engine into a
+        # failure carrying the manager's counters instead of a hang
+        ths = [threading.Thread(target=lambda i=i: got.__setitem__(i, m.wait(m.submit(reqs[i]), timeout_ms=120000)))
+               for i in range(12)]
         for t in ths:
             t.start()
         for t in ths:
             t.join()
+        assert all(g is not None for g in got), ("requests not served within 120 s", m.stats())
         for r, gs in zip(reqs, got):
             assert gs == _oracle(om, r)
         st = m.stats()
