@@ -112,6 +112,8 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--token-chunk-size", type=int, default=2048,
+                    help="prompt rows per engine step (all admitted prompts share it; outputs are chunk-invariant, bitwise)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--profile", action="store_true", help="per-kernel HIP-event pass (default on)")
     ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
@@ -148,7 +150,7 @@ def main():
     from rwkvtts import dist as D
     D.broadcast_blob(wdev, src=0)
     torch.cuda.synchronize()
-    rt = rwkvtts.SharedRwkvRuntime(nbytes, device=local, max_slots=B_PER_GPU, token_chunk_size=512,
+    rt = rwkvtts.SharedRwkvRuntime(nbytes, device=local, max_slots=B_PER_GPU, token_chunk_size=args.token_chunk_size,
                                    use_graphs=True, device_ptr=wdev.data_ptr())
     del wdev
     # ---- vocoder weights: same scheme (rank 0 synthesises, RCCL broadcast)
@@ -201,12 +203,16 @@ def main():
         return len(pcm)
 
     futs = []
+    gen_ms = prefill_ms = 0.0
     with ThreadPoolExecutor(max_workers=1) as pool:
         for s in range(args.steps):
+            tg = time.perf_counter()
             out = rt.generate_batch(requests(s))
+            gen_ms += 1000.0 * (time.perf_counter() - tg)
             sem_tokens += sum(len(x) for _, x in out)
             st = rt.stats()
             decode_ms += st["decode_ms"]
+            prefill_ms += st["prefill_ms"]
             dec_steps += st["steps"]
             futs.append(pool.submit(vocode, out) if args.pipeline else None)
             if not args.pipeline:
@@ -292,6 +298,13 @@ def main():
                                    "exact sampler, + BiCodec vocoder -> PCM (vocoder of batch s overlapped with LM of batch s+1 on its own stream)",
                        "global_batch": B_PER_GPU * world, "seq_len": 32 + 33 + SEMANTIC,
                        "parallelism": f"dp{world} (request sharding)"},
+            # where a step's wall time goes (rank 0, per batch): generate_batch wall time, of it
+            # the engine's decode / prefill stream time; the rest of ms_per_step is the last
+            # batch's vocoder (not overlapped) spread over the steps
+            "breakdown_ms_per_batch": {"generate": round(gen_ms / args.steps, 3),
+                                       "decode": round(decode_ms / args.steps, 3),
+                                       "prefill": round(prefill_ms / args.steps, 3),
+                                       "decode_steps": dec_steps // max(1, args.steps)},
             "roofline": roofline,
             "decode_step_roofline": step_roof,
             "codec_roofline": codec_roof,

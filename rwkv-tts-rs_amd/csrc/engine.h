@@ -155,7 +155,7 @@ class Engine {
         *partK_ = nullptr,
         *vfirst_ = nullptr, *logits_ = nullptr;
   bf16_t *xm_hi_ = nullptr, *xm_lo_ = nullptr, *z_hi_ = nullptr, *z_lo_ = nullptr,
-         *xf_hi_ = nullptr, *xf_lo_ = nullptr,
+         *xf_hi_ = nullptr, *xf_lo_ = nullptr, *xk_hi_ = nullptr, *xk_lo_ = nullptr,
          *xo_hi_ = nullptr, *xo_lo_ = nullptr;
   // controller
   SlotCtrl* d_ctrl_ = nullptr;

@@ -260,6 +260,10 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
   RT_OK(alloc(&partO_, (size_t)splitO_ * RC));
   RT_OK(alloc(&xf_hi_, RC));
   RT_OK(alloc(&xf_lo_, RC));
+  if (!f16_) {  // relu(k)^2 planes of bf16 prefill steps (launch_relu2_planes)
+    RT_OK(alloc(&xk_hi_, (size_t)Rmax_ * F));
+    RT_OK(alloc(&xk_lo_, (size_t)Rmax_ * F));
+  }
   RT_OK(alloc(&partK_, (size_t)splitK_ * Rmax_ * F));
   RT_OK(alloc(&partF_, (size_t)splitF_ * RC));
   RT_OK(alloc(&vfirst_, RC));
@@ -420,6 +424,9 @@ int Engine::flush_prof() {
   return RWKVTTS_OK;
 }
 
+// prefill steps with more rows than this take the relu^2-plane route for the FFN value GEMM
+static constexpr int kPlaneRows = 64;
+
 int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_from_ctrl, bool advance) {
   const int C = dims.n_embd, F = dims.n_ffn, Lc = dims.n_layer;
   hipEvent_t ev;
@@ -576,6 +583,14 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     gv.K = F; gv.M = R; gv.k_split = splitF_; gv.kslice = F / splitF_;
     gv.xmode = kXRelu2; gv.x_part = partK_; gv.x_nsplit = splitK_; gv.x_ld = F;
     gv.x_part_stride = (int64_t)Rmax_ * F;
+    static const bool no_planes = getenv("RWKVTTS_NO_RELU2_PLANES") != nullptr;  // A/B timing switch
+    if (xk_hi_ && R > kPlaneRows && !no_planes) {
+      // prefill steps: relu^2 planes once (every value column tile would otherwise re-read the
+      // NX f32 key slabs of its K-slice); decode steps keep the fused staging (one launch fewer)
+      launch_relu2_planes(partK_, splitK_, (int64_t)Rmax_ * F, F, F, R, xk_hi_, xk_lo_, stream_);
+      gv.seg[0] = {w.ffn_v, xk_hi_, xk_lo_, F, C, 0, 0};
+      gv.xmode = kXPlanes;
+    }
     gv.out = partF_; gv.split_stride = RC; gv.ldo = C;
     gv.allow_xmap = (xmap_mask_ >> 3) & 1;
     if (w.quant) { gv.q_fmt = w.quant; gv.qw = w.q_fv; gv.qs = w.s_fv; gv.q_shift = w.qs_fv; }

@@ -150,6 +150,9 @@ int launch_wkv(const WkvArgs& a, int n_seg, int H, hipStream_t st);
 // (row-major S[i][j], generic kernels), 1 k_wkv4 (two waves per block), 2 k_wkv6 (four waves).
 // variant: rwkvtts_engine_desc.wkv_variant (0 auto by slot count).
 int wkv_perm_layout(int Dw, int Da, int Dv, int Dg, int n_part, int max_slots, int variant);
+// relu(sum of nx f32 slabs [nx][R][ld])^2 -> bf16 hi/lo planes [R][F] (bf16 prefill steps)
+void launch_relu2_planes(const float* part, int nx, int64_t pstride, int ld, int F, int R, bf16_t* hi, bf16_t* lo,
+                         hipStream_t st);
 // Repack a GEMM matrix W [N][K] (K % 32 == 0) into MFMA fragment blocks (k_gemm's layout):
 // out holds ceil(N/16)*16*K elements.
 void launch_pack_frag(const bf16_t* W, int N, int K, bf16_t* out, hipStream_t st);

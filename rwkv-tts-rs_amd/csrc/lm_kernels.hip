@@ -1182,6 +1182,31 @@ static void launch_gemm_t(const GemmArgs& a, dim3 grid, hipStream_t st) {
   }
 }
 
+// Prefill steps (bf16 models): relu(sum of the key GEMM's NX partial slabs)^2 as bf16 hi/lo planes
+// once, so the value GEMM stages 4-byte plane pairs instead of re-reading NX f32 slabs in every
+// one of its column tiles. Same sum order and split as k_gemm2's kXRelu2 staging: bit-identical.
+__global__ __launch_bounds__(256) void k_relu2_planes(const float* part, int nx, int64_t pstride, int ld, int F,
+                                                      bf16_t* hi, bf16_t* lo) {
+  const int row = blockIdx.y, c = 4 * (blockIdx.x * 256 + threadIdx.x);
+  if (c >= F) return;
+  const int64_t o = (int64_t)row * ld + c;
+  float4_ x = *(const float4_*)(part + o);
+  for (int p = 1; p < nx; ++p) x += *(const float4_*)(part + p * pstride + o);
+  float y[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) y[e] = x[e] > 0.f ? x[e] * x[e] : 0.f;
+  uint32_t h0, l0, h1, l1;
+  split2<false>(y[0], y[1], h0, l0);
+  split2<false>(y[2], y[3], h1, l1);
+  const int64_t q = (int64_t)row * F + c;
+  *(uint2*)(hi + q) = make_uint2(h0, h1);
+  *(uint2*)(lo + q) = make_uint2(l0, l1);
+}
+void launch_relu2_planes(const float* part, int nx, int64_t pstride, int ld, int F, int R, bf16_t* hi, bf16_t* lo,
+                         hipStream_t st) {
+  RT_LAUNCH(k_relu2_planes, dim3((F / 4 + 255) / 256, R), dim3(256), 0, st, part, nx, pstride, ld, F, hi, lo);
+}
+
 int gemm_ksteps(int kslice) { return kslice / 32; }
 
 bool gemm_tile_table(GemmArgs& a, int64_t x_mix_stride) {
@@ -1209,6 +1234,9 @@ bool gemm_tile_table(GemmArgs& a, int64_t x_mix_stride) {
 
 int launch_gemm(const GemmArgs& a, hipStream_t st) {
   const int tiles = a.seg[a.nseg - 1].tile_start + (a.seg[a.nseg - 1].N + 63) / 64;
+  // one or two 16-row blocks per workgroup, also for prefill steps: 64- and 128-row groups
+  // (fewer weight re-reads, 135 KB X images, one workgroup per CU) were measured slower on a
+  // 1280-row prefill step (10.6 vs 9.2 ms): the launches are latency-bound, not weight-bound
   const int mt = a.M <= 16 ? 1 : 2;
   const int mg = (a.M + mt * 16 - 1) / (mt * 16);
   dim3 grid(tiles, a.k_split, mg);
@@ -1868,7 +1896,6 @@ __global__ __launch_bounds__(256) void k_wkv6(WkvArgs a) {
   };
   for (int rr = 0; rr < n_rows; ++rr) {
     const int row = r_begin + rr;
-    if (rr > 0) load_parts(row);
     if (hid_thread) {
       float4_ x = hp[0];
 #pragma unroll
@@ -1892,6 +1919,9 @@ __global__ __launch_bounds__(256) void k_wkv6(WkvArgs a) {
       k += kp[p];
       v += vp[p];
     }
+    // prefill segments: the next row's partials go out now and arrive during this row's work
+    const float vf_row = vf;
+    if (rr + 1 < n_rows) load_parts(row + 1);
     __syncthreads();
     if (stp && rr == 0) stp[2] = __builtin_amdgcn_s_memtime() + (uint64_t)(r != r);
     float2_ l0 = {0.f, 0.f}, l1 = {0.f, 0.f}, l2 = {0.f, 0.f}, l3 = {0.f, 0.f};
@@ -1920,7 +1950,7 @@ __global__ __launch_bounds__(256) void k_wkv6(WkvArgs a) {
     if (a.layer == 0) {
       if (qq == 0) a.v_first[(int64_t)row * a.ldv + c] = v;
     } else {
-      v = v + (vf - v) * fsigm(v0 + lo2);
+      v = v + (vf_row - v) * fsigm(v0 + lo2);
     }
     {
       const float ksq = wave_sum(qq == 0 ? kk * kk : 0.f);

@@ -1,6 +1,7 @@
 set -o pipefail
-# kernel trace of a short decode_bench run: the first steps are the 512-row prefill steps
-export TMPDIR=/tmp
-mkdir -p gpurun_out/pf
-env "$@" timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/pf -o pf -- python3 tools/decode_bench.py 4 1 && \
-python3 tools/trace_steps.py gpurun_out/pf 5
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/pf; mkdir -p $O
+cd /tmp && export TMPDIR=/tmp
+for c in 512 2048; do
+PF_CHUNK=$c timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/t$c -o run -- python3 $R/tools/prefill_trace.py > $O/log$c.txt 2>&1 || exit 1
+cat $O/log$c.txt | grep prefill
+done
