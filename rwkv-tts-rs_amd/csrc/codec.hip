@@ -500,7 +500,7 @@ class Codec {
     RT_HIP(hipFuncSetAttribute((const void*)k_conv<TN, KT>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     RT_CONV_ATTR(32, 1) RT_CONV_ATTR(32, 3) RT_CONV_ATTR(32, 7)
     RT_CONV_ATTR(64, 1) RT_CONV_ATTR(64, 3) RT_CONV_ATTR(64, 7)
-    RT_CONV_ATTR(96, 1) RT_CONV_ATTR(48, 1) RT_CONV_ATTR(48, 3) RT_CONV_ATTR(48, 7)
+    RT_CONV_ATTR(96, 1) RT_CONV_ATTR(192, 1) RT_CONV_ATTR(48, 1) RT_CONV_ATTR(48, 3) RT_CONV_ATTR(48, 7)
 #undef RT_CONV_ATTR
     RT_HIP(hipFuncSetAttribute((const void*)k_conv_out, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     // zero page: out-of-range window rows read zeros at channel offsets up to the largest Ci
@@ -592,11 +592,16 @@ class Codec {
     RT_CHECK(Ci % 32 == 0 && Co % 32 == 0, RWKVTTS_EINVAL, "codec conv: channels must be multiples of 32");
     // column tile: 64, or for the last stage's 96 channels 96 (pointwise) / 48 (taps): 32-wide
     // tiles read two LDS fragments per four MFMAs
-    const int TN = (Co % 64 == 0) ? 64 : ((Co % 96 == 0 && K == 1) ? 96 : (Co % 48 == 0 ? 48 : 32));
+    int TN = (Co % 64 == 0) ? 64 : ((Co % 96 == 0 && K == 1) ? 96 : (Co % 48 == 0 ? 48 : 32));
+    // pointwise (memory-bound) convs: 96-wide column tiles read the input window fewer times
+    // (conv1 @ 192 / 384 / 768: 6.9 / 4.1 / 2.2 -> 5.3 / 3.5 / 2.0 ms per batch with the XCD-aware
+    // order below; 192-wide tiles halve the occupancy and are slower)
+    static const int tn1 = getenv("RWKVTTS_CONV1_TN") ? atoi(getenv("RWKVTTS_CONV1_TN")) : 96;  // A/B switch
+    if (K == 1 && tn1 > 0 && Co % tn1 == 0 && (tn1 == 64 || tn1 == 96 || tn1 == 192)) TN = tn1;
     const int ntaps_max = mode == 1 ? (K + s - 1) / s : K;
     const int span = (ntaps_max - 1) * (mode == 1 ? 1 : dil);
     const int KT = ntaps_max <= 1 ? 1 : (ntaps_max <= 3 ? 3 : 7);
-    const int nwv = TN == 96 ? 4 : conv_waves(KT), TM = 32 * nwv;
+    const int nwv = TN >= 96 ? 4 : conv_waves(KT), TM = 32 * nwv;
     const int WRp = (TM + span + 15) & ~15;
     const size_t shm = std::max(2 * (size_t)(2 * WRp + ntaps_max * TN) * 64,        // two chunk buffers
                                 (size_t)nwv * 32 * (TN + 4) * sizeof(float));        // epilogue tiles
@@ -609,9 +614,10 @@ class Codec {
     a.y_alpha = o.alpha; a.y_bs = o.y_bs >= 0 ? o.y_bs : bs; a.ntok = d_ntok; a.zeros = zeros;
     const int phases = mode == 1 ? s : 1;
     dim3 grid((unsigned)((Tmax * (int64_t)tin_mul + TM - 1) / TM), (unsigned)(phases * (Co / TN)), (unsigned)n);
-    // XCD-aware order for the long-time-axis residual convs (conv7 at >= 32 time tiles: -4 %);
-    // the short prenet / conv_in / convT launches keep the default order (2x slower remapped)
-    static const int xm = getenv("RWKVTTS_CODEC_XMAP") ? atoi(getenv("RWKVTTS_CODEC_XMAP")) : 1;
+    // XCD-aware order for the long-time-axis residual convs (conv7 and conv1 at >= 32 time tiles:
+    // a time tile's column tiles share one L2); the short prenet / conv_in / convT launches keep
+    // the default order (2x slower remapped)
+    static const int xm = getenv("RWKVTTS_CODEC_XMAP") ? atoi(getenv("RWKVTTS_CODEC_XMAP")) : 3;
     a.xmap = 0;
     if (grid.y > 1 && mode == 0 && grid.x >= 32 && (((xm & 1) && K == 7) || ((xm & 2) && K == 1))) {
       a.xmap = 1;
@@ -621,7 +627,8 @@ class Codec {
     }
     pbeg();
     const int nthr = 64 * nwv;
-    if (TN == 96) k_conv<96, 1><<<grid, nthr, shm, stream>>>(a);
+    if (TN == 192) k_conv<192, 1><<<grid, nthr, shm, stream>>>(a);
+    else if (TN == 96) k_conv<96, 1><<<grid, nthr, shm, stream>>>(a);
     else if (TN == 48) {
       if (KT == 1) k_conv<48, 1><<<grid, nthr, shm, stream>>>(a);
       else if (KT == 3) k_conv<48, 3><<<grid, nthr, shm, stream>>>(a);
