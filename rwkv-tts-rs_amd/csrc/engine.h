@@ -69,7 +69,7 @@ class Engine {
   ~Engine();
   int init(const rwkvtts_engine_desc& desc, const void* weights, size_t bytes, int on_device);
 
-  int slot_reset(int slot);
+  int slot_reset(int slot, bool sync = true);  // sync = false: stream-ordered only (admission)
   int slot_read(int slot, float* out);
   int slot_write(int slot, const float* in);
   int64_t state_floats() const;
@@ -144,6 +144,7 @@ class Engine {
   float* ffn_sh_ = nullptr;  // [2][S][L][C]
   int* slot_par_ = nullptr;  // [S]
   std::vector<int> par_host_;
+  std::vector<SlotCtrl> ctrl_stage_;  // [S] host copy of each admitted slot's initial control block
   // per-step tables
   uint32_t* d_tok_ = nullptr;
   int4* d_rows_ = nullptr;

@@ -242,6 +242,7 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
   RT_OK(alloc(&ffn_sh_, (size_t)2 * S_ * Lc * C));
   RT_OK(alloc(&slot_par_, (size_t)S_));
   par_host_.assign(S_, 0);
+  ctrl_stage_.assign(S_, SlotCtrl{});
   // tables
   RT_OK(alloc(&d_tok_, (size_t)Rmax_));
   RT_OK(alloc(&d_rows_, (size_t)Rmax_));
@@ -283,7 +284,7 @@ int64_t Engine::state_floats() const {
   return (int64_t)dims.n_layer * (2 * C + (int64_t)H_ * 64 * 64);
 }
 
-int Engine::slot_reset(int slot) {
+int Engine::slot_reset(int slot, bool sync) {
   RT_CHECK(slot >= 0 && slot < S_, RWKVTTS_EINVAL, "slot out of range");
   RT_HIP(hipSetDevice(device_));
   const int64_t C = dims.n_embd, Lc = dims.n_layer, per = Lc * H_ * 64 * 64;
@@ -294,7 +295,7 @@ int Engine::slot_reset(int slot) {
   }
   par_host_[slot] = 0;
   RT_HIP(hipMemcpyAsync(slot_par_ + slot, &par_host_[slot], 4, hipMemcpyHostToDevice, stream_));
-  RT_HIP(hipStreamSynchronize(stream_));
+  if (sync) RT_HIP(hipStreamSynchronize(stream_));
   return RWKVTTS_OK;
 }
 
@@ -1014,8 +1015,11 @@ int Engine::serve(JobSource& src) {
       c.phase = kPhGlobal;
       a.total = RWKVTTS_N_GLOBAL + 1 + c.sem_limit;
     }
-    RT_OK(slot_reset(slot));
-    RT_HIP(hipMemcpyAsync(d_ctrl_ + slot, &c, sizeof(c), hipMemcpyHostToDevice, stream_));
+    RT_OK(slot_reset(slot, false));  // ordered before the slot's first step on stream_
+    // from per-slot host storage: admissions are not synchronised, so the source must outlive the
+    // stream-ordered copy (the slot's entry is rewritten only after the slot retires)
+    ctrl_stage_[slot] = c;
+    RT_HIP(hipMemcpyAsync(d_ctrl_ + slot, &ctrl_stage_[slot], sizeof(c), hipMemcpyHostToDevice, stream_));
     act.push_back(std::move(a));
     decode_plan_valid = false;
     return RWKVTTS_OK;
@@ -1140,7 +1144,20 @@ int Engine::serve(JobSource& src) {
       }
       tl_steps_++;
     }
-    // ---- retire finished slots
+    // ---- retire finished slots: every finished slot's tokens copied on the engine's stream (no
+    // null-stream sync), one synchronisation, then the jobs are handed back
+    bool copied = false;
+    for (auto& a : act) {
+      const SlotCtrl& c = h_ctrl_[a.slot];
+      if (a.prefilled < (int)a.prompt.size() || c.phase != kPhDone) continue;
+      rwkvtts_result& r = *a.job->res;
+      if (r.semantic_tokens && c.n_sem > 0) {
+        RT_HIP(hipMemcpyAsync(r.semantic_tokens, d_sem_ + (int64_t)a.slot * RWKVTTS_SEMANTIC_LIMIT,
+                              sizeof(int32_t) * c.n_sem, hipMemcpyDeviceToHost, stream_));
+        copied = true;
+      }
+    }
+    if (copied) RT_HIP(hipStreamSynchronize(stream_));
     for (size_t i = 0; i < act.size();) {
       Active& a = act[i];
       const SlotCtrl& c = h_ctrl_[a.slot];
@@ -1153,11 +1170,6 @@ int Engine::serve(JobSource& src) {
       r.n_global = c.n_global;
       memcpy(r.global_tokens, c.global_out, sizeof(int32_t) * RWKVTTS_N_GLOBAL);
       r.n_semantic = c.n_sem;
-      if (r.semantic_tokens && c.n_sem > 0) {  // on the engine's stream: no null-stream sync
-        RT_HIP(hipMemcpyAsync(r.semantic_tokens, d_sem_ + (int64_t)a.slot * RWKVTTS_SEMANTIC_LIMIT,
-                              sizeof(int32_t) * c.n_sem, hipMemcpyDeviceToHost, stream_));
-        RT_HIP(hipStreamSynchronize(stream_));
-      }
       src.finish(a.job);
       free_slots.push_back(a.slot);
       act.erase(act.begin() + i);
