@@ -1124,7 +1124,17 @@ int Engine::serve(JobSource& src) {
     }
     RT_HIP(hipMemcpyAsync(h_ctrl_, d_ctrl_, sizeof(SlotCtrl) * S_, hipMemcpyDeviceToHost, stream_));
     RT_HIP(hipEventRecord(e1, stream_));
-    RT_HIP(hipEventSynchronize(e1));
+    // the owner thread polls the window's end event instead of sleeping in hipEventSynchronize:
+    // the GPU idles from the window's last kernel until the next window's first graph arrives,
+    // and a blocking wait adds its wake-up latency to that gap once per window
+    static const bool blocking = getenv("RWKVTTS_SYNC_BLOCKING") != nullptr;  // A/B switch
+    if (blocking) {
+      RT_HIP(hipEventSynchronize(e1));
+    } else {
+      hipError_t q;
+      while ((q = hipEventQuery(e1)) == hipErrorNotReady) __builtin_ia32_pause();
+      RT_HIP(q);
+    }
     float ms = 0;
     hipEventElapsedTime(&ms, e0, e1);
     (any_prefill ? stats.prefill_ms : stats.decode_ms) += ms;
