@@ -57,6 +57,8 @@ class JobSource {
   virtual void finish(Job* j) = 0;  // j->res is filled
 };
 
+struct Active;  // a request decoding in a state slot (engine.hip, Engine::serve)
+
 struct ProfEntry {
   std::string name;
   int64_t launches = 0;
@@ -93,6 +95,8 @@ class Engine {
 
  private:
   int run_step(const StepPlan& p, bool upload);
+  int finish_unit(int b, bool prefill, std::vector<Active>& act, std::vector<int>& free_slots, JobSource& src,
+                  hipEvent_t* ev0, hipEvent_t* ev1);
   int launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_from_ctrl, bool advance);
   int upload_plan(const StepPlan& p);
   void prof_begin(hipEvent_t* ev);

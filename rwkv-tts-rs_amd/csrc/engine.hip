@@ -273,7 +273,7 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
   RT_OK(alloc(&logits_, (size_t)splitH_ * Rmax_ * Vpad_));
   RT_OK(alloc(&d_ctrl_, (size_t)S_));
   RT_OK(alloc(&d_sem_, (size_t)S_ * RWKVTTS_SEMANTIC_LIMIT));
-  RT_HIP(hipHostMalloc((void**)&h_ctrl_, sizeof(SlotCtrl) * S_, hipHostMallocDefault));
+  RT_HIP(hipHostMalloc((void**)&h_ctrl_, sizeof(SlotCtrl) * 2 * S_, hipHostMallocDefault));  // 2 snapshots
 
   RT_HIP(hipDeviceSynchronize());
   return RWKVTTS_OK;
@@ -862,7 +862,6 @@ int Engine::sample(const float* logits, int n_rows, int row_len, const rwkvtts_s
 // ------------------------------------------------------------------------------------------
 // Continuous-batching scheduler (DynamicBatchManager semantics, src/dynamic_batch_manager.rs)
 // ------------------------------------------------------------------------------------------
-namespace {
 struct Active {
   Job* job;
   int slot;
@@ -872,6 +871,8 @@ struct Active {
   int total = 0;     // advances after which the request is certainly done (its step limit)
   bool zero_shot = false;
 };
+
+namespace {
 
 // generate_batch: a fixed list of requests
 class ListSource : public JobSource {
@@ -942,15 +943,92 @@ int Engine::generate(const rwkvtts_request* reqs, int n, rwkvtts_result* res) {
   return serve(src);
 }
 
+// Waits for a unit's end event (polling: a blocking wait adds its wake-up latency to the GPU's
+// idle gap), accounts its time, and retires the slots its control-block snapshot shows done.
+int Engine::finish_unit(int b, bool prefill, std::vector<Active>& act, std::vector<int>& free_slots, JobSource& src,
+                        hipEvent_t* ev0, hipEvent_t* ev1) {
+  static const bool blocking = getenv("RWKVTTS_SYNC_BLOCKING") != nullptr;  // A/B switch
+  if (blocking) {
+    RT_HIP(hipEventSynchronize(ev1[b]));
+  } else {
+    hipError_t q;
+    while ((q = hipEventQuery(ev1[b])) == hipErrorNotReady) __builtin_ia32_pause();
+    RT_HIP(q);
+  }
+  float ms = 0;
+  hipEventElapsedTime(&ms, ev0[b], ev1[b]);
+  (prefill ? stats.prefill_ms : stats.decode_ms) += ms;
+  RT_OK(flush_prof());
+  if (d_tl_ && !prefill && stats.steps > 40) {  // semantic-phase steps only
+    std::vector<unsigned long long> h((size_t)kTlStride * kTlMax);
+    RT_HIP(hipMemcpy(h.data(), d_tl_, h.size() * 8, hipMemcpyDeviceToHost));
+    const int n = (int)tl_names_.size();
+    tl_start_.resize(n, 0.0);
+    tl_dur_.resize(n, 0.0);
+    for (int i = 0; i < n; ++i) {
+      const unsigned long long* q = h.data() + (size_t)kTlStride * i;
+      unsigned long long e = 0;
+      for (int j = 2; j < kTlStride; ++j) e = std::max(e, q[j]);
+      tl_start_[i] += (double)(q[0] - h[0]) * 0.01;  // us
+      tl_dur_[i] += (double)(e - q[0]) * 0.01;
+    }
+    tl_steps_++;
+  }
+  // retire finished slots: every finished slot's tokens copied on the engine's stream (no
+  // null-stream sync), one synchronisation, then the jobs are handed back
+  const SlotCtrl* snap = h_ctrl_ + (size_t)b * S_;
+  bool copied = false;
+  for (auto& a : act) {
+    const SlotCtrl& c = snap[a.slot];
+    if (a.prefilled < (int)a.prompt.size() || c.phase != kPhDone) continue;
+    rwkvtts_result& r = *a.job->res;
+    if (r.semantic_tokens && c.n_sem > 0) {
+      RT_HIP(hipMemcpyAsync(r.semantic_tokens, d_sem_ + (int64_t)a.slot * RWKVTTS_SEMANTIC_LIMIT,
+                            sizeof(int32_t) * c.n_sem, hipMemcpyDeviceToHost, stream_));
+      copied = true;
+    }
+  }
+  if (copied) RT_HIP(hipStreamSynchronize(stream_));
+  for (size_t i = 0; i < act.size();) {
+    Active& a = act[i];
+    const SlotCtrl& c = snap[a.slot];
+    if (a.prefilled < (int)a.prompt.size() || c.phase != kPhDone) {
+      ++i;
+      continue;
+    }
+    rwkvtts_result& r = *a.job->res;
+    r.status = 0;
+    r.n_global = c.n_global;
+    memcpy(r.global_tokens, c.global_out, sizeof(int32_t) * RWKVTTS_N_GLOBAL);
+    r.n_semantic = c.n_sem;
+    src.finish(a.job);
+    free_slots.push_back(a.slot);
+    act.erase(act.begin() + i);
+  }
+  return RWKVTTS_OK;
+}
+
 int Engine::serve(JobSource& src) {
   RT_HIP(hipSetDevice(device_));
   std::vector<int> free_slots;
   for (int s = S_ - 1; s >= 0; --s) free_slots.push_back(s);
   std::vector<Active> act;
   std::random_device rd;
-  hipEvent_t e0, e1;
-  RT_HIP(hipEventCreate(&e0));
-  RT_HIP(hipEventCreate(&e1));
+  // Each unit of work (a mixed step or a decode window) ends with a control-block snapshot into
+  // its own pinned buffer and an end event. In steady decode (no admission possible, no prompt
+  // rows, the plan uploaded earlier, no slot able to pass its step limit) the next window is
+  // launched before the host reads the previous one's snapshot, so the GPU does not idle while
+  // the host polls, retires and relaunches. A slot that finished inside the older window idles
+  // (k_advance skips it) through the newer one; every later operation on it is stream-ordered.
+  hipEvent_t ev0[2], ev1[2];
+  for (int i = 0; i < 2; ++i) {
+    RT_HIP(hipEventCreate(&ev0[i]));
+    RT_HIP(hipEventCreate(&ev1[i]));
+  }
+  struct Unit {
+    bool valid = false, prefill = false;
+    int buf = 0;
+  } pending;
   bool open = true, decode_plan_valid = false;
   StepPlan dp;  // the decode plan (all active slots, tokens from the control blocks)
   std::vector<Job*> fresh;
@@ -1043,8 +1121,9 @@ int Engine::serve(JobSource& src) {
     bool any_prefill = false;
     for (auto& a : act) any_prefill |= a.prefilled < (int)a.prompt.size();
     int K = 1;
-    bool all_global = true;
-    RT_HIP(hipEventRecord(e0, stream_));
+    bool all_global = true, uploaded = false;
+    const int b = pending.valid ? pending.buf ^ 1 : 0;  // this unit's snapshot buffer / events
+    RT_HIP(hipEventRecord(ev0[b], stream_));
     if (any_prefill) {
       // ---- mixed step: every decoding slot's row (token from its control block) plus prompt
       // rows of the admitted slots, up to token_chunk_size rows; the decoding slots never stall
@@ -1105,6 +1184,7 @@ int Engine::serve(JobSource& src) {
         }
         if ((rc = upload_plan(dp)) != RWKVTTS_OK) break;
         decode_plan_valid = true;
+        uploaded = true;
       }
       K = (profiling || d_tl_) ? 1 : kLookahead;
       for (auto& a : act) K = std::min(K, std::max(1, a.total - a.advances));
@@ -1122,72 +1202,36 @@ int Engine::serve(JobSource& src) {
       stats.decode_rows += (int64_t)dp.rows.size() * K;
       max_active = std::max<int64_t>(max_active, (int64_t)dp.rows.size());
     }
-    RT_HIP(hipMemcpyAsync(h_ctrl_, d_ctrl_, sizeof(SlotCtrl) * S_, hipMemcpyDeviceToHost, stream_));
-    RT_HIP(hipEventRecord(e1, stream_));
-    // the owner thread polls the window's end event instead of sleeping in hipEventSynchronize:
-    // the GPU idles from the window's last kernel until the next window's first graph arrives,
-    // and a blocking wait adds its wake-up latency to that gap once per window
-    static const bool blocking = getenv("RWKVTTS_SYNC_BLOCKING") != nullptr;  // A/B switch
-    if (blocking) {
-      RT_HIP(hipEventSynchronize(e1));
+    RT_HIP(hipMemcpyAsync(h_ctrl_ + (size_t)b * S_, d_ctrl_, sizeof(SlotCtrl) * S_, hipMemcpyDeviceToHost, stream_));
+    RT_HIP(hipEventRecord(ev1[b], stream_));
+    Unit now;
+    now.valid = true;
+    now.prefill = any_prefill;
+    now.buf = b;
+    // the older unit first (its retirements are stream-ordered after this one), then this one
+    // unless the next window may go out before its snapshot is read
+    if (pending.valid) {
+      const Unit u = pending;
+      pending.valid = false;
+      if ((rc = finish_unit(u.buf, u.prefill, act, free_slots, src, ev0, ev1)) != RWKVTTS_OK) break;
+      if (act.size() != dp.rows.size()) decode_plan_valid = false;
+    }
+    static const bool no_ahead = getenv("RWKVTTS_NO_AHEAD") != nullptr;  // A/B switch
+    bool ahead = !no_ahead && !any_prefill && !uploaded && use_graphs_ && !profiling && !d_tl_ &&
+                 (!open || free_slots.empty());
+    for (auto& a : act) ahead &= a.total - a.advances >= 1;
+    if (ahead) {
+      pending = now;
     } else {
-      hipError_t q;
-      while ((q = hipEventQuery(e1)) == hipErrorNotReady) __builtin_ia32_pause();
-      RT_HIP(q);
-    }
-    float ms = 0;
-    hipEventElapsedTime(&ms, e0, e1);
-    (any_prefill ? stats.prefill_ms : stats.decode_ms) += ms;
-    if ((rc = flush_prof()) != RWKVTTS_OK) break;
-    if (d_tl_ && !any_prefill && stats.steps > 40) {  // semantic-phase steps only
-      std::vector<unsigned long long> h((size_t)kTlStride * kTlMax);
-      RT_HIP(hipMemcpy(h.data(), d_tl_, h.size() * 8, hipMemcpyDeviceToHost));
-      const int n = (int)tl_names_.size();
-      tl_start_.resize(n, 0.0);
-      tl_dur_.resize(n, 0.0);
-      for (int i = 0; i < n; ++i) {
-        const unsigned long long* q = h.data() + (size_t)kTlStride * i;
-        unsigned long long e = 0;
-        for (int j = 2; j < kTlStride; ++j) e = std::max(e, q[j]);
-        tl_start_[i] += (double)(q[0] - h[0]) * 0.01;  // us
-        tl_dur_[i] += (double)(e - q[0]) * 0.01;
-      }
-      tl_steps_++;
-    }
-    // ---- retire finished slots: every finished slot's tokens copied on the engine's stream (no
-    // null-stream sync), one synchronisation, then the jobs are handed back
-    bool copied = false;
-    for (auto& a : act) {
-      const SlotCtrl& c = h_ctrl_[a.slot];
-      if (a.prefilled < (int)a.prompt.size() || c.phase != kPhDone) continue;
-      rwkvtts_result& r = *a.job->res;
-      if (r.semantic_tokens && c.n_sem > 0) {
-        RT_HIP(hipMemcpyAsync(r.semantic_tokens, d_sem_ + (int64_t)a.slot * RWKVTTS_SEMANTIC_LIMIT,
-                              sizeof(int32_t) * c.n_sem, hipMemcpyDeviceToHost, stream_));
-        copied = true;
-      }
-    }
-    if (copied) RT_HIP(hipStreamSynchronize(stream_));
-    for (size_t i = 0; i < act.size();) {
-      Active& a = act[i];
-      const SlotCtrl& c = h_ctrl_[a.slot];
-      if (a.prefilled < (int)a.prompt.size() || c.phase != kPhDone) {
-        ++i;
-        continue;
-      }
-      rwkvtts_result& r = *a.job->res;
-      r.status = 0;
-      r.n_global = c.n_global;
-      memcpy(r.global_tokens, c.global_out, sizeof(int32_t) * RWKVTTS_N_GLOBAL);
-      r.n_semantic = c.n_sem;
-      src.finish(a.job);
-      free_slots.push_back(a.slot);
-      act.erase(act.begin() + i);
-      decode_plan_valid = false;
+      if ((rc = finish_unit(now.buf, now.prefill, act, free_slots, src, ev0, ev1)) != RWKVTTS_OK) break;
+      if (act.size() != dp.rows.size()) decode_plan_valid = false;
     }
   }
-  hipEventDestroy(e0);
-  hipEventDestroy(e1);
+  if (pending.valid || rc != RWKVTTS_OK) (void)hipStreamSynchronize(stream_);
+  for (int i = 0; i < 2; ++i) {
+    hipEventDestroy(ev0[i]);
+    hipEventDestroy(ev1[i]);
+  }
   if (rc != RWKVTTS_OK) {  // engine failure: every job still in flight fails with it
     for (auto& a : act) {
       a.job->res->status = rc;
