@@ -150,7 +150,9 @@ typedef struct rwkvtts_engine rwkvtts_engine;
 typedef struct {
   int32_t device;           /* HIP device ordinal */
   int32_t max_slots;        /* state slots = Bundle max_batch (shared_runtime.rs:177) */
-  int32_t token_chunk_size; /* rows per forward = RnnInput token_chunk_size (lightweight_tts_pipeline.rs:799) */
+  int32_t token_chunk_size; /* prompt rows per forward step, shared by the admitted requests (the
+                               reference's per-request RnnInput token_chunk_size, 512 at
+                               lightweight_tts_pipeline.rs:799; outputs are chunk-invariant) */
   int32_t use_graphs;       /* capture decode steps in hipGraphs */
   int32_t wkv_variant;      /* 0 auto; 1 k_wkv4 (2 waves per (slot, head)); 2 k_wkv6 (4 waves).
                                0.4B LoRA ranks only; both are tested against the oracle */
