@@ -500,7 +500,7 @@ class Codec {
     RT_HIP(hipFuncSetAttribute((const void*)k_conv<TN, KT>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     RT_CONV_ATTR(32, 1) RT_CONV_ATTR(32, 3) RT_CONV_ATTR(32, 7)
     RT_CONV_ATTR(64, 1) RT_CONV_ATTR(64, 3) RT_CONV_ATTR(64, 7)
-    RT_CONV_ATTR(96, 1) RT_CONV_ATTR(192, 1) RT_CONV_ATTR(48, 1) RT_CONV_ATTR(48, 3) RT_CONV_ATTR(48, 7)
+    RT_CONV_ATTR(96, 1) RT_CONV_ATTR(96, 7) RT_CONV_ATTR(192, 1) RT_CONV_ATTR(48, 1) RT_CONV_ATTR(48, 3) RT_CONV_ATTR(48, 7)
 #undef RT_CONV_ATTR
     RT_HIP(hipFuncSetAttribute((const void*)k_conv_out, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     // zero page: out-of-range window rows read zeros at channel offsets up to the largest Ci
@@ -601,7 +601,15 @@ class Codec {
     const int ntaps_max = mode == 1 ? (K + s - 1) / s : K;
     const int span = (ntaps_max - 1) * (mode == 1 ? 1 : dil);
     const int KT = ntaps_max <= 1 ? 1 : (ntaps_max <= 3 ? 3 : 7);
-    const int nwv = TN >= 96 ? 4 : conv_waves(KT), TM = 32 * nwv;
+    {  // 7-tap convs: 96-wide column tiles wherever the double-buffered chunk (window + 7 taps'
+       // weights) fits the LDS: fewer column tiles re-reading each window (residual conv7 33.4 ->
+       // 31.1 ms per batch; tests bit-identical: the per-element accumulation order is unchanged)
+      static const int tn7 = getenv("RWKVTTS_CONV7_TN") ? atoi(getenv("RWKVTTS_CONV7_TN")) : 96;  // A/B switch
+      const int wr = (256 + span + 15) & ~15;
+      if (KT == 7 && mode == 0 && tn7 == 96 && Co % 96 == 0 && 2 * (size_t)(2 * wr + ntaps_max * 96) * 64 <= 160 * 1024)
+        TN = 96;
+    }
+    const int nwv = (TN >= 96 && KT == 1) ? 4 : conv_waves(KT), TM = 32 * nwv;
     const int WRp = (TM + span + 15) & ~15;
     const size_t shm = std::max(2 * (size_t)(2 * WRp + ntaps_max * TN) * 64,        // two chunk buffers
                                 (size_t)nwv * 32 * (TN + 4) * sizeof(float));        // epilogue tiles
@@ -628,6 +636,7 @@ class Codec {
     pbeg();
     const int nthr = 64 * nwv;
     if (TN == 192) k_conv<192, 1><<<grid, nthr, shm, stream>>>(a);
+    else if (TN == 96 && KT == 7) k_conv<96, 7><<<grid, nthr, shm, stream>>>(a);
     else if (TN == 96) k_conv<96, 1><<<grid, nthr, shm, stream>>>(a);
     else if (TN == 48) {
       if (KT == 1) k_conv<48, 1><<<grid, nthr, shm, stream>>>(a);
