@@ -500,7 +500,7 @@ class Codec {
     RT_HIP(hipFuncSetAttribute((const void*)k_conv<TN, KT>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     RT_CONV_ATTR(32, 1) RT_CONV_ATTR(32, 3) RT_CONV_ATTR(32, 7)
     RT_CONV_ATTR(64, 1) RT_CONV_ATTR(64, 3) RT_CONV_ATTR(64, 7)
-    RT_CONV_ATTR(96, 1) RT_CONV_ATTR(96, 7) RT_CONV_ATTR(192, 1) RT_CONV_ATTR(48, 1) RT_CONV_ATTR(48, 3) RT_CONV_ATTR(48, 7)
+    RT_CONV_ATTR(96, 1) RT_CONV_ATTR(96, 3) RT_CONV_ATTR(96, 7) RT_CONV_ATTR(192, 1) RT_CONV_ATTR(48, 1) RT_CONV_ATTR(48, 3) RT_CONV_ATTR(48, 7)
 #undef RT_CONV_ATTR
     RT_HIP(hipFuncSetAttribute((const void*)k_conv_out, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     // zero page: out-of-range window rows read zeros at channel offsets up to the largest Ci
@@ -608,8 +608,12 @@ class Codec {
       const int wr = (256 + span + 15) & ~15;
       if (KT == 7 && mode == 0 && tn7 == 96 && Co % 96 == 0 && 2 * (size_t)(2 * wr + ntaps_max * 96) * 64 <= 160 * 1024)
         TN = 96;
+      // ConvTranspose: 96-wide tiles measured faster at 96 and 384 output channels (2.54 -> 2.14,
+      // 2.30 -> 2.10 ms per batch), slower at 192 (2.51 -> 2.62), equal at 768
+      static const int tnT = getenv("RWKVTTS_CONVT_TN") ? atoi(getenv("RWKVTTS_CONVT_TN")) : -1;  // A/B switch
+      if (mode == 1 && KT == 3 && Co % 96 == 0 && (tnT == 96 || (tnT < 0 && (Co == 96 || Co == 384)))) TN = 96;
     }
-    const int nwv = (TN >= 96 && KT == 1) ? 4 : conv_waves(KT), TM = 32 * nwv;
+    const int nwv = (TN >= 96 && KT != 7) ? 4 : conv_waves(KT), TM = 32 * nwv;
     const int WRp = (TM + span + 15) & ~15;
     const size_t shm = std::max(2 * (size_t)(2 * WRp + ntaps_max * TN) * 64,        // two chunk buffers
                                 (size_t)nwv * 32 * (TN + 4) * sizeof(float));        // epilogue tiles
@@ -637,6 +641,7 @@ class Codec {
     const int nthr = 64 * nwv;
     if (TN == 192) k_conv<192, 1><<<grid, nthr, shm, stream>>>(a);
     else if (TN == 96 && KT == 7) k_conv<96, 7><<<grid, nthr, shm, stream>>>(a);
+    else if (TN == 96 && KT == 3) k_conv<96, 3><<<grid, nthr, shm, stream>>>(a);
     else if (TN == 96) k_conv<96, 1><<<grid, nthr, shm, stream>>>(a);
     else if (TN == 48) {
       if (KT == 1) k_conv<48, 1><<<grid, nthr, shm, stream>>>(a);
