@@ -809,7 +809,9 @@ class Codec {
                        3 * dils[r], 1, F(2, ub, CU_R0_B7 + o), o7))) return rc;
         cur ^= 1;
         ConvOut o1;
-        o1.y = xf;
+        // the f32 residual stream after a stage's last unit is never read (the next ConvTranspose
+        // or conv_out reads the planes, and the ConvTranspose rewrites xf): planes only
+        o1.y = r < 2 ? xf : nullptr;
         o1.res = xf;
         o1.p = pp[cur ^ 1];
         o1.alpha = r < 2 ? F(2, ub, CU_R0_A1 + o + (CU_R1_A1 - CU_R0_A1))
