@@ -1383,6 +1383,28 @@ __device__ inline float load_logit(const AdvanceArgs& a, const float* lg, int i)
   return v;
 }
 
+// The row's logits into LDS: four elements per round with all their partial-slab loads issued
+// before any add (each element still sums its slabs in order p = 0, 1, ...: same values)
+template <int NT>
+__device__ inline void load_logits_row(const AdvanceArgs& a, const float* lg, float* p, int n) {
+  int i = threadIdx.x;
+  for (; i + 3 * NT < n; i += 4 * NT) {
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = lg[i + u * NT];
+    for (int q = 1; q < a.n_part; ++q) {
+      float w[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) w[u] = lg[q * a.part_stride + i + u * NT];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] += w[u];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) p[i + u * NT] = v[u];
+  }
+  for (; i < n; i += NT) p[i] = load_logit(a, lg, i);
+}
+
 __device__ __attribute__((always_inline)) void advance_body(const AdvanceArgs& a, char* smem) {
   constexpr int NT = kSampleThreads;
   const int row = blockIdx.x;
@@ -1403,7 +1425,7 @@ __device__ __attribute__((always_inline)) void advance_body(const AdvanceArgs& a
   const float* lg = a.logits + (int64_t)row * a.ld;
   if (phase == kPhGlobal) {
     const SampleSmem sm = carve<NT>(smem, 4096);
-    for (int i = threadIdx.x; i < 4096; i += NT) sm.p[i] = load_logit(a, lg, i);
+    load_logits_row<NT>(a, lg, sm.p, 4096);
     __syncthreads();
     int status;
     const int id = sample_block<NT>(sm, 4096, 1.0f, 0.95f, c->top_k_g, c->gkey, c->gdraw, false,
@@ -1420,7 +1442,7 @@ __device__ __attribute__((always_inline)) void advance_body(const AdvanceArgs& a
   constexpr int NS = RWKVTTS_EOS_TOKEN + 1;
   const SampleSmem sm = carve<NT>(smem, NS);
   const bool eos_masked = c->fixed || (c->mode == 1 && c->n_sem < c->hard_min);
-  for (int i = threadIdx.x; i < NS; i += NT) sm.p[i] = load_logit(a, lg, i);
+  load_logits_row<NT>(a, lg, sm.p, NS);
   __syncthreads();
   if (threadIdx.x == 0 && eos_masked) sm.p[RWKVTTS_EOS_TOKEN] = -__builtin_inff();
   __syncthreads();
