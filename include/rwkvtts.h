@@ -293,7 +293,11 @@ typedef struct {
   int32_t max_batch_size;                 /* DynamicBatchConfig.max_batch_size (batch_types.rs:71) */
   int32_t collect_timeout_ms;             /* DynamicBatchConfig.collect_timeout_ms (batch_types.rs:73) */
 } rwkvtts_manager_desc;
-/* weights: one host blob, uploaded to every engine's device. */
+/* weights: one host blob. It crosses PCIe once, into the first engine's device; the manager then
+ * broadcasts it over RCCL (ncclBroadcast over xGMI, one rank per distinct device, ncclCommInitAll)
+ * to the other devices, and engines that share a device copy it device-to-device. This replaces
+ * the reference's single model load handed to every infer worker (src/shared_runtime.rs:143-184,
+ * src/dynamic_batch_manager.rs:33-87). */
 int rwkvtts_manager_create(const rwkvtts_manager_desc* desc, const void* weights, size_t bytes,
                            rwkvtts_manager** out);
 /* Stops the collector and the engine threads after the requests already submitted finish. */
@@ -314,6 +318,9 @@ typedef struct {
   int64_t served[RWKVTTS_MAX_ENGINES];      /* requests completed per engine */
   int64_t max_active[RWKVTTS_MAX_ENGINES];  /* most slots an engine had decoding at once */
   int64_t steps[RWKVTTS_MAX_ENGINES];       /* forward steps per engine */
+  int32_t bcast_ranks;                      /* distinct devices in the weight broadcast (RCCL ranks) */
+  int32_t bcast_rccl;                       /* 1: the weights went out by ncclBroadcast */
+  double bcast_ms;                          /* upload + broadcast wall time at create */
 } rwkvtts_manager_stats;
 int rwkvtts_manager_get_stats(rwkvtts_manager* m, rwkvtts_manager_stats* out);
 

@@ -31,7 +31,8 @@ struct ConvArgs {
   const bf16_t* xl;
   int64_t x_bs;      // per-utterance stride (elements)
   int Ci, tin_mul;
-  const bf16_t* w;   // [Co][K][Ci]
+  const bf16_t* w;   // [Co][K][Ci]: bf16 hi part of the f32 weights
+  const bf16_t* wl;  // WLO kernels: bf16 lo part (w_f32 = hi + lo to ~2^-16 relative)
   int K, Co;
   int mode;          // 0: conv (dil, pad), 1: ConvTranspose (stride s, pad (K - s) / 2)
   int dil, pad, s;
@@ -75,6 +76,16 @@ __device__ inline void split_store(bf16_t* h, bf16_t* l, int64_t o, float v) {
 // run one wave per SIMD and expose every wait; 8 waves share the same weight tiles.
 constexpr int conv_waves(int KT) { return KT == 7 ? 8 : 4; }
 
+// every k_conv instantiation the host dispatches: (column tile, taps class, weight lo plane, waves)
+#define RT_CONV_KERNELS(X)                                                                       \
+  X(32, 1, false, 4) X(32, 3, false, 4) X(32, 7, false, 8) X(48, 1, false, 4) X(48, 3, false, 4)    \
+  X(48, 7, false, 8) X(64, 1, false, 4) X(64, 3, false, 4) X(64, 7, false, 8) X(96, 1, false, 4)    \
+  X(96, 3, false, 4) X(96, 7, false, 8) X(192, 1, false, 4)                                         \
+  X(32, 1, true, 4) X(48, 1, true, 4) X(64, 1, true, 4) X(96, 1, true, 4)                           \
+  X(32, 3, true, 4) X(48, 3, true, 4) X(64, 3, true, 4) X(96, 3, true, 4)                           \
+  X(32, 7, true, 8) X(48, 7, true, 8) X(64, 7, true, 8) X(96, 7, true, 8)                           \
+  X(48, 7, true, 4) X(64, 7, true, 4) X(96, 7, true, 4)
+
 // LDS image of a 32-channel chunk: 64-B rows of four 16-B pieces, piece p of row r stored at
 // slot p ^ ((r >> 1) & 3): the MFMA fragment reads (16 rows x 4 pieces per ds_read_b128 lane
 // group) are then bank-conflict free. The image is filled by global_load_lds_dwordx4 (one
@@ -86,14 +97,17 @@ __device__ inline void glds16(const void* g, void* l) {
                                    (__attribute__((address_space(3))) void*)l, 16, 0, 0);
 }
 
-// Workgroup = 4 waves along time, each 32 rows x TN channels (2 x TN/16 MFMA 16x16x32 tiles).
+// Workgroup = NWV waves along time, each 32 rows x TN channels (2 x TN/16 MFMA 16x16x32 tiles).
 // Per 32-channel chunk the workgroup stages (double-buffered, async global->LDS) the input
 // window that ALL taps read -- TM + (ntaps - 1) * |tap stride| rows of the hi and lo planes --
 // and the chunk of every tap's weights, then runs ntaps x 2 x NT x 2 MFMAs per wave while the
-// next chunk streams in.
-template <int TN, int KT>
-__global__ __launch_bounds__(64 * conv_waves(KT), conv_waves(KT) == 8 ? 1 : 2) void k_conv(ConvArgs a) {
-  constexpr int NWV = conv_waves(KT), TM = 32 * NWV, NT = TN / 16;
+// next chunk streams in. WLO: f32 weights that bf16 cannot hold (real checkpoints; the reference
+// runs this decoder in fp32 on ORT) are staged as hi + lo planes too, and every product takes a
+// third MFMA x_hi * w_lo: weights enter at ~2^-16 relative, as the activations do. With w_lo = 0
+// the third MFMA adds exact zeros, so a WLO launch on bf16-exact weights is bit-identical.
+template <int TN, int KT, bool WLO = false, int NWV = conv_waves(KT)>
+__global__ __launch_bounds__(64 * NWV, NWV == 8 ? 1 : 2) void k_conv(ConvArgs a) {
+  constexpr int TM = 32 * NWV, NT = TN / 16;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int req = blockIdx.z;
   const int Tin = a.ntok[req] * a.tin_mul;
@@ -120,7 +134,8 @@ __global__ __launch_bounds__(64 * conv_waves(KT), conv_waves(KT) == 8 ? 1 : 2) v
   const int WRp = (TM + span + 15) & ~15;  // window rows, whole 16-row blocks
   const int wlo = pstep < 0 ? -span : 0;   // window row 0 <-> position q0 + pbase + wlo
   const int wstart = q0 + pbase + wlo;
-  const int nAblk = 2 * WRp / 16, nblk = nAblk + ntaps * (TN / 16);
+  const int nWblk = ntaps * (TN / 16);  // one weight plane's blocks
+  const int nAblk = 2 * WRp / 16, nblk = nAblk + (WLO ? 2 : 1) * nWblk;
   const int buf_bytes = nblk * 1024;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, g = lane >> 4;
   const int64_t xoff = req * a.x_bs;
@@ -141,9 +156,10 @@ __global__ __launch_bounds__(64 * conv_waves(KT), conv_waves(KT) == 8 ? 1 : 2) v
       if (pos >= 0 && pos < Tin) src = (plane ? a.xl : a.xh) + xoff + (int64_t)pos * a.Ci + piece * 8;
       else src = a.zeros + piece * 8;
     } else if (b < nblk) {
-      const int wb = b - nAblk, tap = wb / (TN / 16), co = (wb % (TN / 16)) * 16 + lrow;
+      const int wb0 = b - nAblk, lo = wb0 >= nWblk, wb = wb0 - (lo ? nWblk : 0);
+      const int tap = wb / (TN / 16), co = (wb % (TN / 16)) * 16 + lrow;
       const int piece = lslot ^ ((co >> 1) & 3);
-      src = a.w + ((int64_t)(co0 + co) * a.K + k0 + tap * kstep) * a.Ci + piece * 8;
+      src = (lo ? a.wl : a.w) + ((int64_t)(co0 + co) * a.K + k0 + tap * kstep) * a.Ci + piece * 8;
     }
     srcp[u] = src;
   }
@@ -169,12 +185,17 @@ __global__ __launch_bounds__(64 * conv_waves(KT), conv_waves(KT) == 8 ? 1 : 2) v
     if (ck + 1 < nck) issue(ck + 1, lds + ((ck + 1) & 1) * buf_bytes);
     const uint8_t* sA = cur;
     const uint8_t* sW = cur + nAblk * 1024;
+    const uint8_t* sWl = sW + nWblk * 1024;
 #pragma unroll
     for (int j = 0; j < KT; ++j) {
       if (j >= ntaps) break;
-      short8 bw[NT];
+      short8 bw[NT], bwl[WLO ? NT : 1];
 #pragma unroll
       for (int n = 0; n < NT; ++n) bw[n] = *(const short8*)(sW + j * TN * 64 + swz(n * 16 + li, g));
+      if constexpr (WLO) {
+#pragma unroll
+        for (int n = 0; n < NT; ++n) bwl[n] = *(const short8*)(sWl + j * TN * 64 + swz(n * 16 + li, g));
+      }
 #pragma unroll
       for (int m = 0; m < 2; ++m) {
         const int wr = wave * 32 + m * 16 + li + j * pstep - wlo;
@@ -186,6 +207,9 @@ __global__ __launch_bounds__(64 * conv_waves(KT), conv_waves(KT) == 8 ? 1 : 2) v
                                                               __builtin_bit_cast(cbf16x8, bw[n]), acc[m][n], 0, 0, 0);
           acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(cbf16x8, al),
                                                               __builtin_bit_cast(cbf16x8, bw[n]), acc[m][n], 0, 0, 0);
+          if constexpr (WLO)
+            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(cbf16x8, ah),
+                                                                __builtin_bit_cast(cbf16x8, bwl[n]), acc[m][n], 0, 0, 0);
         }
       }
     }
@@ -402,9 +426,13 @@ __global__ __launch_bounds__(256) void k_conv_out(const bf16_t* xh, const bf16_t
   pcm[req * p_bs + t] = tanhf(acc + b[0]);
 }
 
-__global__ void k_f32_to_bf16(const float* in, bf16_t* out, int64_t n) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    out[i] = f32_to_bf16(in[i]);
+// f32 weights -> bf16 hi + lo planes (w = hi + lo to ~2^-16 relative; lo = 0 for bf16-exact w)
+__global__ void k_f32_split_bf16(const float* in, bf16_t* hi, bf16_t* lo, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint16_t h = f32_to_bf16(in[i]);
+    hi[i] = h;
+    lo[i] = f32_to_bf16(in[i] - bf16_to_f32(h));
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -422,7 +450,9 @@ class Codec {
   hipStream_t stream = nullptr;
   float* wf = nullptr;   // f32 blob on device
   bf16_t* zeros = nullptr;
-  bf16_t* wb = nullptr;  // bf16 mirror (same element offsets) for MFMA operands
+  bf16_t* wb = nullptr;  // bf16 mirror (same element offsets) for MFMA operands: hi part
+  bf16_t* wlb = nullptr; // lo part (f32 - hi), read by the WLO conv kernels
+  bool wlo = false;      // some conv weight is not bf16-exact: three MFMAs per product
   int cap_n = 0, cap_T = 0;
   int *d_tok = nullptr, *d_glob = nullptr, *d_ntok = nullptr;
   // prenet: x f32 residual stream [n][T][P]; zp/up/hp planes [n][T][L|P|I]
@@ -441,6 +471,7 @@ class Codec {
     release();
     if (wf) (void)hipFree(wf);
     if (wb) (void)hipFree(wb);
+    if (wlb) (void)hipFree(wlb);
     if (zeros) (void)hipFree(zeros);
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -496,11 +527,9 @@ class Codec {
         RT_HIP(hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, least));
       }
     }
-#define RT_CONV_ATTR(TN, KT) \
-    RT_HIP(hipFuncSetAttribute((const void*)k_conv<TN, KT>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    RT_CONV_ATTR(32, 1) RT_CONV_ATTR(32, 3) RT_CONV_ATTR(32, 7)
-    RT_CONV_ATTR(64, 1) RT_CONV_ATTR(64, 3) RT_CONV_ATTR(64, 7)
-    RT_CONV_ATTR(96, 1) RT_CONV_ATTR(96, 3) RT_CONV_ATTR(96, 7) RT_CONV_ATTR(192, 1) RT_CONV_ATTR(48, 1) RT_CONV_ATTR(48, 3) RT_CONV_ATTR(48, 7)
+#define RT_CONV_ATTR(TN_, KT_, WLO_, NWV_) \
+    RT_HIP(hipFuncSetAttribute((const void*)k_conv<TN_, KT_, WLO_, NWV_>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    RT_CONV_KERNELS(RT_CONV_ATTR)
 #undef RT_CONV_ATTR
     RT_HIP(hipFuncSetAttribute((const void*)k_conv_out, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     // zero page: out-of-range window rows read zeros at channel offsets up to the largest Ci
@@ -509,8 +538,13 @@ class Codec {
     const int64_t n = rwkvtts_codec_offset(&d, -1, 0, 0);
     RT_HIP(hipMalloc(&wf, n * sizeof(float)));
     RT_HIP(hipMalloc(&wb, n * sizeof(bf16_t)));
+    RT_HIP(hipMalloc(&wlb, n * sizeof(bf16_t)));
     RT_HIP(hipMemcpy(wf, host_w, n * sizeof(float), hipMemcpyHostToDevice));
-    k_f32_to_bf16<<<2048, 256, 0, stream>>>(wf, wb, n);
+    k_f32_split_bf16<<<2048, 256, 0, stream>>>(wf, wb, wlb, n);
+    // the MFMA convs take the three-product path when any of their weights is not bf16-exact
+    // (RWKVTTS_CODEC_WLO=0 / 1 forces the choice: A/B timing)
+    wlo = !conv_weights_bf16_exact(host_w);
+    if (const char* e = getenv("RWKVTTS_CODEC_WLO")) wlo = atoi(e) != 0;
     RT_HIP(hipGetLastError());
     RT_HIP(hipStreamSynchronize(stream));
     // largest per-frame activation of the WaveGenerator (conv_in or any up stage)
@@ -547,6 +581,25 @@ class Codec {
     cap_n = n;
     cap_T = T;
     return RWKVTTS_OK;
+  }
+
+  // every tensor the MFMA conv kernel reads as weights
+  bool conv_weights_bf16_exact(const float* w) const {
+    std::vector<std::pair<int64_t, int64_t>> ts;  // (offset, count)
+    auto add = [&](int g, int i, int t) {
+      ts.push_back({rwkvtts_codec_offset(&d, g, i, t), rwkvtts_codec_numel(&d, g, i, t)});
+    };
+    for (int t : {CD_PRE_W, CD_EMB_W, CD_LIN_W, CD_CIN_W}) add(0, 0, t);
+    for (int l = 0; l < d.prenet_layers; ++l)
+      for (int t : {CB_PW1_W, CB_PW2_W}) add(1, l, t);
+    for (int ub = 0; ub < d.n_up; ++ub)
+      for (int t : {CU_T_W, CU_R0_W7, CU_R0_W1, CU_R1_W7, CU_R1_W1, CU_R2_W7, CU_R2_W1}) add(2, ub, t);
+    for (auto& tc : ts)
+      for (int64_t i = 0; i < tc.second; ++i) {
+        const float x = w[tc.first + i];
+        if (bf16_to_f32(f32_to_bf16(x)) != x) return false;
+      }
+    return true;
   }
 
   hipEvent_t ev0 = nullptr;
@@ -613,14 +666,35 @@ class Codec {
       static const int tnT = getenv("RWKVTTS_CONVT_TN") ? atoi(getenv("RWKVTTS_CONVT_TN")) : -1;  // A/B switch
       if (mode == 1 && KT == 3 && Co % 96 == 0 && (tnT == 96 || (tnT < 0 && (Co == 96 || Co == 384)))) TN = 96;
     }
-    const int nwv = (TN >= 96 && KT != 7) ? 4 : conv_waves(KT), TM = 32 * nwv;
-    const int WRp = (TM + span + 15) & ~15;
-    const size_t shm = std::max(2 * (size_t)(2 * WRp + ntaps_max * TN) * 64,        // two chunk buffers
-                                (size_t)nwv * 32 * (TN + 4) * sizeof(float));        // epilogue tiles
-    RT_CHECK(shm <= 160 * 1024 && (2 * WRp + ntaps_max * TN) / 16 <= 16 * nwv && ntaps_max <= 7 && Ci <= 4096,
-             RWKVTTS_EINVAL, "codec conv: tile window too large");
+    int nwv = conv_waves(KT);
+    const int wplanes = wlo ? 2 : 1;  // weight planes staged per chunk
+    auto chunk_rows = [&](int tn, int nw) { return 2 * ((32 * nw + span + 15) & ~15) + wplanes * ntaps_max * tn; };
+    auto shm_of = [&](int tn, int nw) {
+      return std::max(2 * (size_t)chunk_rows(tn, nw) * 64, (size_t)nw * 32 * (tn + 4) * sizeof(float));
+    };
+    auto fits = [&](int tn, int nw) {
+      return Co % tn == 0 && shm_of(tn, nw) <= 160 * 1024 && chunk_rows(tn, nw) / 16 <= 16 * nw;
+    };
+    if (wlo && !fits(TN, nwv)) {
+      // the weight lo plane doubles the staged weights: the (tile width, waves) that fits and
+      // stages the fewest LDS rows per output element
+      int bt = 0, bw = 0;
+      double best = 0.0;
+      for (int nw : {conv_waves(KT), 4})
+        for (int tn : {96, 64, 48, 32}) {
+          if (!fits(tn, nw) || (nw != conv_waves(KT) && KT != 7)) continue;
+          const double sc = (double)(32 * nw * tn) / chunk_rows(tn, nw);
+          if (sc > best) { best = sc; bt = tn; bw = nw; }
+        }
+      RT_CHECK(bt > 0, RWKVTTS_EINVAL, "codec conv: no tile fits the LDS with weight lo planes");
+      TN = bt;
+      nwv = bw;
+    }
+    const int TM = 32 * nwv;
+    const size_t shm = shm_of(TN, nwv);
+    RT_CHECK(fits(TN, nwv) && ntaps_max <= 7 && Ci <= 4096, RWKVTTS_EINVAL, "codec conv: tile window too large");
     ConvArgs a;
-    a.xh = x.h; a.xl = x.l; a.x_bs = bs; a.Ci = Ci; a.tin_mul = tin_mul; a.w = w; a.K = K; a.Co = Co;
+    a.xh = x.h; a.xl = x.l; a.x_bs = bs; a.Ci = Ci; a.tin_mul = tin_mul; a.w = w; a.wl = wlb + (w - wb); a.K = K; a.Co = Co;
     a.mode = mode; a.dil = dil; a.pad = pad; a.s = s; a.bias = bias; a.rbias = o.rbias; a.rb_bs = o.rb_bs;
     a.gamma = o.gamma; a.res = o.res; a.act = o.act; a.y = o.y; a.yh = o.p.h; a.yl = o.p.l;
     a.y_alpha = o.alpha; a.y_bs = o.y_bs >= 0 ? o.y_bs : bs; a.ntok = d_ntok; a.zeros = zeros;
@@ -639,24 +713,15 @@ class Codec {
     }
     pbeg();
     const int nthr = 64 * nwv;
-    if (TN == 192) k_conv<192, 1><<<grid, nthr, shm, stream>>>(a);
-    else if (TN == 96 && KT == 7) k_conv<96, 7><<<grid, nthr, shm, stream>>>(a);
-    else if (TN == 96 && KT == 3) k_conv<96, 3><<<grid, nthr, shm, stream>>>(a);
-    else if (TN == 96) k_conv<96, 1><<<grid, nthr, shm, stream>>>(a);
-    else if (TN == 48) {
-      if (KT == 1) k_conv<48, 1><<<grid, nthr, shm, stream>>>(a);
-      else if (KT == 3) k_conv<48, 3><<<grid, nthr, shm, stream>>>(a);
-      else k_conv<48, 7><<<grid, nthr, shm, stream>>>(a);
+    bool launched = false;
+#define RT_CONV_LAUNCH(TN_, KT_, WLO_, NWV_)                                          \
+    if (!launched && TN == TN_ && KT == KT_ && wlo == WLO_ && nwv == NWV_) {          \
+      k_conv<TN_, KT_, WLO_, NWV_><<<grid, nthr, shm, stream>>>(a);                   \
+      launched = true;                                                                \
     }
-    else if (TN == 64) {
-      if (KT == 1) k_conv<64, 1><<<grid, nthr, shm, stream>>>(a);
-      else if (KT == 3) k_conv<64, 3><<<grid, nthr, shm, stream>>>(a);
-      else k_conv<64, 7><<<grid, nthr, shm, stream>>>(a);
-    } else {
-      if (KT == 1) k_conv<32, 1><<<grid, nthr, shm, stream>>>(a);
-      else if (KT == 3) k_conv<32, 3><<<grid, nthr, shm, stream>>>(a);
-      else k_conv<32, 7><<<grid, nthr, shm, stream>>>(a);
-    }
+    RT_CONV_KERNELS(RT_CONV_LAUNCH)
+#undef RT_CONV_LAUNCH
+    RT_CHECK(launched, RWKVTTS_EINVAL, "codec conv: no kernel for this tile shape");
     RT_HIP(hipGetLastError());
     pend(name.c_str());
     return RWKVTTS_OK;

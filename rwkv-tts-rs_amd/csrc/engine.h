@@ -46,6 +46,8 @@ struct Job {
   void* user = nullptr;
 };
 
+class Engine;
+
 // Where Engine::serve gets requests and returns results (a fixed list for generate_batch, the
 // manager's per-engine inbox for rwkvtts_manager_*). Called only from the engine's owner thread.
 class JobSource {
@@ -55,6 +57,8 @@ class JobSource {
   // source is closed. Returns false once the source is closed and drained (no job will follow).
   virtual bool next(int max, bool wait, std::vector<Job*>& out) = 0;
   virtual void finish(Job* j) = 0;  // j->res is filled
+  // called by the owner thread after every unit of work (live statistics)
+  virtual void progress(const Engine&) {}
 };
 
 struct Active;  // a request decoding in a state slot (engine.hip, Engine::serve)
@@ -87,6 +91,7 @@ class Engine {
   bool validate(const rwkvtts_request& q, std::string& why) const;
   int max_slots() const { return S_; }
   int64_t max_active = 0;  // most slots decoding at once (serve)
+  int64_t admissions_ = 0;  // requests admitted over the engine's life (test hook counter)
 
   rwkvtts_dims dims{};
   rwkvtts_stats stats{};

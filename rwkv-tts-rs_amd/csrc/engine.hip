@@ -689,7 +689,10 @@ int Engine::run_step(const StepPlan& p, bool upload) {
       // one capture at a time per process: engines owned by different threads (the manager's
       // workers) never capture / instantiate concurrently
       static std::mutex capture_mu;
-      std::lock_guard<std::mutex> cap_lock(capture_mu);
+      // RWKVTTS_CAPTURE_UNSERIALIZED: experiment switch (the round-2 manager hang)
+      static const bool unser = getenv("RWKVTTS_CAPTURE_UNSERIALIZED") != nullptr;
+      std::unique_lock<std::mutex> cap_lock(capture_mu, std::defer_lock);
+      if (!unser) cap_lock.lock();
       hipGraph_t graph;
       RT_HIP(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
       int rc = launch_forward(R, n_seg, n_lg, p.head_rows, true, p.advance);
@@ -989,6 +992,7 @@ int Engine::finish_unit(int b, bool prefill, std::vector<Active>& act, std::vect
     }
   }
   if (copied) RT_HIP(hipStreamSynchronize(stream_));
+  src.progress(*this);
   for (size_t i = 0; i < act.size();) {
     Active& a = act[i];
     const SlotCtrl& c = snap[a.slot];
@@ -1044,6 +1048,13 @@ int Engine::serve(JobSource& src) {
       set_error("request rejected: " + why);
       src.finish(j);
       return RWKVTTS_OK;
+    }
+    // test hook: RWKVTTS_TEST_FAIL_ADMIT=k fails this engine's k-th admission as a HIP error would
+    if (const char* fa = getenv("RWKVTTS_TEST_FAIL_ADMIT")) {
+      if (++admissions_ == atoi(fa)) {
+        set_error("injected admission failure (RWKVTTS_TEST_FAIL_ADMIT)");
+        return RWKVTTS_EHIP;
+      }
     }
     const int slot = free_slots.back();
     free_slots.pop_back();
@@ -1109,9 +1120,21 @@ int Engine::serve(JobSource& src) {
     if (open && !free_slots.empty()) {
       fresh.clear();
       open = src.next((int)free_slots.size(), act.empty(), fresh);
-      for (Job* j : fresh)
-        if ((rc = admit(j)) != RWKVTTS_OK) break;
-      if (rc != RWKVTTS_OK) break;
+      size_t n_admitted = 0;
+      for (; n_admitted < fresh.size(); ++n_admitted)
+        if ((rc = admit(fresh[n_admitted])) != RWKVTTS_OK) break;
+      if (rc != RWKVTTS_OK) {
+        // the failing job and every later one were taken from the source but never reached
+        // `act`: they fail with the engine (the failure fan-out below covers `act` only)
+        for (size_t i = n_admitted; i < fresh.size(); ++i) {
+          Job* j = fresh[i];
+          if (std::any_of(act.begin(), act.end(), [&](const Active& a) { return a.job == j; })) continue;
+          j->res->status = rc;
+          j->res->n_global = j->res->n_semantic = 0;
+          src.finish(j);
+        }
+        break;
+      }
     }
     if (act.empty()) {
       if (!open) break;

@@ -16,6 +16,7 @@
 // parallelism over the node; no collective is needed on this path.
 #include <string.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -25,11 +26,19 @@
 #include <mutex>
 #include <thread>
 
+#include <rccl/rccl.h>
+
 #include "engine.h"
 
 namespace rwkvtts {
 
 namespace {
+
+#define RT_OK(x)                      \
+  do {                                \
+    int _r = (x);                     \
+    if (_r != RWKVTTS_OK) return _r;  \
+  } while (0)
 
 using Clock = std::chrono::steady_clock;
 
@@ -39,6 +48,7 @@ struct MJob : Job {
   std::vector<int32_t> sem;                        // semantic token buffer
   rwkvtts_result out{};
   bool done = false;
+  bool claimed = false;  // a wait() is in progress on this ticket (a second waiter is refused)
   int engine = -1;
 };
 
@@ -58,6 +68,11 @@ class Worker : public JobSource {
     return !(closing_ && inbox_.empty());
   }
   void finish(Job* j) override;
+  // live statistics, published by the owner thread after every unit of work
+  void progress(const Engine& e) override {
+    steps = e.stats.steps + e.stats.prefill_steps;
+    max_active = e.max_active;
+  }
   void push(MJob* j) {
     {
       std::lock_guard<std::mutex> lk(mu_);
@@ -96,12 +111,14 @@ class Manager {
   int create(const rwkvtts_manager_desc& d, const void* w, size_t bytes) {
     desc_ = d;
     RT_CHECK(d.n_engines >= 1 && d.n_engines <= RWKVTTS_MAX_ENGINES, RWKVTTS_EINVAL, "manager: 1..16 engines");
+    RT_OK(broadcast_weights(d, w, bytes));
     for (int i = 0; i < d.n_engines; ++i) workers_.emplace_back(new Worker(this, i));
     for (int i = 0; i < d.n_engines; ++i) {
       rwkvtts_engine_desc ed = d.engine;
       ed.device = d.devices[i];
       Worker* wk = workers_[i].get();
-      wk->th = std::thread([wk, ed, w, bytes] { wk->run(ed, w, bytes); });
+      const void* dw = dev_blob_[rank_of_[i]];  // this engine's device's copy of the blob
+      wk->th = std::thread([wk, ed, dw, bytes] { wk->run(ed, dw, bytes); });
     }
     // engines upload their weights in parallel; create() returns once all are ready
     int rc = RWKVTTS_OK;
@@ -118,8 +135,83 @@ class Manager {
           set_error("manager: engine init failed: " + wk->init_err);
         }
     }
+    free_dev_blobs();  // every engine holds its own copy now
     collector_ = std::thread([this] { collect_loop(); });
     return rc;
+  }
+
+  // The weight blob crosses PCIe once (host -> the first device), then goes to every other
+  // distinct device by ncclBroadcast over xGMI (RCCL, one rank per device in one process:
+  // ncclCommInitAll). With a single distinct device the broadcast is a one-rank RCCL call (the
+  // same code path, a no-op transfer); engines sharing a device read that device's copy.
+  int broadcast_weights(const rwkvtts_manager_desc& d, const void* w, size_t bytes) {
+    const auto t0 = Clock::now();
+    std::vector<int> devs;
+    rank_of_.assign(d.n_engines, 0);
+    for (int i = 0; i < d.n_engines; ++i) {
+      auto it = std::find(devs.begin(), devs.end(), d.devices[i]);
+      rank_of_[i] = (int)(it - devs.begin());
+      if (it == devs.end()) devs.push_back(d.devices[i]);
+    }
+    const int n = (int)devs.size();
+    dev_blob_.assign(n, nullptr);
+    dev_of_ = devs;
+    for (int r = 0; r < n; ++r) {
+      RT_HIP(hipSetDevice(devs[r]));
+      RT_HIP(hipMalloc(&dev_blob_[r], bytes));
+    }
+    RT_HIP(hipSetDevice(devs[0]));
+    RT_HIP(hipMemcpy(dev_blob_[0], w, bytes, hipMemcpyHostToDevice));
+    std::vector<ncclComm_t> comms(n, nullptr);
+    std::vector<hipStream_t> streams(n, nullptr);
+    auto nccl_ok = [](ncclResult_t r, const char* what) {
+      if (r == ncclSuccess) return true;
+      set_error(std::string("manager: ") + what + ": " + ncclGetErrorString(r));
+      return false;
+    };
+    int rc = RWKVTTS_OK;
+    if (!nccl_ok(ncclCommInitAll(comms.data(), n, devs.data()), "ncclCommInitAll")) rc = RWKVTTS_EHIP;
+    for (int r = 0; r < n && rc == RWKVTTS_OK; ++r) {
+      if (hipSetDevice(devs[r]) != hipSuccess || hipStreamCreateWithFlags(&streams[r], hipStreamNonBlocking) != hipSuccess) {
+        set_error("manager: broadcast stream");
+        rc = RWKVTTS_EHIP;
+      }
+    }
+    if (rc == RWKVTTS_OK) {
+      bool ok = nccl_ok(ncclGroupStart(), "ncclGroupStart");
+      for (int r = 0; r < n && ok; ++r)
+        ok = nccl_ok(ncclBroadcast(dev_blob_[0], dev_blob_[r], bytes, ncclUint8, 0, comms[r], streams[r]), "ncclBroadcast");
+      ok = nccl_ok(ncclGroupEnd(), "ncclGroupEnd") && ok;
+      for (int r = 0; r < n && ok; ++r) {
+        hipSetDevice(devs[r]);
+        ok = hipStreamSynchronize(streams[r]) == hipSuccess;
+        if (!ok) set_error("manager: broadcast synchronisation");
+      }
+      if (!ok) rc = RWKVTTS_EHIP;
+    }
+    for (int r = 0; r < n; ++r) {
+      if (streams[r]) {
+        hipSetDevice(devs[r]);
+        hipStreamDestroy(streams[r]);
+      }
+      if (comms[r]) ncclCommDestroy(comms[r]);
+    }
+    if (rc != RWKVTTS_OK) {
+      free_dev_blobs();
+      return rc;
+    }
+    bcast_ranks_ = n;
+    bcast_ms_ = std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
+    return RWKVTTS_OK;
+  }
+
+  void free_dev_blobs() {
+    for (size_t r = 0; r < dev_blob_.size(); ++r)
+      if (dev_blob_[r]) {
+        hipSetDevice(dev_of_[r]);
+        hipFree(dev_blob_[r]);
+        dev_blob_[r] = nullptr;
+      }
   }
 
   void shutdown() {
@@ -132,7 +224,13 @@ class Manager {
     for (auto& wk : workers_) wk->close();
     for (auto& wk : workers_)
       if (wk->th.joinable()) wk->th.join();
-    std::lock_guard<std::mutex> lk(t_mu_);
+    // every job has completed (the workers drain their inboxes); wake any waiter still blocked
+    // and free the jobs only once no thread is inside wait() -- the caller may destroy the
+    // manager (its mutexes and condition variables) right after this returns
+    std::unique_lock<std::mutex> lk(t_mu_);
+    t_closed_ = true;
+    t_cv_.notify_all();
+    t_cv_.wait(lk, [&] { return waiters_ == 0; });
     for (auto& kv : jobs_) delete kv.second;
     jobs_.clear();
   }
@@ -177,22 +275,36 @@ class Manager {
 
   int wait(uint64_t ticket, int timeout_ms, rwkvtts_result* out) {
     std::unique_lock<std::mutex> lk(t_mu_);
+    RT_CHECK(!t_closed_, RWKVTTS_ECLOSED, "manager_wait: manager is shutting down");
     auto it = jobs_.find(ticket);
     RT_CHECK(it != jobs_.end(), RWKVTTS_EINVAL, "manager_wait: unknown ticket");
     MJob* j = it->second;
-    auto ready = [&] { return j->done; };
-    if (timeout_ms < 0) {
+    RT_CHECK(!j->claimed, RWKVTTS_EINVAL, "manager_wait: another thread is already waiting on this ticket");
+    j->claimed = true;
+    ++waiters_;
+    auto ready = [&] { return j->done || t_closed_; };
+    bool got = true;
+    if (timeout_ms < 0)
       t_cv_.wait(lk, ready);
-    } else if (!t_cv_.wait_for(lk, std::chrono::milliseconds(timeout_ms), ready)) {
-      return RWKVTTS_EBUSY;
+    else
+      got = t_cv_.wait_for(lk, std::chrono::milliseconds(timeout_ms), ready);
+    int rc = RWKVTTS_OK;
+    if (!got) {
+      j->claimed = false;  // may be waited on again
+      rc = RWKVTTS_EBUSY;
+    } else if (!j->done) {  // shutdown woke us before the job completed
+      rc = RWKVTTS_ECLOSED;
+      set_error("manager_wait: manager shut down");
+    } else {
+      int32_t* sem = out->semantic_tokens;
+      *out = j->out;
+      out->semantic_tokens = sem;
+      if (sem && j->out.n_semantic > 0) memcpy(sem, j->sem.data(), sizeof(int32_t) * j->out.n_semantic);
+      jobs_.erase(it);
+      delete j;
     }
-    int32_t* sem = out->semantic_tokens;
-    *out = j->out;
-    out->semantic_tokens = sem;
-    if (sem && j->out.n_semantic > 0) memcpy(sem, j->sem.data(), sizeof(int32_t) * j->out.n_semantic);
-    jobs_.erase(it);
-    delete j;
-    return RWKVTTS_OK;
+    if (--waiters_ == 0 && t_closed_) t_cv_.notify_all();  // shutdown waits for the last waiter
+    return rc;
   }
 
   void complete(MJob* j, int engine) {
@@ -213,6 +325,9 @@ class Manager {
       s->completed = completed_;
     }
     s->batches = batches_.load();
+    s->bcast_ranks = bcast_ranks_;
+    s->bcast_rccl = bcast_ranks_ > 0 ? 1 : 0;
+    s->bcast_ms = bcast_ms_;
     for (size_t i = 0; i < workers_.size(); ++i) {
       s->served[i] = workers_[i]->served.load();
       s->max_active[i] = workers_[i]->max_active.load();
@@ -291,6 +406,11 @@ class Manager {
   }
 
   rwkvtts_manager_desc desc_{};
+  std::vector<void*> dev_blob_;  // per distinct device: the broadcast weight blob (freed after init)
+  std::vector<int> dev_of_;      // distinct devices, RCCL rank order
+  std::vector<int> rank_of_;     // engine -> its device's rank
+  int bcast_ranks_ = 0;
+  double bcast_ms_ = 0.0;
   std::vector<std::unique_ptr<Worker>> workers_;
   std::thread collector_;
   std::condition_variable init_cv_;
@@ -303,6 +423,8 @@ class Manager {
   std::mutex t_mu_;
   std::condition_variable t_cv_;
   std::map<uint64_t, MJob*> jobs_;
+  int waiters_ = 0;        // threads inside wait()
+  bool t_closed_ = false;  // shutdown: no new waits, blocked waiters wake
   uint64_t next_ticket_ = 0;
   int64_t submitted_ = 0, completed_ = 0;
   std::atomic<int64_t> batches_{0};
@@ -315,7 +437,7 @@ void Worker::finish(Job* j) {
 }
 
 void Worker::run(rwkvtts_engine_desc desc, const void* w, size_t bytes) {
-  int rc = eng.init(desc, w, bytes, 0);
+  int rc = eng.init(desc, w, bytes, 1);  // w: the broadcast copy on this engine's device
   {
     std::lock_guard<std::mutex> lk(m_->init_mu_);
     init_rc = rc;
@@ -325,8 +447,7 @@ void Worker::run(rwkvtts_engine_desc desc, const void* w, size_t bytes) {
   if (rc != RWKVTTS_OK) return;
   while (true) {
     rc = eng.serve(*this);
-    steps = eng.stats.steps + eng.stats.prefill_steps;
-    max_active = eng.max_active;
+    progress(eng);
     if (rc != RWKVTTS_OK) {
       dead = true;  // an engine failure fails its in-flight jobs (serve) and everything queued here
       std::vector<Job*> rest;

@@ -47,6 +47,16 @@ def synth_codec_blob(d: dict, seed: int = 20251205) -> np.ndarray:
     return out
 
 
+def synth_codec_blob_f32(d: dict, seed: int = 20251205, rel: float = 2.0 ** -12) -> np.ndarray:
+    """synth_codec_blob with every weight perturbed by a relative 2^-12 (seeded): f32 values that
+    bf16 cannot hold, as a real fp32 checkpoint's (the reference runs BiCodec in fp32 on ORT).
+    The 64-float header (the dims) is left alone."""
+    w = synth_codec_blob(d, seed)
+    u = np.random.default_rng(seed ^ 0x5EED).uniform(-1.0, 1.0, w.size - 64)
+    w[64:] = (w[64:].astype(np.float64) * (1.0 + rel * u)).astype(np.float32)
+    return w
+
+
 class BiCodecDetokenizer:
     """One decoder per GPU (replaces the 4-session ORT pool of src/onnx_session_pool.rs:204-279)."""
 

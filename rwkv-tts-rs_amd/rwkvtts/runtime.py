@@ -386,7 +386,14 @@ class DynamicBatchManager:
         self._h = h
         self.devices = devices
         self.tokenizer = tokenizer
-        self.last_status = []
+        # per calling thread: concurrent generate_tts callers (the server's worker threads) never
+        # see each other's status codes
+        self._tls = threading.local()
+
+    @property
+    def last_status(self):
+        """Status codes of this thread's last wait / generate_tts_batch call."""
+        return getattr(self._tls, "last_status", [])
 
     def close(self):
         if getattr(self, "_h", None):
@@ -414,17 +421,22 @@ class DynamicBatchManager:
 
     def wait(self, ticket: int, timeout_ms: int = -1):
         """(global, semantic) or None if not ready within timeout_ms; ([], []) for a failed request."""
+        out, status = self.wait_status(ticket, timeout_ms)
+        self._tls.last_status = [] if status is None else [status]
+        return out
+
+    def wait_status(self, ticket: int, timeout_ms: int = -1):
+        """((global, semantic), status code); (None, None) if not ready within timeout_ms."""
         r = _ffi.Result()
         sb = np.zeros(_ffi.SEMANTIC_LIMIT, dtype=np.int32)
         r.semantic_tokens = sb.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
         rc = lib().rwkvtts_manager_wait(self._h, ctypes.c_uint64(ticket), timeout_ms, ctypes.byref(r))
         if rc == _ffi.EBUSY:
-            return None
+            return None, None
         check(rc, "manager_wait")
         res = (_ffi.Result * 1)(r)
         out, status = _unpack_results(res, [sb])
-        self.last_status = status
-        return out[0]
+        return out[0], status[0]
 
     def generate_tts(self, text, property_tokens, ref_global_tokens=None, ref_semantic_tokens=None,
                      voice_id=None, args: Optional[SamplerArgs] = None):
@@ -436,9 +448,10 @@ class DynamicBatchManager:
         tickets = [self.submit(r) for r in requests]
         out, status = [], []
         for t in tickets:
-            out.append(self.wait(t))
-            status.extend(self.last_status)
-        self.last_status = status
+            o, st = self.wait_status(t)
+            out.append(o)
+            status.append(st)
+        self._tls.last_status = status
         return out
 
     def stats(self):
@@ -446,4 +459,5 @@ class DynamicBatchManager:
         check(lib().rwkvtts_manager_get_stats(self._h, ctypes.byref(s)), "manager_get_stats")
         n = len(self.devices)
         return {"submitted": s.submitted, "completed": s.completed, "batches": s.batches,
-                "served": list(s.served[:n]), "max_active": list(s.max_active[:n]), "steps": list(s.steps[:n])}
+                "served": list(s.served[:n]), "max_active": list(s.max_active[:n]), "steps": list(s.steps[:n]),
+                "bcast_ranks": s.bcast_ranks, "bcast_rccl": s.bcast_rccl, "bcast_ms": s.bcast_ms}

@@ -19,3 +19,21 @@ def oracle_mod():
     import oracle
     oracle.lib()
     return oracle
+
+
+def pytest_sessionstart(session):
+    """Start a multiprocessing fork server while this process has not touched a GPU: the
+    multi-process GPU tests (tests/test_gpu_dist_gloo.py) fork their ranks from it, so no rank is
+    ever exec'ed from a process that has initialised HIP."""
+    import multiprocessing as mp
+    from multiprocessing import forkserver
+    try:
+        mp.get_context("forkserver")
+        forkserver.ensure_running()
+    except Exception:  # pragma: no cover - the GPU test then reports the failure itself
+        pass
+
+
+def forkserver_context():
+    import multiprocessing as mp
+    return mp.get_context("forkserver")

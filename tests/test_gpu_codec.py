@@ -91,3 +91,73 @@ def test_full_dims_batch_of_32_vs_oracle(oracle_mod):
             _check(pcm, oracle_mod.codec_decode(cd, w, s, g, threads=16))
     finally:
         c.close()
+
+
+def _decoder(w, d, wlo=None):
+    """A decoder with the conv path forced (RWKVTTS_CODEC_WLO, read at creation) or automatic."""
+    old = os.environ.pop("RWKVTTS_CODEC_WLO", None)
+    if wlo is not None:
+        os.environ["RWKVTTS_CODEC_WLO"] = "1" if wlo else "0"
+    try:
+        return codec.BiCodecDetokenizer(w, d)
+    finally:
+        os.environ.pop("RWKVTTS_CODEC_WLO", None)
+        if old is not None:
+            os.environ["RWKVTTS_CODEC_WLO"] = old
+
+
+def test_weight_lo_path_bit_identical_on_bf16_weights():
+    """The three-product (weight hi + lo) kernels on bf16-exact weights add exact zeros: PCM is
+    bitwise the two-product path's, at every stage's tile choice (tiny and full dims)."""
+    rs = np.random.default_rng(77)
+    for d, T in ((codec.CODEC_DIMS_TINY, 37), (codec.CODEC_DIMS_FULL, 6)):
+        w = codec.synth_codec_blob(d, seed=3)
+        items = [(rs.integers(0, 4096, 32), rs.integers(0, 8192, T - i)) for i in range(3)]
+        a, b = _decoder(w, d, False), _decoder(w, d, True)
+        try:
+            for x, y in zip(a.decode_audio_batch(items), b.decode_audio_batch(items)):
+                assert np.array_equal(x, y)
+        finally:
+            a.close()
+            b.close()
+
+
+def test_full_dims_f32_weights_vs_oracle(oracle_mod):
+    """f32 weights that bf16 cannot hold (a real fp32 checkpoint's; synth + 2^-12 relative
+    perturbation): the decoder picks the weight hi + lo path automatically and matches the f32
+    oracle at the same PCM tolerance as bf16-exact weights. The forced bf16-weight path's error
+    on the same input is reported (test output) as the bound the hi + lo split removes; the
+    full-batch vocoder time of both paths is reported too."""
+    import time
+    d = codec.CODEC_DIMS_FULL
+    w = codec.synth_codec_blob_f32(d, seed=21)
+    r = json.load(open(os.path.join(HERE, "golden", "raf_voice_05d8f5ed.json")))
+    g, sem = r["global_tokens"], r["semantic_tokens"][:24]
+    ref = oracle_mod.codec_decode(codec.make_codec_dims(d), w, sem, g, threads=16)
+    c, cb = _decoder(w, d), _decoder(w, d, False)
+    try:
+        got = c.decode_audio(g, sem)
+        _check(got, ref)
+        lo = cb.decode_audio(g, sem)
+        e_lo = (float(np.abs(lo - ref).max()), float(np.linalg.norm(lo - ref) / np.linalg.norm(ref)))
+        e_hi = (float(np.abs(got - ref).max()), float(np.linalg.norm(got - ref) / np.linalg.norm(ref)))
+        # the bench's launch shape: 32 x 512 frames
+        rs = np.random.default_rng(1)
+        items = [(rs.integers(0, 4096, 32), rs.integers(0, 8192, 512)) for _ in range(32)]
+        ms = []
+        for dec in (c, cb):
+            dec.decode_audio_batch(items)
+            t0 = time.perf_counter()
+            dec.decode_audio_batch(items)
+            ms.append(1e3 * (time.perf_counter() - t0))
+        print(f"f32 weights: hi+lo path max|err| {e_hi[0]:.2e} rel-L2 {e_hi[1]:.2e}; bf16-weight path "
+              f"max|err| {e_lo[0]:.2e} rel-L2 {e_lo[1]:.2e}; 32 x 512 frames: {ms[0]:.1f} ms hi+lo, {ms[1]:.1f} ms bf16")
+        d_rep = os.environ.get("RWKVTTS_REPORT_DIR")
+        if d_rep:
+            os.makedirs(d_rep, exist_ok=True)
+            json.dump({"hi_lo": {"max_abs": e_hi[0], "rel_l2": e_hi[1], "batch_ms": ms[0]},
+                       "bf16_weights": {"max_abs": e_lo[0], "rel_l2": e_lo[1], "batch_ms": ms[1]}},
+                      open(os.path.join(d_rep, "codec_f32_weights.json"), "w"), indent=1)
+    finally:
+        c.close()
+        cb.close()
