@@ -60,6 +60,7 @@ struct AdvanceArgs {
   int32_t* sem_out;      // [S][2048]
   int n_rows;
   unsigned long long* tl;  // debug timeline slot (null in production)
+  int cert;              // set by launch_advance: 1 certified fast path allowed (sample_cert)
 };
 
 size_t wide_scratch_bytes(int n);

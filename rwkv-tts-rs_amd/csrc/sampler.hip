@@ -934,12 +934,126 @@ __device__ __attribute__((always_inline)) int sample_fast(const SampleSmem& sm, 
   return sm.ired[5];
 }
 
+// ---------------------------------------------------------------------------------------
+// Certified fast path: the token WITHOUT the exact sequential softmax sum.
+//
+// The exact emulation of the sequential f32 sum S (exact_seq_sum) is the serial part of the
+// sampler. But the sampled index depends on S only through comparisons -- top-k membership,
+// the top-p cut, and the draw r against the index-order cumulative -- and S lies within a
+// rigorous interval around the real sum E = sum e_i (computed here in f64, to ~n 2^-53):
+// recursive f32 summation of n non-negative terms errs by at most (n - 1) 2^-24 E (1 + O(n u)),
+// widened here to n 2^-23 E. Every p_i = RN(e_i / S) then lies in [e_i / S_hi (1 - 2^-24),
+// e_i / S_lo (1 + 2^-24)] and every sequential f32 cumulative of j + 1 such terms within
+// (1 -+ (j + 1) 2^-23) of the exact sums of those bounds. When, over that whole interval,
+// (a) the k-th and (k+1)-th largest e (by e desc, index asc) cannot round to equal p (ratio >= 1 +
+//     2^-22, p normal), so the top-k set is the one ranked on e,
+// (b) the top-p cumulative over the k survivors stays below top_p (no cut: rwkv_sampler.rs:108-153
+//     then changes nothing), and
+// (c) r is not inside the uncertainty band of the cumulative it is compared with,
+// the result equals the exact algorithm's for EVERY S in the interval, hence for the exact S;
+// otherwise the caller runs the exact sum. Returns the index, or -1 (not certified).
+// sm.keys[0, nc): candidates (e bits << 32 | index); E: f64 sum of e over the row; r: the draw.
+template <int NT>
+__device__ int sample_cert(const SampleSmem& sm, int n, int nc, double E, float r, float top_p, int top_k) {
+  const int tid = threadIdx.x;
+  uint64_t* srt = sm.keys + 2048;  // candidates ranked by (e desc, index asc)
+  uint64_t* idx_o = sm.keys + 3072;  // survivors in index order (e bits << 32 | index)
+  static_assert(kSampleMaxSorted >= 3072 + kFastK, "certified-path key regions");
+  for (int c = tid; c < nc; c += NT) {
+    const uint64_t kc = sm.keys[c];
+    const uint64_t qc = (kc & 0xFFFFFFFF00000000ull) | (uint64_t)(0xFFFFFFFFu - (uint32_t)kc);
+    int rank = 0;
+    for (int j = 0; j < nc; ++j) {
+      const uint64_t kj = sm.keys[j];
+      rank += ((kj & 0xFFFFFFFF00000000ull) | (uint64_t)(0xFFFFFFFFu - (uint32_t)kj)) > qc ? 1 : 0;
+    }
+    srt[rank] = qc;
+  }
+  __syncthreads();
+  // survivors (ranks < k) into index order
+  for (int t = tid; t < top_k; t += NT) {
+    const uint64_t kt = srt[t];
+    const uint32_t it = 0xFFFFFFFFu - (uint32_t)kt;
+    int ri = 0;
+    for (int j = 0; j < top_k; ++j) ri += (0xFFFFFFFFu - (uint32_t)srt[j]) < it ? 1 : 0;
+    idx_o[ri] = (kt & 0xFFFFFFFF00000000ull) | it;
+  }
+  __syncthreads();
+  int ret = -1;
+  if (tid < 64) {
+    const double eps = (double)n * 0x1p-23 + 0x1p-36;  // recursive f32 summation (2x) + the f64 sum's own error
+    const double s_lo = E * (1.0 - eps), s_hi = E * (1.0 + eps);
+    const double u = 0x1p-24, ua = 0x1p-23;
+    bool ok = E > 0.0 && s_lo > 0.0 && E < 3.0e38;
+    // (a) the top-k boundary
+    const float ek = __builtin_bit_cast(float, (uint32_t)(srt[top_k - 1] >> 32));
+    if (ok && nc > top_k) {
+      const float eb = __builtin_bit_cast(float, (uint32_t)(srt[top_k] >> 32));
+      ok = (double)ek >= (double)eb * (1.0 + 0x1p-22);
+    }
+    // (nc == k: every non-candidate has e < L (1 - 2^-19) <= e_k (1 - 2^-19), see sample_fast_ok)
+    ok = ok && (double)ek / s_hi >= 0x1p-120;
+    // (b) no top-p cut: the whole survivor mass stays below top_p
+    double tot_hi = 0.0;
+    for (int q0 = 0; q0 < top_k; q0 += 64) {
+      const double e = q0 + tid < top_k ? (double)__builtin_bit_cast(float, (uint32_t)(idx_o[q0 + tid] >> 32)) : 0.0;
+      double v = e;
+      for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+      tot_hi += v;
+    }
+    tot_hi = tot_hi / s_lo * (1.0 + u) * (1.0 + (double)top_k * ua);
+    if (top_p < 1.0f) ok = ok && tot_hi < (double)top_p;
+    // (c) the draw against the index-order cumulative
+    if (ok) {
+      if (r <= 0.0f) {
+        ret = 0;  // cum at index 0 is >= 0 >= r
+      } else {
+        double plo = 0.0, phi = 0.0, hi_prev = 0.0;
+        bool amb = false;
+        for (int q0 = 0; q0 < top_k && ret < 0 && !amb; q0 += 64) {
+          const bool in = q0 + tid < top_k;
+          const uint64_t kv = in ? idx_o[q0 + tid] : 0ull;
+          const double e = in ? (double)__builtin_bit_cast(float, (uint32_t)(kv >> 32)) : 0.0;
+          // inclusive prefix sums of the p bounds (lane order = index order)
+          double a = e / s_hi * (1.0 - u), b = e / s_lo * (1.0 + u);
+          for (int o = 1; o < 64; o <<= 1) {
+            const double ta = __shfl_up(a, o), tb = __shfl_up(b, o);
+            if (tid >= o) { a += ta; b += tb; }
+          }
+          const int j = q0 + tid;  // survivors summed so far: j + 1
+          const double lo = (plo + a) * (1.0 - (double)(j + 1) * ua);
+          const double hi = (phi + b) * (1.0 + (double)(j + 1) * ua);
+          const uint64_t le = __ballot(in && (double)r <= lo);
+          const uint64_t hm = __ballot(in && (double)r <= hi);  // possibly at or before
+          if (le) {
+            const int f = __builtin_ctzll(le);
+            // no earlier survivor may catch r: the first possible one is f itself
+            const int fh = __builtin_ctzll(hm);
+            if (fh == f && (f > 0 || hi_prev < (double)r)) ret = (int)(uint32_t)__shfl(kv, f);
+            else amb = true;
+          } else if (hm) {
+            amb = true;
+          }
+          plo = __shfl(plo + a, 63);
+          phi = __shfl(phi + b, 63);
+          hi_prev = phi * (1.0 + (double)min(q0 + 64, top_k) * ua);
+        }
+        if (ret < 0 && !amb) ret = (int)(uint32_t)idx_o[top_k - 1];  // past every survivor: highest index
+        if (amb) ret = -1;
+      }
+    }
+    if (tid == 0) sm.ired[7] = ret;
+  }
+  __syncthreads();
+  return sm.ired[7];
+}
+
 // The sampler. p holds the (masked) logits on entry. Returns the index in every thread.
 // status: 0 ok, RWKVTTS_EUNSUPPORTED for the documented limitation.
 template <int NT>
 __device__ __attribute__((always_inline)) int sample_block(const SampleSmem& sm, int n, float temperature, float top_p,
                             int top_k, const uint32_t* key, uint64_t draw, bool fixed42,
-                            float* dbg, int* status, uint64_t* stamps = nullptr) {
+                            float* dbg, int* status, uint64_t* stamps = nullptr, bool cert = true) {
   const int tid = threadIdx.x;
   *status = 0;
   if (n == 0) return 0;
@@ -1027,7 +1141,30 @@ __device__ __attribute__((always_inline)) int sample_block(const SampleSmem& sm,
     collect();
     if (tid == NT - 64) sm.fred[21] = draw_r(key, draw, fixed42);
   };
-  const float sum = exact_seq_sum<NT>(sm, n, stamps, other);
+  float sum;
+  if (want_fast && !dbg && cert && n <= kSampleMaxN) {
+    // certified path (sample_cert): wave 0 takes the real sum in f64 while the others collect
+    // the candidates and draw; the exact sequential sum runs only when the decision is not
+    // certified
+    if (tid < 64) {
+      double e = 0.0;
+      for (int i = tid; i < n; i += 64) e += (double)sm.p[i];
+      for (int o = 32; o >= 1; o >>= 1) e += __shfl_xor(e, o);
+      if (tid == 0) sm.dscan[12] = e;
+    } else {
+      other();
+    }
+    __syncthreads();
+    const int nc = sm.ired[31];
+    const float L = sm.fred[20];
+    if (L > 0.0f && nc >= top_k && nc <= kFastCap) {
+      const int ret = sample_cert<NT>(sm, n, nc, sm.dscan[12], sm.fred[21], top_p, top_k);
+      if (ret >= 0) return ret;
+    }
+    sum = exact_seq_sum<NT>(sm, n, stamps);
+  } else {
+    sum = exact_seq_sum<NT>(sm, n, stamps, other);
+  }
   STAMP(3);
   if (want_fast) {
     const int nc = sm.ired[31];
@@ -1429,7 +1566,7 @@ __device__ __attribute__((always_inline)) void advance_body(const AdvanceArgs& a
     __syncthreads();
     int status;
     const int id = sample_block<NT>(sm, 4096, 1.0f, 0.95f, c->top_k_g, c->gkey, c->gdraw, false,
-                                nullptr, &status);
+                                nullptr, &status, nullptr, a.cert != 0);
     if (threadIdx.x == 0) {
       c->gdraw += 1;
       c->global_out[c->n_global++] = id;
@@ -1447,7 +1584,8 @@ __device__ __attribute__((always_inline)) void advance_body(const AdvanceArgs& a
   if (threadIdx.x == 0 && eos_masked) sm.p[RWKVTTS_EOS_TOKEN] = -__builtin_inff();
   __syncthreads();
   int status;
-  int id = sample_block<NT>(sm, NS, 1.0f, 0.95f, c->top_k_s, c->skey, c->sdraw, false, nullptr, &status);
+  int id = sample_block<NT>(sm, NS, 1.0f, 0.95f, c->top_k_s, c->skey, c->sdraw, false, nullptr, &status, nullptr,
+                            a.cert != 0);
   uint64_t used = 1;
   bool stop = false;
   if (id == RWKVTTS_EOS_TOKEN) {
@@ -1465,7 +1603,7 @@ __device__ __attribute__((always_inline)) void advance_body(const AdvanceArgs& a
         if (threadIdx.x == 0) sm.p[RWKVTTS_EOS_TOKEN] = -__builtin_inff();
         __syncthreads();
         id = sample_block<NT>(sm, NS, 1.0f, 0.95f, c->top_k_s, c->skey, c->sdraw + 1, false, nullptr,
-                          &status);
+                          &status, nullptr, a.cert != 0);
         used = 2;
       }
     }
@@ -1494,7 +1632,11 @@ __global__ __launch_bounds__(kSampleThreads) void k_advance(AdvanceArgs a) {
   tl_end(a.tl);
 }
 
-int launch_advance(const AdvanceArgs& a, hipStream_t st) {
+int launch_advance(const AdvanceArgs& a0, hipStream_t st) {
+  AdvanceArgs a = a0;
+  // RWKVTTS_SAMPLER_EXACT=1: always walk the exact sequential sum (A/B switch for sample_cert)
+  static const bool exact = getenv("RWKVTTS_SAMPLER_EXACT") != nullptr;
+  a.cert = exact ? 0 : 1;
   RT_LAUNCH(k_advance, dim3(a.n_rows), dim3(kSampleThreads), smem_bytes<kSampleThreads>(RWKVTTS_EOS_TOKEN + 1),
                      st, a);
   return a.n_rows;

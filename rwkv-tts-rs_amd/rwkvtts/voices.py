@@ -13,6 +13,7 @@ import datetime as _dt
 import hashlib
 import json
 import os
+import re
 import threading
 import uuid
 from dataclasses import dataclass, field
@@ -132,6 +133,9 @@ class VoiceFeatureManager:
         os.makedirs(os.path.join(raf_dir, "temp", "upload_temp_files"), exist_ok=True)
         self._cache: Dict[str, VoiceFeature] = {}
         self._lock = threading.Lock()
+        # serialises every metadata read-modify-write and RAF file write (concurrent extract /
+        # delete / rename must not lose entries)
+        self._io_lock = threading.RLock()
         self.stats = CacheStats()
 
     @classmethod
@@ -156,7 +160,14 @@ class VoiceFeatureManager:
         now = now or _dt.datetime.now(_dt.timezone.utc)
         return f"voice_{now.strftime('%Y%m%d_%H%M%S')}_{str(uuid.uuid4())[:8]}"
 
+    # Deliberate deviation from the reference (voice_feature_manager.rs:318 joins the id as given):
+    # the id comes from unauthenticated request bodies, so anything that is not a plain file stem
+    # ("../x", "/abs/x", "a/b") is refused instead of reading or deleting outside raf_dir.
+    _ID_RE = re.compile(r"[A-Za-z0-9_\-]{1,128}")
+
     def _path(self, voice_id: str) -> str:
+        if not isinstance(voice_id, str) or not self._ID_RE.fullmatch(voice_id):
+            raise ValueError(f"invalid voice id: {voice_id!r}")
         return os.path.join(self.raf_dir, f"{voice_id}.raf.json")
 
     def save_voice_feature(self, name: str, prompt_text: str, global_tokens, semantic_tokens,
@@ -168,11 +179,12 @@ class VoiceFeatureManager:
         vf.checksum = vf.compute_checksum()
         data = vf.serialise()
         path = self._path(vf.id)
-        os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
-        with open(path, "wb") as f:
-            f.write(data)
-        self._edit_metadata(lambda vs: vs + [VoiceMetadata(vf.id, name, prompt_text, vf.created_at, path,
-                                                           len(data), vf.checksum)])
+        with self._io_lock:
+            os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+            with open(path, "wb") as f:
+                f.write(data)
+            self._edit_metadata(lambda vs: vs + [VoiceMetadata(vf.id, name, prompt_text, vf.created_at, path,
+                                                               len(data), vf.checksum)])
         with self._lock:
             self._cache[vf.id] = vf
         return vf.id
@@ -212,18 +224,20 @@ class VoiceFeatureManager:
         return [VoiceMetadata(**{k: v[k] for k in _META_FIELDS}) for v in d["voices"]]
 
     def _edit_metadata(self, fn):
-        voices = fn(self.list_voices())
-        text = _pretty({"voices": [{k: getattr(v, k) for k in _META_FIELDS} for v in voices]})
-        os.makedirs(os.path.dirname(self.metadata_file) or ".", exist_ok=True)
-        with open(self.metadata_file, "w", encoding="utf-8") as f:
-            f.write(text)
+        with self._io_lock:
+            voices = fn(self.list_voices())
+            text = _pretty({"voices": [{k: getattr(v, k) for k in _META_FIELDS} for v in voices]})
+            os.makedirs(os.path.dirname(self.metadata_file) or ".", exist_ok=True)
+            with open(self.metadata_file, "w", encoding="utf-8") as f:
+                f.write(text)
 
     def delete_voice(self, voice_id: str) -> None:
         path = self._path(voice_id)
-        if os.path.exists(path):
-            os.remove(path)
-        if os.path.exists(self.metadata_file):
-            self._edit_metadata(lambda vs: [v for v in vs if v.id != voice_id])
+        with self._io_lock:
+            if os.path.exists(path):
+                os.remove(path)
+            if os.path.exists(self.metadata_file):
+                self._edit_metadata(lambda vs: [v for v in vs if v.id != voice_id])
         with self._lock:
             self._cache.pop(voice_id, None)
 
@@ -231,17 +245,18 @@ class VoiceFeatureManager:
         vf = self.load_voice_feature(voice_id)
         vf = VoiceFeature(**{**vf.__dict__, "name": new_name})
         vf.checksum = vf.compute_checksum()
-        with open(self._path(voice_id), "wb") as f:
-            f.write(vf.serialise())
-        if not os.path.exists(self.metadata_file):
-            raise FileNotFoundError("元数据文件不存在")
+        with self._io_lock:
+            with open(self._path(voice_id), "wb") as f:
+                f.write(vf.serialise())
+            if not os.path.exists(self.metadata_file):
+                raise FileNotFoundError("元数据文件不存在")
 
-        def upd(vs):
-            for v in vs:
-                if v.id == voice_id:
-                    v.name = new_name
-            return vs
-        self._edit_metadata(upd)
+            def upd(vs):
+                for v in vs:
+                    if v.id == voice_id:
+                        v.name = new_name
+                return vs
+            self._edit_metadata(upd)
         with self._lock:
             self._cache[voice_id] = vf
 

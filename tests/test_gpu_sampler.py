@@ -158,3 +158,27 @@ def test_softmax_sum_bit_exact(rt, oracle_mod, n):
         o_idx, o_sum, _ = oracle_mod.sample(row, 1.0, 0.95, 80, None, None, debug=True)
         assert np.float32(dbg[i, 0]).view(np.uint32) == np.float32(o_sum).view(np.uint32), (i, dbg[i, 0], o_sum)
         assert tok[i] == o_idx, i
+
+
+@pytest.mark.parametrize("k,p", [(80, 0.95), (20, 0.95), (80, 1.0), (256, 0.5), (7, 0.999)])
+def test_sampler_certified_path_sweep(rt, oracle_mod, k, p):
+    """sample_cert (the token without the exact sequential sum whenever the decision holds for
+    every S in the rigorous interval) against the oracle over many rows: near-uniform rows (the
+    benchmark's regime: certified), mid-scale and peaked rows (the draw lands inside the kept mass,
+    top-p cuts: the exact sum runs), rows whose k-th / (k+1)-th logits are 1 ulp apart or tied."""
+    rs = np.random.RandomState(k * 1000 + int(p * 100))
+    n = 8193
+    rows = []
+    for scale in (0.02, 0.2, 1.0, 3.0):
+        rows.append((rs.randn(96, n) * scale).astype(np.float32))
+    x = rs.randn(64, n).astype(np.float32)
+    for i in range(64):  # the k-th and (k+1)-th largest 1 ulp apart (i even) or equal (i odd)
+        order = np.argsort(-x[i], kind="stable")
+        a, b = order[k - 1], order[k]
+        x[i, b] = x[i, a] if i % 2 else np.nextafter(x[i, a], np.float32(-np.inf))
+    rows.append(x)
+    rows = np.concatenate(rows)
+    seeds = [5 + 31 * i for i in range(len(rows))]
+    dev = rt.sample(rows, 1.0, p, k, None, [rwkvtts.StdRng.seed_from_u64(s) for s in seeds])
+    ref = [oracle_mod.sample(rows[i], 1.0, p, k, None, oracle_mod.Rng(seeds[i])) for i in range(len(rows))]
+    assert dev.tolist() == ref

@@ -98,3 +98,33 @@ def test_voice_routes(tmp_path):
     assert SV.handle_voice_delete(b"{bad", d)[1] == {"success": False, "message": "请求格式错误"}
     assert SV.handle_voice_delete(json.dumps({"voice_id": vid}), d)[1] == {"success": True, "message": "音色删除成功"}
     assert SV.handle_voice_list(d)[1]["voices"] == []
+
+
+def test_voice_id_path_traversal_refused(tmp_path):
+    """Deliberate deviation from voice_feature_manager.rs:318: ids from request bodies that are not
+    a plain file stem never reach the filesystem (no read / delete outside raf_dir)."""
+    import pytest
+    from rwkvtts.voices import VoiceFeatureManager
+    outside = tmp_path / "victim.raf.json"
+    outside.write_text("{}")
+    m = VoiceFeatureManager(str(tmp_path / "raf"))
+    for bad in ("../victim", str(tmp_path / "victim"), "a/b", "..", "", "x\x00y"):
+        with pytest.raises(ValueError):
+            m.delete_voice(bad)
+        with pytest.raises(ValueError):
+            m.load_voice_feature(bad)
+    assert outside.exists()
+
+
+def test_concurrent_saves_keep_every_entry(tmp_path):
+    import threading
+    from rwkvtts.voices import VoiceFeatureManager
+    m = VoiceFeatureManager(str(tmp_path / "raf"))
+    ids = []
+    ths = [threading.Thread(target=lambda i=i: ids.append(m.save_voice_feature(f"v{i}", "t", [1] * 32, [2] * 4, 1.0, 16000)))
+           for i in range(12)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert sorted(v.id for v in m.list_voices()) == sorted(ids) and len(set(ids)) == 12
