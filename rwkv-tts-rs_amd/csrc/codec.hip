@@ -47,6 +47,12 @@ struct ConvArgs {
   bf16_t* yl;
   const float* y_alpha;  // Snake1d alpha applied to the planes output (nullable)
   int64_t y_bs;
+  // FUSE kernels (a whole residual unit at 96 channels: conv7 -> Snake -> conv1 -> + residual):
+  // the conv7 result (+ bias) goes through Snake(mid_alpha) into an LDS image of bf16 hi + lo
+  // planes, the pointwise conv w1 ([Co][Co]) runs on it, and the epilogue above uses bias1
+  const float* mid_alpha;
+  const bf16_t* w1;
+  const float* bias1;
   const int* ntok;     // tokens per utterance; input length = ntok * tin_mul
   const bf16_t* zeros; // >= 16 zero bytes (source of out-of-range window rows)
   // XCD-aware 1-D grid (xmap = 1): the gy column tiles of time tile x run back to back on one XCD
@@ -85,6 +91,8 @@ constexpr int conv_waves(int KT) { return KT == 7 ? 8 : 4; }
   X(32, 3, true, 4) X(48, 3, true, 4) X(64, 3, true, 4) X(96, 3, true, 4)                           \
   X(32, 7, true, 8) X(48, 7, true, 8) X(64, 7, true, 8) X(96, 7, true, 8)                           \
   X(48, 7, true, 4) X(64, 7, true, 4) X(96, 7, true, 4)
+// fused residual units (conv7 -> Snake -> conv1 in one launch, 96 channels, bf16-exact weights)
+#define RT_CONV_FUSED(X) X(96, 7, false, 8) X(96, 7, false, 4)
 
 // LDS image of a 32-channel chunk: 64-B rows of four 16-B pieces, piece p of row r stored at
 // slot p ^ ((r >> 1) & 3): the MFMA fragment reads (16 rows x 4 pieces per ds_read_b128 lane
@@ -105,9 +113,10 @@ __device__ inline void glds16(const void* g, void* l) {
 // runs this decoder in fp32 on ORT) are staged as hi + lo planes too, and every product takes a
 // third MFMA x_hi * w_lo: weights enter at ~2^-16 relative, as the activations do. With w_lo = 0
 // the third MFMA adds exact zeros, so a WLO launch on bf16-exact weights is bit-identical.
-template <int TN, int KT, bool WLO = false, int NWV = conv_waves(KT)>
+template <int TN, int KT, bool WLO = false, int NWV = conv_waves(KT), bool FUSE = false>
 __global__ __launch_bounds__(64 * NWV, NWV == 8 ? 1 : 2) void k_conv(ConvArgs a) {
   constexpr int TM = 32 * NWV, NT = TN / 16;
+  static_assert(!FUSE || (TN == 96 && !WLO), "fused residual unit: 96 channels, bf16-exact weights");
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int req = blockIdx.z;
   const int Tin = a.ntok[req] * a.tin_mul;
@@ -214,6 +223,81 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? 1 : 2) void k_conv(ConvArgs a)
       }
     }
   }
+  if constexpr (FUSE) {
+    // ---- residual unit, second half: v = conv7 + bias -> Snake(mid_alpha) -> hi + lo planes in an
+    // LDS image laid out like a chunk window (3 chunks of 32 channels, rows = the TM time rows),
+    // W1 staged beside it, the pointwise conv on the image; the epilogue below then adds bias1
+    // and the residual. Saves the intermediate planes' HBM round trip (4 B per element).
+    constexpr int LDE0 = TN + 4;
+    constexpr int NCH = TN / 32;
+    __syncthreads();  // every wave is done with the chunk buffers
+    float* sE0 = (float*)lds + wave * 32 * LDE0;
+#pragma unroll
+    for (int n = 0; n < NT; ++n) {
+      const float b = a.bias[co0 + n * 16 + li];
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sE0[(m * 16 + 4 * g + j) * LDE0 + n * 16 + li] = acc[m][n][j] + b;
+    }
+    constexpr int NIT0 = TN / 8;
+    uint2 ph[NIT0], pl[NIT0];
+#pragma unroll
+    for (int it = 0; it < NIT0; ++it) {
+      const int idx = lane + 64 * it, r = idx / (TN / 4), c4 = (idx % (TN / 4)) * 4;
+      const float4_ v = *(const float4_*)(sE0 + r * LDE0 + c4);
+      uint16_t h[4], l[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float pv = snake_fast(v[e], a.mid_alpha[co0 + c4 + e]);
+        h[e] = f32_to_bf16(pv);
+        l[e] = f32_to_bf16(pv - bf16_to_f32(h[e]));
+      }
+      ph[it] = make_uint2(h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16));
+      pl[it] = make_uint2(l[0] | ((uint32_t)l[1] << 16), l[2] | ((uint32_t)l[3] << 16));
+    }
+    __syncthreads();  // every wave has read its sE0 tile: the image may overwrite it
+    uint8_t* img = lds;                              // [NCH][2 planes][TM rows][64 B]
+    uint8_t* wimg = lds + NCH * 2 * TM * 64;         // [NCH][TN rows][64 B]
+#pragma unroll
+    for (int it = 0; it < NIT0; ++it) {
+      const int idx = lane + 64 * it, r = idx / (TN / 4), c4 = (idx % (TN / 4)) * 4;
+      const int row = wave * 32 + r, ch = c4 >> 5, piece = (c4 & 31) >> 3, half = (c4 & 7) >> 2;
+      uint8_t* base = img + ch * 2 * TM * 64 + swz(row, piece) + half * 8;
+      *(uint2*)base = ph[it];
+      *(uint2*)(base + TM * 64) = pl[it];
+    }
+    // W1 [Co][Ci = TN] chunks into the swizzled image (16-row blocks, one per wave-instruction)
+    for (int blk = wave; blk < NCH * (TN / 16); blk += NWV) {
+      const int ch = blk / (TN / 16), co = (blk % (TN / 16)) * 16 + lrow;
+      const int piece = lslot ^ ((co >> 1) & 3);
+      glds16(a.w1 + (int64_t)(co0 + co) * a.Co + ch * 32 + piece * 8, wimg + ch * TN * 64 + (blk % (TN / 16)) * 1024);
+    }
+    __syncthreads();  // the image and W1 have landed
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int n = 0; n < NT; ++n) acc[m][n] = (float4_){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+      short8 bw[NT];
+#pragma unroll
+      for (int n = 0; n < NT; ++n) bw[n] = *(const short8*)(wimg + ch * TN * 64 + swz(n * 16 + li, g));
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        const int wr = wave * 32 + m * 16 + li;
+        const short8 ah = *(const short8*)(img + ch * 2 * TM * 64 + swz(wr, g));
+        const short8 al = *(const short8*)(img + ch * 2 * TM * 64 + TM * 64 + swz(wr, g));
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(cbf16x8, ah),
+                                                              __builtin_bit_cast(cbf16x8, bw[n]), acc[m][n], 0, 0, 0);
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(cbf16x8, al),
+                                                              __builtin_bit_cast(cbf16x8, bw[n]), acc[m][n], 0, 0, 0);
+        }
+      }
+    }
+  }
   // Epilogue. (1) bias / GELU / gamma in the MFMA layout (col = lane & 15 -> co,
   // row = 4 * (lane >> 4) + j -> q), staged through this wave's LDS tile [32][TN + 4] f32;
   // (2) read back row-contiguous so each lane moves 16 B of f32 (residual, y) and 8 B per
@@ -240,7 +324,7 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? 1 : 2) void k_conv(ConvArgs a)
 #pragma unroll
   for (int n = 0; n < NT; ++n) {
     const int co = co0 + n * 16 + li;
-    const float b = a.bias[co] + (a.rbias ? a.rbias[req * a.rb_bs + co] : 0.0f);
+    const float b = (FUSE ? a.bias1 : a.bias)[co] + (a.rbias ? a.rbias[req * a.rb_bs + co] : 0.0f);
     const float gm = a.gamma ? a.gamma[co] : 1.0f;
 #pragma unroll
     for (int m = 0; m < 2; ++m)
@@ -531,6 +615,10 @@ class Codec {
     RT_HIP(hipFuncSetAttribute((const void*)k_conv<TN_, KT_, WLO_, NWV_>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     RT_CONV_KERNELS(RT_CONV_ATTR)
 #undef RT_CONV_ATTR
+#define RT_CONV_ATTR_F(TN_, KT_, WLO_, NWV_) \
+    RT_HIP(hipFuncSetAttribute((const void*)k_conv<TN_, KT_, WLO_, NWV_, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    RT_CONV_FUSED(RT_CONV_ATTR_F)
+#undef RT_CONV_ATTR_F
     RT_HIP(hipFuncSetAttribute((const void*)k_conv_out, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     // zero page: out-of-range window rows read zeros at channel offsets up to the largest Ci
     RT_HIP(hipMalloc(&zeros, 16384));
@@ -693,7 +781,7 @@ class Codec {
     const int TM = 32 * nwv;
     const size_t shm = shm_of(TN, nwv);
     RT_CHECK(fits(TN, nwv) && ntaps_max <= 7 && Ci <= 4096, RWKVTTS_EINVAL, "codec conv: tile window too large");
-    ConvArgs a;
+    ConvArgs a{};
     a.xh = x.h; a.xl = x.l; a.x_bs = bs; a.Ci = Ci; a.tin_mul = tin_mul; a.w = w; a.wl = wlb + (w - wb); a.K = K; a.Co = Co;
     a.mode = mode; a.dil = dil; a.pad = pad; a.s = s; a.bias = bias; a.rbias = o.rbias; a.rb_bs = o.rb_bs;
     a.gamma = o.gamma; a.res = o.res; a.act = o.act; a.y = o.y; a.yh = o.p.h; a.yl = o.p.l;
@@ -724,6 +812,49 @@ class Codec {
     RT_CHECK(launched, RWKVTTS_EINVAL, "codec conv: no kernel for this tile shape");
     RT_HIP(hipGetLastError());
     pend(name.c_str());
+    return RWKVTTS_OK;
+  }
+
+  // One residual unit (conv7 -> Snake -> conv1 -> + residual) as ONE launch when it fits: 96
+  // channels (one column tile covers every channel the pointwise conv needs), bf16-exact weights
+  // (the weight lo plane would not fit beside the 7-tap chunk). Returns 1 if launched, 0 if the
+  // caller must run the two convs.
+  int resunit_fused(int n, int Tmax, const std::string& name, Planes x, int64_t bs, int C, int tin_mul,
+                    const bf16_t* w7, const float* b7, int dil, const float* mid_alpha, const bf16_t* w1,
+                    const float* b1, const ConvOut& o, bool* done) {
+    *done = false;
+    const bool off = getenv("RWKVTTS_NO_RESFUSE") != nullptr;  // A/B switch (read per call: tests toggle it)
+    if (off || wlo || C != 96) return RWKVTTS_OK;
+    const int span = 6 * dil;
+    int nwv = 0;
+    for (int nw : {8, 4}) {
+      const int wr = (32 * nw + span + 15) & ~15;
+      const size_t chunk = 2 * (size_t)(2 * wr + 7 * 96) * 64;
+      const size_t fused = (size_t)3 * 2 * 32 * nw * 64 + 3 * 96 * 64;
+      const size_t epi = (size_t)nw * 32 * 100 * sizeof(float);
+      if (std::max(std::max(chunk, fused), epi) <= 160 * 1024 && (2 * wr + 7 * 96) / 16 <= 16 * nw) {
+        nwv = nw;
+        break;
+      }
+    }
+    if (!nwv) return RWKVTTS_OK;
+    const int TM = 32 * nwv, wr = (TM + span + 15) & ~15;
+    const size_t shm = std::max(std::max(2 * (size_t)(2 * wr + 7 * 96) * 64, (size_t)3 * 2 * TM * 64 + 3 * 96 * 64),
+                                (size_t)nwv * 32 * 100 * sizeof(float));
+    ConvArgs a{};
+    a.xh = x.h; a.xl = x.l; a.x_bs = bs; a.Ci = C; a.tin_mul = tin_mul; a.w = w7; a.wl = wlb + (w7 - wb); a.K = 7; a.Co = C;
+    a.mode = 0; a.dil = dil; a.pad = 3 * dil; a.s = 1; a.bias = b7; a.rbias = nullptr; a.rb_bs = 0;
+    a.gamma = nullptr; a.res = o.res; a.act = 0; a.y = o.y; a.yh = o.p.h; a.yl = o.p.l;
+    a.y_alpha = o.alpha; a.y_bs = o.y_bs >= 0 ? o.y_bs : bs; a.ntok = d_ntok; a.zeros = zeros;
+    a.mid_alpha = mid_alpha; a.w1 = w1; a.bias1 = b1;
+    a.xmap = 0;
+    dim3 grid((unsigned)((Tmax * (int64_t)tin_mul + TM - 1) / TM), 1, (unsigned)n);
+    pbeg();
+    if (nwv == 8) k_conv<96, 7, false, 8, true><<<grid, 512, shm, stream>>>(a);
+    else k_conv<96, 7, false, 4, true><<<grid, 256, shm, stream>>>(a);
+    RT_HIP(hipGetLastError());
+    pend(name.c_str());
+    *done = true;
     return RWKVTTS_OK;
   }
 
@@ -867,6 +998,22 @@ class Codec {
       C = Co;
       for (int r = 0; r < 3; ++r) {
         const int o = r * (CU_R1_A1 - CU_R0_A1);
+        {
+          ConvOut of;
+          of.y = r < 2 ? xf : nullptr;
+          of.res = xf;
+          of.p = pp[cur ^ 1];
+          of.alpha = r < 2 ? F(2, ub, CU_R0_A1 + o + (CU_R1_A1 - CU_R0_A1))
+                           : (ub + 1 < d.n_up ? F(2, ub + 1, CU_SNAKE) : F(0, 0, CD_SOUT_A));
+          bool done = false;
+          if ((rc = resunit_fused(n, Tmax, stage_name("codec_resunit", C), pp[cur], bs, C, mul, B(2, ub, CU_R0_W7 + o),
+                                  F(2, ub, CU_R0_B7 + o), dils[r], F(2, ub, CU_R0_A2 + o), B(2, ub, CU_R0_W1 + o),
+                                  F(2, ub, CU_R0_B1 + o), of, &done))) return rc;
+          if (done) {
+            cur ^= 1;
+            continue;
+          }
+        }
         ConvOut o7;
         o7.p = pp[cur ^ 1];
         o7.alpha = F(2, ub, CU_R0_A2 + o);

@@ -161,3 +161,25 @@ def test_full_dims_f32_weights_vs_oracle(oracle_mod):
     finally:
         c.close()
         cb.close()
+
+
+def test_fused_residual_unit_bit_identical():
+    """The 96-channel residual units as one launch (conv7 -> Snake -> conv1 -> + residual, the
+    intermediate planes kept in LDS) give bitwise the two-launch result: same products, same
+    per-element accumulation order (RWKVTTS_NO_RESFUSE switches the fusion off per call)."""
+    rs = np.random.default_rng(96)
+    for d, T in ((codec.CODEC_DIMS_TINY, 41), (codec.CODEC_DIMS_FULL, 7)):
+        w = codec.synth_codec_blob(d, seed=9)
+        items = [(rs.integers(0, 4096, 32), rs.integers(0, 8192, T - 2 * i)) for i in range(3)]
+        c = codec.BiCodecDetokenizer(w, d)
+        try:
+            fused = c.decode_audio_batch(items)
+            os.environ["RWKVTTS_NO_RESFUSE"] = "1"
+            try:
+                plain = c.decode_audio_batch(items)
+            finally:
+                del os.environ["RWKVTTS_NO_RESFUSE"]
+            for x, y in zip(fused, plain):
+                assert np.array_equal(x, y)
+        finally:
+            c.close()
