@@ -26,6 +26,7 @@
 #include <mutex>
 #include <thread>
 
+#include <dlfcn.h>
 #include <rccl/rccl.h>
 
 #include "engine.h"
@@ -41,6 +42,36 @@ namespace {
   } while (0)
 
 using Clock = std::chrono::steady_clock;
+
+// RCCL is opened when a manager broadcasts its weights (dlopen), not linked into the library:
+// single-engine users never load it, and tools that intercept it (profilers) only see it in
+// processes that use the manager.
+struct Rccl {
+  decltype(&ncclCommInitAll) CommInitAll = nullptr;
+  decltype(&ncclCommDestroy) CommDestroy = nullptr;
+  decltype(&ncclBroadcast) Broadcast = nullptr;
+  decltype(&ncclGroupStart) GroupStart = nullptr;
+  decltype(&ncclGroupEnd) GroupEnd = nullptr;
+  decltype(&ncclGetErrorString) GetErrorString = nullptr;
+  bool ok = false;
+};
+const Rccl& rccl() {
+  static Rccl r = [] {
+    Rccl x;
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) return x;
+    x.CommInitAll = (decltype(x.CommInitAll))dlsym(h, "ncclCommInitAll");
+    x.CommDestroy = (decltype(x.CommDestroy))dlsym(h, "ncclCommDestroy");
+    x.Broadcast = (decltype(x.Broadcast))dlsym(h, "ncclBroadcast");
+    x.GroupStart = (decltype(x.GroupStart))dlsym(h, "ncclGroupStart");
+    x.GroupEnd = (decltype(x.GroupEnd))dlsym(h, "ncclGroupEnd");
+    x.GetErrorString = (decltype(x.GetErrorString))dlsym(h, "ncclGetErrorString");
+    x.ok = x.CommInitAll && x.CommDestroy && x.Broadcast && x.GroupStart && x.GroupEnd && x.GetErrorString;
+    return x;
+  }();
+  return r;
+}
 
 struct MJob : Job {
   uint64_t ticket = 0;
@@ -164,13 +195,19 @@ class Manager {
     RT_HIP(hipMemcpy(dev_blob_[0], w, bytes, hipMemcpyHostToDevice));
     std::vector<ncclComm_t> comms(n, nullptr);
     std::vector<hipStream_t> streams(n, nullptr);
-    auto nccl_ok = [](ncclResult_t r, const char* what) {
+    const Rccl& R = rccl();
+    if (!R.ok) {
+      free_dev_blobs();
+      set_error("manager: RCCL (librccl.so.1) not available for the weight broadcast");
+      return RWKVTTS_EUNSUPPORTED;
+    }
+    auto nccl_ok = [&R](ncclResult_t r, const char* what) {
       if (r == ncclSuccess) return true;
-      set_error(std::string("manager: ") + what + ": " + ncclGetErrorString(r));
+      set_error(std::string("manager: ") + what + ": " + R.GetErrorString(r));
       return false;
     };
     int rc = RWKVTTS_OK;
-    if (!nccl_ok(ncclCommInitAll(comms.data(), n, devs.data()), "ncclCommInitAll")) rc = RWKVTTS_EHIP;
+    if (!nccl_ok(R.CommInitAll(comms.data(), n, devs.data()), "ncclCommInitAll")) rc = RWKVTTS_EHIP;
     for (int r = 0; r < n && rc == RWKVTTS_OK; ++r) {
       if (hipSetDevice(devs[r]) != hipSuccess || hipStreamCreateWithFlags(&streams[r], hipStreamNonBlocking) != hipSuccess) {
         set_error("manager: broadcast stream");
@@ -178,10 +215,10 @@ class Manager {
       }
     }
     if (rc == RWKVTTS_OK) {
-      bool ok = nccl_ok(ncclGroupStart(), "ncclGroupStart");
+      bool ok = nccl_ok(R.GroupStart(), "ncclGroupStart");
       for (int r = 0; r < n && ok; ++r)
-        ok = nccl_ok(ncclBroadcast(dev_blob_[0], dev_blob_[r], bytes, ncclUint8, 0, comms[r], streams[r]), "ncclBroadcast");
-      ok = nccl_ok(ncclGroupEnd(), "ncclGroupEnd") && ok;
+        ok = nccl_ok(R.Broadcast(dev_blob_[0], dev_blob_[r], bytes, ncclUint8, 0, comms[r], streams[r]), "ncclBroadcast");
+      ok = nccl_ok(R.GroupEnd(), "ncclGroupEnd") && ok;
       for (int r = 0; r < n && ok; ++r) {
         hipSetDevice(devs[r]);
         ok = hipStreamSynchronize(streams[r]) == hipSuccess;
@@ -194,7 +231,7 @@ class Manager {
         hipSetDevice(devs[r]);
         hipStreamDestroy(streams[r]);
       }
-      if (comms[r]) ncclCommDestroy(comms[r]);
+      if (comms[r]) R.CommDestroy(comms[r]);
     }
     if (rc != RWKVTTS_OK) {
       free_dev_blobs();
