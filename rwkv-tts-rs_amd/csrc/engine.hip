@@ -981,11 +981,19 @@ int Engine::finish_unit(int b, bool prefill, std::vector<Active>& act, std::vect
   // null-stream sync), one synchronisation, then the jobs are handed back
   const SlotCtrl* snap = h_ctrl_ + (size_t)b * S_;
   bool copied = false;
+  // RWKVTTS_RESULT_COPY_SYNC=1: experiment switch recreating the round-2 result copies
+  // (synchronous null-stream hipMemcpy per finished slot; DESIGN §3, the manager hang)
+  static const bool sync_copy = getenv("RWKVTTS_RESULT_COPY_SYNC") != nullptr;
   for (auto& a : act) {
     const SlotCtrl& c = snap[a.slot];
     if (a.prefilled < (int)a.prompt.size() || c.phase != kPhDone) continue;
     rwkvtts_result& r = *a.job->res;
     if (r.semantic_tokens && c.n_sem > 0) {
+      if (sync_copy) {
+        RT_HIP(hipMemcpy(r.semantic_tokens, d_sem_ + (int64_t)a.slot * RWKVTTS_SEMANTIC_LIMIT,
+                         sizeof(int32_t) * c.n_sem, hipMemcpyDeviceToHost));
+        continue;
+      }
       RT_HIP(hipMemcpyAsync(r.semantic_tokens, d_sem_ + (int64_t)a.slot * RWKVTTS_SEMANTIC_LIMIT,
                             sizeof(int32_t) * c.n_sem, hipMemcpyDeviceToHost, stream_));
       copied = true;

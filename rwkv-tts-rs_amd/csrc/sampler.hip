@@ -1141,11 +1141,11 @@ __device__ __attribute__((always_inline)) int sample_block(const SampleSmem& sm,
     collect();
     if (tid == NT - 64) sm.fred[21] = draw_r(key, draw, fixed42);
   };
-  float sum;
+  // certified path (sample_cert): wave 0 takes the real sum in f64 while the others collect the
+  // candidates and draw; the exact sequential sum runs only when the decision is not certified
+  // (one instance of exact_seq_sum either way: its `other` work is skipped once done)
+  bool other_done = false;
   if (want_fast && !dbg && cert && n <= kSampleMaxN) {
-    // certified path (sample_cert): wave 0 takes the real sum in f64 while the others collect
-    // the candidates and draw; the exact sequential sum runs only when the decision is not
-    // certified
     if (tid < 64) {
       double e = 0.0;
       for (int i = tid; i < n; i += 64) e += (double)sm.p[i];
@@ -1155,16 +1155,18 @@ __device__ __attribute__((always_inline)) int sample_block(const SampleSmem& sm,
       other();
     }
     __syncthreads();
+    other_done = true;
     const int nc = sm.ired[31];
     const float L = sm.fred[20];
     if (L > 0.0f && nc >= top_k && nc <= kFastCap) {
       const int ret = sample_cert<NT>(sm, n, nc, sm.dscan[12], sm.fred[21], top_p, top_k);
       if (ret >= 0) return ret;
     }
-    sum = exact_seq_sum<NT>(sm, n, stamps);
-  } else {
-    sum = exact_seq_sum<NT>(sm, n, stamps, other);
   }
+  auto other_once = [&]() {
+    if (!other_done) other();
+  };
+  const float sum = exact_seq_sum<NT>(sm, n, stamps, other_once);
   STAMP(3);
   if (want_fast) {
     const int nc = sm.ired[31];
