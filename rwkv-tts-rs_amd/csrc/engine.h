@@ -187,6 +187,8 @@ class Engine {
   uint64_t* dbg_stamps_ = nullptr;  // RWKVTTS_WKV_STAMPS=<file>: layer-5 WKV phase stamps
   std::string dbg_stamp_path_;
   int dbg_exp_ = 0;
+  uint64_t* dbg_astamps_ = nullptr;  // RWKVTTS_ADV_STAMPS=<file>: k_advance phase stamps, [rows][16]
+  std::string dbg_astamp_path_;
   uint64_t* dbg_gstamps_ = nullptr;  // RWKVTTS_GEMM_STAMPS=<file>: layer-5 rkv / ffn_value GEMM stamps
   std::string dbg_gstamp_path_;  // RWKVTTS_DEBUG_EXP: timing experiments (wrong numerics), never in production
   template <typename T>

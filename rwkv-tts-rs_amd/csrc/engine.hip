@@ -106,6 +106,10 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
     RT_OK(alloc(&d_tl_, (size_t)kTlStride * kTlMax));
     use_graphs_ = desc.use_graphs != 0;
   }
+  if (const char* ap = getenv("RWKVTTS_ADV_STAMPS")) {
+    dbg_astamp_path_ = ap;
+    RT_OK(alloc(&dbg_astamps_, 256 * 16));
+  }
   if (const char* sp = getenv("RWKVTTS_WKV_STAMPS")) {
     dbg_stamp_path_ = sp;
     RT_OK(alloc(&dbg_stamps_, 4096 * 8));
@@ -650,6 +654,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
       a.sem_out = d_sem_;
       a.n_rows = n_lg;
       a.tl = tl_next("advance");
+      a.stamps = dbg_astamps_;
       prof_begin(&ev);
       launch_advance(a, stream_);
       prof_end("sample_advance", ev);
@@ -1281,6 +1286,15 @@ int Engine::dump_stamps() {
       fprintf(f, "# steps %d: launch index, name, mean start (us from the step's first launch), mean duration (us)\n", tl_steps_);
       for (size_t i = 0; i < tl_dur_.size(); ++i)
         fprintf(f, "%zu %s %.3f %.3f\n", i, tl_names_[i].c_str(), tl_start_[i] / tl_steps_, tl_dur_[i] / tl_steps_);
+      fclose(f);
+    }
+  }
+  if (dbg_astamps_) {
+    std::vector<uint64_t> ha(256 * 16);
+    RT_HIP(hipMemcpy(ha.data(), dbg_astamps_, ha.size() * 8, hipMemcpyDeviceToHost));
+    FILE* f = fopen(dbg_astamp_path_.c_str(), "wb");
+    if (f) {
+      fwrite(ha.data(), 8, ha.size(), f);
       fclose(f);
     }
   }

@@ -61,6 +61,7 @@ struct AdvanceArgs {
   int n_rows;
   unsigned long long* tl;  // debug timeline slot (null in production)
   int cert;              // set by launch_advance: 1 certified fast path allowed (sample_cert)
+  uint64_t* stamps;      // debug: [rows][16] s_memtime phase stamps (RWKVTTS_ADV_STAMPS; null in production)
 };
 
 size_t wide_scratch_bytes(int n);

@@ -1155,11 +1155,13 @@ __device__ __attribute__((always_inline)) int sample_block(const SampleSmem& sm,
       other();
     }
     __syncthreads();
+    STAMP(10);
     other_done = true;
     const int nc = sm.ired[31];
     const float L = sm.fred[20];
     if (L > 0.0f && nc >= top_k && nc <= kFastCap) {
       const int ret = sample_cert<NT>(sm, n, nc, sm.dscan[12], sm.fred[21], top_p, top_k);
+      STAMP(11);
       if (ret >= 0) return ret;
     }
   }
@@ -1549,6 +1551,8 @@ __device__ __attribute__((always_inline)) void advance_body(const AdvanceArgs& a
   const int row = blockIdx.x;
   const int slot = a.row_slot[row];
   SlotCtrl* c = a.ctrl + slot;
+  uint64_t* stamps = a.stamps ? a.stamps + row * 16 : nullptr;
+  STAMP(0);
   const int phase = c->phase;  // uniform (read by all threads before any write)
   __syncthreads();
   if (phase == kPhDone) return;
@@ -1568,7 +1572,7 @@ __device__ __attribute__((always_inline)) void advance_body(const AdvanceArgs& a
     __syncthreads();
     int status;
     const int id = sample_block<NT>(sm, 4096, 1.0f, 0.95f, c->top_k_g, c->gkey, c->gdraw, false,
-                                nullptr, &status, nullptr, a.cert != 0);
+                                nullptr, &status, stamps, a.cert != 0);
     if (threadIdx.x == 0) {
       c->gdraw += 1;
       c->global_out[c->n_global++] = id;
@@ -1586,8 +1590,9 @@ __device__ __attribute__((always_inline)) void advance_body(const AdvanceArgs& a
   if (threadIdx.x == 0 && eos_masked) sm.p[RWKVTTS_EOS_TOKEN] = -__builtin_inff();
   __syncthreads();
   int status;
-  int id = sample_block<NT>(sm, NS, 1.0f, 0.95f, c->top_k_s, c->skey, c->sdraw, false, nullptr, &status, nullptr,
+  int id = sample_block<NT>(sm, NS, 1.0f, 0.95f, c->top_k_s, c->skey, c->sdraw, false, nullptr, &status, stamps,
                             a.cert != 0);
+  STAMP(15);
   uint64_t used = 1;
   bool stop = false;
   if (id == RWKVTTS_EOS_TOKEN) {

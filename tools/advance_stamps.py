@@ -1,0 +1,33 @@
+"""Per-phase s_memtime stamps of k_advance (the device sampler + phase controller) in the last
+decode step of a 32-request 0.4B batch (RWKVTTS_ADV_STAMPS debug hook). Usage: advance_stamps.py [S]"""
+import os
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+path = os.path.join(tempfile.gettempdir(), "adv_stamps.bin")
+os.environ["RWKVTTS_ADV_STAMPS"] = path
+sys.path.insert(0, os.path.join(ROOT, "rwkv-tts-rs_amd"))
+import numpy as np  # noqa: E402
+import rwkvtts  # noqa: E402
+from rwkvtts import weights as W  # noqa: E402
+
+S = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+rt = rwkvtts.SharedRwkvRuntime(W.synth_blob(W.DIMS_04B, seed=20251205), max_slots=32, token_chunk_size=2048,
+                               use_graphs=True)
+reqs = []
+for i in range(32):
+    rs = np.random.RandomState(i)
+    reqs.append(rwkvtts.TtsBatchRequest(text_tokens=rs.randint(12293, 77822, size=24).tolist(),
+                                        property_tokens=[77823, 77838, 77869, 77845, 77830, 77826],
+                                        args=rwkvtts.SamplerArgs(seed=i), fixed_semantic=S))
+for rep in range(2):
+    rt.generate_batch(reqs)
+    st = np.fromfile(path, dtype=np.uint64).reshape(256, 16)[:32].astype(np.int64)
+    names = {(0, 1): "load logits", (1, 2): "max + exp", (2, 10): "f64 sum | collect + draw",
+             (10, 11): "sample_cert", (11, 15): "controller tail", (0, 15): "total"}
+    print(f"rep {rep}: cycles (mean over 32 rows of the last step; s_memtime)")
+    for (a, b), nm in names.items():
+        d = st[:, b] - st[:, a]
+        print(f"  {nm:26s} mean {d.mean():8.0f}  min {d.min():8d}  max {d.max():8d}")
+rt.close()
