@@ -31,6 +31,13 @@ struct SlotCtrl {
   uint64_t gdraw;
   uint64_t sdraw;
   int32_t global_out[32];
+  // ChaCha12 keystream block cache of each stream (k_advance): 16 consecutive draws share one
+  // block, so 15 of 16 draws are a word read instead of a ChaCha12 block on the critical path.
+  // *_blk_id = block index + 1 (0: empty -- the host zero-fills a new request's block)
+  uint64_t gblk_id;
+  uint64_t sblk_id;
+  uint32_t gblk[16];
+  uint32_t sblk[16];
 };
 
 struct SampleRowArgs {

@@ -56,6 +56,46 @@ __device__ uint32_t chacha12_word(const uint32_t* key, uint64_t index) {
   return out;
 }
 
+// the whole ChaCha12 block `ctr` (words 16 ctr .. 16 ctr + 15 of the keystream)
+__device__ void chacha12_block(const uint32_t* key, uint64_t ctr, uint32_t* out) {
+  uint32_t in[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u};
+  for (int i = 0; i < 8; ++i) in[4 + i] = key[i];
+  in[12] = (uint32_t)ctr;
+  in[13] = (uint32_t)(ctr >> 32);
+  in[14] = 0;
+  in[15] = 0;
+  uint32_t x[16];
+  for (int i = 0; i < 16; ++i) x[i] = in[i];
+  for (int i = 0; i < 12; i += 2) {
+    QR(x[0], x[4], x[8], x[12]);
+    QR(x[1], x[5], x[9], x[13]);
+    QR(x[2], x[6], x[10], x[14]);
+    QR(x[3], x[7], x[11], x[15]);
+    QR(x[0], x[5], x[10], x[15]);
+    QR(x[1], x[6], x[11], x[12]);
+    QR(x[2], x[7], x[8], x[13]);
+    QR(x[3], x[4], x[9], x[14]);
+  }
+  for (int i = 0; i < 16; ++i) out[i] = x[i] + in[i];
+}
+
+// rng.gen::<f32>() draw `index` through a per-stream block cache in the control block (one
+// thread): a hit reads one word, a miss computes the block and stores it
+__device__ float draw_cached(const uint32_t* key, uint64_t index, uint32_t* blk, uint64_t* blk_id) {
+  const uint64_t b = index >> 4;
+  uint32_t w;
+  if (*blk_id == b + 1) {
+    w = blk[index & 15];
+  } else {
+    uint32_t o[16];
+    chacha12_block(key, b, o);
+    for (int i = 0; i < 16; ++i) blk[i] = o[i];
+    *blk_id = b + 1;
+    w = blk[index & 15];
+  }
+  return (float)(w >> 8) * (1.0f / 16777216.0f);
+}
+
 __device__ inline float draw_f32(const uint32_t* key, uint64_t index) {
   return (float)(chacha12_word(key, index) >> 8) * (1.0f / 16777216.0f);
 }
@@ -187,9 +227,11 @@ __device__ inline float lane_serial_add(float s, const float* p, int b, int e) {
 }
 // In-order prefix sums of one 64-block: lane i receives s + v[0] + ... + v[i] (sequential).
 __device__ inline float prefix64(float s, float v, float* total) {
+  // partly unrolled: fully unrolled, the 64 `lane == i` masks are loop invariants that the
+  // compiler hoists to the kernel entry (k_advance's preamble) and spills
   float out = 0.0f;
   const int lane = threadIdx.x & 63;
-#pragma unroll
+#pragma unroll 8
   for (int i = 0; i < 64; ++i) {
     s += readlane_f(v, i);
     out = lane == i ? s : out;
@@ -257,6 +299,37 @@ __device__ inline double readlane_d(double v, int l) {
   const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
   return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
+// inclusive prefix sum over the wave's 64 lanes (DPP row shifts, then the row totals by readlane)
+__device__ inline double wave_incl_scan_d(double x) {
+  x += dpp_shr<1>(x);
+  x += dpp_shr<2>(x);
+  x += dpp_shr<4>(x);
+  x += dpp_shr<8>(x);
+  const double r0 = readlane_d(x, 15), r1 = readlane_d(x, 31), r2 = readlane_d(x, 47);
+  const int row = (threadIdx.x & 63) >> 4;
+  return x + (row == 0 ? 0.0 : (row == 1 ? r0 : (row == 2 ? r0 + r1 : (r0 + r1) + r2)));
+}
+
+__device__ inline uint64_t readlane_u64(uint64_t v, int l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+  return ((uint64_t)hi << 32) | lo;
+}
+// rank_of(q) = #{j < m : key(j) > q} for every lane's q (wave-wide; lanes without a query pass
+// any q). The m keys are read 64 at a time into lanes and broadcast by readlane: no LDS round trip
+// per key (a per-key LDS broadcast loop is latency-bound: 13.8K cycles for the certified path's
+// ranking at a few hundred candidates). Padding keys are 0, which exceeds no q.
+template <typename KeyAt>
+__device__ inline int wave_rank_gt(uint64_t q, int m, const KeyAt& key_at) {
+  const int lane = threadIdx.x & 63;
+  int rank = 0;
+  for (int j0 = 0; j0 < m; j0 += 64) {
+    const uint64_t kl = j0 + lane < m ? key_at(j0 + lane) : 0ull;
+#pragma unroll
+    for (int j = 0; j < 64; ++j) rank += readlane_u64(kl, j) > q ? 1 : 0;
+  }
+  return rank;
+}
 __device__ inline int readlane_t(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
 __device__ inline uint32_t readlane_t(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
 __device__ inline double readlane_t(double v, int l) { return readlane_d(v, l); }
@@ -293,42 +366,51 @@ __device__ inline int block_excl_scan(int v, int* scratch, int* tot) { return bl
 
 // compact indices with p > 0 into list (index order); returns count (may exceed capacity:
 // then list is incomplete and callers fall back to a scan of p).
+// (the arrays are passed one by one: an out-of-line callee taking the SampleSmem by reference
+// makes the caller keep the struct in scratch memory)
 template <int NT>
-__device__ int compact_positive(const SampleSmem& sm, int n) {
+__device__ int compact_positive_(const float* p, int* list, int* scan, int cap, int n) {
   const int chunk = (n + NT - 1) / NT;
   const int b = min(n, (int)threadIdx.x * chunk), e = min(n, b + chunk);
   int cnt = 0;
-  for (int i = b; i < e; ++i) cnt += sm.p[i] > 0.0f;
+  for (int i = b; i < e; ++i) cnt += p[i] > 0.0f;
   int tot;
-  int off = block_excl_scan<NT>(cnt, sm.scan, &tot);
+  int off = block_excl_scan<NT>(cnt, scan, &tot);
   for (int i = b; i < e; ++i)
-    if (sm.p[i] > 0.0f) {
-      if (off < sm.cap) sm.list[off] = i;
+    if (p[i] > 0.0f) {
+      if (off < cap) list[off] = i;
       ++off;
     }
   __syncthreads();
   return tot;
 }
+template <int NT>
+__device__ inline int compact_positive(const SampleSmem& sm, int n) {
+  return compact_positive_<NT>(sm.p, sm.list, sm.scan, sm.cap, n);
+}
 
 // index-order sequential f32 sum of p by one wave (only positive entries contribute: +0 adds
 // are exact); positive values staged into lanes, added in order from registers.
-__device__ float wave_sum_positive(const SampleSmem& sm, int n, int npos) {
+__device__ float wave_sum_positive_(const float* p, const int* list, int cap, int n, int npos) {
   const int lane = threadIdx.x & 63;
   float s = 0.0f;
-  if (npos <= sm.cap) {
+  if (npos <= cap) {
     for (int q0 = 0; q0 < npos; q0 += 64) {
-      const float v = (q0 + lane < npos) ? sm.p[sm.list[q0 + lane]] : 0.0f;
+      const float v = (q0 + lane < npos) ? p[list[q0 + lane]] : 0.0f;
       const int cnt = min(64, npos - q0);
       for (int i = 0; i < cnt; ++i) s += readlane_f(v, i);
     }
   } else {
     for (int q0 = 0; q0 < n; q0 += 64) {
-      const float v = (q0 + lane < n) ? sm.p[q0 + lane] : 0.0f;
+      const float v = (q0 + lane < n) ? p[q0 + lane] : 0.0f;
       const int cnt = min(64, n - q0);
       for (int i = 0; i < cnt; ++i) s += readlane_f(v, i);
     }
   }
   return s;
+}
+__device__ inline float wave_sum_positive(const SampleSmem& sm, int n, int npos) {
+  return wave_sum_positive_(sm.p, sm.list, sm.cap, n, npos);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -954,31 +1036,39 @@ __device__ __attribute__((always_inline)) int sample_fast(const SampleSmem& sm, 
 // otherwise the caller runs the exact sum. Returns the index, or -1 (not certified).
 // sm.keys[0, nc): candidates (e bits << 32 | index); E: f64 sum of e over the row; r: the draw.
 template <int NT>
-__device__ int sample_cert(const SampleSmem& sm, int n, int nc, double E, float r, float top_p, int top_k) {
+__device__ __attribute__((always_inline)) int sample_cert(const SampleSmem& sm, int n, int nc, double E, float r, float top_p, int top_k,
+                           uint64_t* stamps = nullptr) {
   const int tid = threadIdx.x;
+  STAMP(7);
   uint64_t* srt = sm.keys + 2048;  // candidates ranked by (e desc, index asc)
   uint64_t* idx_o = sm.keys + 3072;  // survivors in index order (e bits << 32 | index)
   static_assert(kSampleMaxSorted >= 3072 + kFastK, "certified-path key regions");
-  for (int c = tid; c < nc; c += NT) {
-    const uint64_t kc = sm.keys[c];
-    const uint64_t qc = (kc & 0xFFFFFFFF00000000ull) | (uint64_t)(0xFFFFFFFFu - (uint32_t)kc);
-    int rank = 0;
-    for (int j = 0; j < nc; ++j) {
-      const uint64_t kj = sm.keys[j];
-      rank += ((kj & 0xFFFFFFFF00000000ull) | (uint64_t)(0xFFFFFFFFu - (uint32_t)kj)) > qc ? 1 : 0;
-    }
-    srt[rank] = qc;
+  auto qkey = [&](int j) {
+    const uint64_t kj = sm.keys[j];
+    return (kj & 0xFFFFFFFF00000000ull) | (uint64_t)(0xFFFFFFFFu - (uint32_t)kj);
+  };
+  for (int c0 = 0; c0 < nc; c0 += NT) {
+    if (c0 + (tid & ~63) >= nc) break;  // wave-uniform: no candidate in this wave
+    const int c = c0 + tid;
+    const uint64_t qc = c < nc ? qkey(c) : ~0ull;
+    const int rank = wave_rank_gt(qc, nc, qkey);
+    if (c < nc) srt[rank] = qc;
   }
   __syncthreads();
+  STAMP(8);
   // survivors (ranks < k) into index order
-  for (int t = tid; t < top_k; t += NT) {
-    const uint64_t kt = srt[t];
+  for (int t0 = 0; t0 < top_k; t0 += NT) {
+    if (t0 + (tid & ~63) >= top_k) break;  // wave-uniform
+    const int t = t0 + tid;
+    const uint64_t kt = t < top_k ? srt[t] : 0ull;
     const uint32_t it = 0xFFFFFFFFu - (uint32_t)kt;
-    int ri = 0;
-    for (int j = 0; j < top_k; ++j) ri += (0xFFFFFFFFu - (uint32_t)srt[j]) < it ? 1 : 0;
-    idx_o[ri] = (kt & 0xFFFFFFFF00000000ull) | it;
+    // rank by index ascending == rank by ~index descending: #{j : ~idx_j > ~idx_t}
+    auto nkey = [&](int j) { return (uint64_t)(uint32_t)srt[j]; };
+    const int ri = wave_rank_gt((uint64_t)(uint32_t)kt, top_k, nkey);
+    if (t < top_k) idx_o[ri] = (kt & 0xFFFFFFFF00000000ull) | it;
   }
   __syncthreads();
+  STAMP(9);
   int ret = -1;
   if (tid < 64) {
     const double eps = (double)n * 0x1p-23 + 0x1p-36;  // recursive f32 summation (2x) + the f64 sum's own error
@@ -997,12 +1087,11 @@ __device__ int sample_cert(const SampleSmem& sm, int n, int nc, double E, float 
     double tot_hi = 0.0;
     for (int q0 = 0; q0 < top_k; q0 += 64) {
       const double e = q0 + tid < top_k ? (double)__builtin_bit_cast(float, (uint32_t)(idx_o[q0 + tid] >> 32)) : 0.0;
-      double v = e;
-      for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-      tot_hi += v;
+      tot_hi += readlane_d(wave_incl_scan_d(e), 63);
     }
     tot_hi = tot_hi / s_lo * (1.0 + u) * (1.0 + (double)top_k * ua);
     if (top_p < 1.0f) ok = ok && tot_hi < (double)top_p;
+    STAMP(12);
     // (c) the draw against the index-order cumulative
     if (ok) {
       if (r <= 0.0f) {
@@ -1015,11 +1104,7 @@ __device__ int sample_cert(const SampleSmem& sm, int n, int nc, double E, float 
           const uint64_t kv = in ? idx_o[q0 + tid] : 0ull;
           const double e = in ? (double)__builtin_bit_cast(float, (uint32_t)(kv >> 32)) : 0.0;
           // inclusive prefix sums of the p bounds (lane order = index order)
-          double a = e / s_hi * (1.0 - u), b = e / s_lo * (1.0 + u);
-          for (int o = 1; o < 64; o <<= 1) {
-            const double ta = __shfl_up(a, o), tb = __shfl_up(b, o);
-            if (tid >= o) { a += ta; b += tb; }
-          }
+          const double a = wave_incl_scan_d(e / s_hi * (1.0 - u)), b = wave_incl_scan_d(e / s_lo * (1.0 + u));
           const int j = q0 + tid;  // survivors summed so far: j + 1
           const double lo = (plo + a) * (1.0 - (double)(j + 1) * ua);
           const double hi = (phi + b) * (1.0 + (double)(j + 1) * ua);
@@ -1029,13 +1114,13 @@ __device__ int sample_cert(const SampleSmem& sm, int n, int nc, double E, float 
             const int f = __builtin_ctzll(le);
             // no earlier survivor may catch r: the first possible one is f itself
             const int fh = __builtin_ctzll(hm);
-            if (fh == f && (f > 0 || hi_prev < (double)r)) ret = (int)(uint32_t)__shfl(kv, f);
+            if (fh == f && (f > 0 || hi_prev < (double)r)) ret = __builtin_amdgcn_readlane((int)(uint32_t)kv, f);
             else amb = true;
           } else if (hm) {
             amb = true;
           }
-          plo = __shfl(plo + a, 63);
-          phi = __shfl(phi + b, 63);
+          plo = readlane_d(plo + a, 63);
+          phi = readlane_d(phi + b, 63);
           hi_prev = phi * (1.0 + (double)min(q0 + 64, top_k) * ua);
         }
         if (ret < 0 && !amb) ret = (int)(uint32_t)idx_o[top_k - 1];  // past every survivor: highest index
@@ -1044,6 +1129,7 @@ __device__ int sample_cert(const SampleSmem& sm, int n, int nc, double E, float 
     }
     if (tid == 0) sm.ired[7] = ret;
   }
+  STAMP(13);
   __syncthreads();
   return sm.ired[7];
 }
@@ -1053,12 +1139,15 @@ __device__ int sample_cert(const SampleSmem& sm, int n, int nc, double E, float 
 template <int NT>
 __device__ __attribute__((always_inline)) int sample_block(const SampleSmem& sm, int n, float temperature, float top_p,
                             int top_k, const uint32_t* key, uint64_t draw, bool fixed42,
-                            float* dbg, int* status, uint64_t* stamps = nullptr, bool cert = true) {
+                            float* dbg, int* status, uint64_t* stamps = nullptr, bool cert = true,
+                            bool prepped = false) {
   const int tid = threadIdx.x;
   *status = 0;
   if (n == 0) return 0;
-  STAMP(1);
-  // (2) softmax: max, exp, sequential sum (exact emulation), divide
+  if (!prepped) STAMP(1);
+  // (2) softmax: max, exp, sequential sum (exact emulation), divide. prepped (advance_prep): p
+  // already holds e = exp(l - max), the candidates, L, the f64 sum and the draw are in place.
+  if (!prepped) {
   float mx = -__builtin_inff();
   if (tid < 32) sm.etab[tid] = exp2_tab(tid);  // ordered before the reads by block_max's barriers
   for (int i = tid; i < n; i += NT) mx = fmaxf(mx, sm.p[i]);
@@ -1076,12 +1165,13 @@ __device__ __attribute__((always_inline)) int sample_block(const SampleSmem& sm,
     }
     for (; i < n; i += NT) sm.p[i] = glibc_expf_t(sm.p[i] - mx, tab);
   }
+  }
   // Fast path (top-k <= kFastK, no temperature step): while wave 0 walks the exact sum, the
   // other waves collect the top-k candidates on the unnormalised e = exp(l - max), so that after
   // the sum only the candidates are divided, ranked and sampled. See sample_fast_ok below.
   static_assert(NT <= 512, "fred[8 + wave] per candidate wave");
   const bool want_fast = top_k > 0 && top_k < n && top_k <= kFastK && !(temperature != 1.0f && temperature > 0.0f);
-  if (tid == 0) {
+  if (tid == 0 && !prepped) {
     sm.ired[30] = 0;  // sub-group arrival counter of the candidate waves
     sm.ired[31] = 0;  // candidate count
     sm.fred[20] = 0.0f;
@@ -1144,8 +1234,16 @@ __device__ __attribute__((always_inline)) int sample_block(const SampleSmem& sm,
   // certified path (sample_cert): wave 0 takes the real sum in f64 while the others collect the
   // candidates and draw; the exact sequential sum runs only when the decision is not certified
   // (one instance of exact_seq_sum either way: its `other` work is skipped once done)
-  bool other_done = false;
-  if (want_fast && !dbg && cert && n <= kSampleMaxN) {
+  bool other_done = prepped;
+  if (prepped) {
+    const int nc = sm.ired[31];
+    const float L = sm.fred[20];
+    if (want_fast && !dbg && cert && n <= kSampleMaxN && L > 0.0f && nc >= top_k && nc <= kFastCap) {
+      const int ret = sample_cert<NT>(sm, n, nc, sm.dscan[12], sm.fred[21], top_p, top_k, stamps);
+      STAMP(11);
+      if (ret >= 0) return ret;
+    }
+  } else if (want_fast && !dbg && cert && n <= kSampleMaxN) {
     if (tid < 64) {
       double e = 0.0;
       for (int i = tid; i < n; i += 64) e += (double)sm.p[i];
@@ -1546,13 +1644,145 @@ __device__ inline void load_logits_row(const AdvanceArgs& a, const float* lg, fl
   for (; i < n; i += NT) p[i] = load_logit(a, lg, i);
 }
 
+// k_advance's preparation of a row for sample_block(prepped = true), with the row in registers
+// instead of LDS round trips: element i = tid + k NT of thread tid (k < PT); every partial-slab
+// load of the row is issued before the first add (each element sums its slabs in order p = 0, 1,
+// ..., as load_logit does) and the last wave makes the draw (a ChaCha12 block) while they are in
+// flight; block max; e = glibc expf(l - max) into p (the exact paths read it there); the real sum
+// E of the row in f64 from per-thread partial sums (any order: its error, <= n 2^-53 E, is inside
+// sample_cert's 2^-36 term); and, for top-k <= kFastK, the bound L and the candidates
+// e >= L (1 - 2^-19) appended straight from the registers (the collect() of sample_block with all
+// NW waves: each wave holds >= ceil(k / NW) elements >= its ceil(k / NW)-th largest thread-local
+// maximum, so >= k elements are >= L). Leaves: p = e, fred[20] = L (0: no bound), ired[31] = the
+// candidate count with the keys in keys[0, min(count, kFastCap)), fred[21] = r, dscan[12] = E.
+// The row length N is a template parameter: every i < N test but the last element's folds away
+// (with a runtime n the compiler hoisted seventeen lane masks per test into the kernel's preamble
+// and spilled them, +5 us per launch). mask_eos: the last element (EOS, semantic rows) is -inf.
+// The row's logits into registers, every partial-slab load issued before the first add (element i
+// = tid + k NT sums its slabs in order p = 0, 1, ..., as load_logit does). Issued by k_advance
+// before it reads the slot's control block. Indices past the row are clamped (never used).
+template <int NT, int PT>
+__device__ __attribute__((always_inline)) void advance_load_row(const AdvanceArgs& a, const float* lg, float* v) {
+  const int last = a.ld - 1, tid = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < PT; ++k) v[k] = lg[min(tid + k * NT, last)];
+  if (a.n_part == 2) {
+    float w[PT];
+#pragma unroll
+    for (int k = 0; k < PT; ++k) w[k] = lg[a.part_stride + min(tid + k * NT, last)];
+#pragma unroll
+    for (int k = 0; k < PT; ++k) v[k] += w[k];
+  } else {
+    for (int q = 1; q < a.n_part; ++q)
+#pragma unroll
+      for (int k = 0; k < PT; ++k) v[k] += lg[q * a.part_stride + min(tid + k * NT, last)];
+  }
+}
+
+template <int NT, int N, int PT>
+__device__ __attribute__((always_inline)) void advance_prep(const float* raw, const SampleSmem& sm, bool mask_eos,
+                                                            int top_k, const uint32_t* key, uint64_t draw,
+                                                            uint32_t* blk, uint64_t* blk_id, uint64_t* stamps) {
+  constexpr int NW = NT / 64, n = N;
+  static_assert(PT * NT >= N, "row registers");
+  const int masked = mask_eos ? N - 1 : -1;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float v[PT];
+#pragma unroll
+  for (int k = 0; k < PT; ++k) v[k] = raw[k];
+  if (tid == NT - 64) sm.fred[21] = draw_cached(key, draw, blk, blk_id);
+  if (tid < 32) sm.etab[tid] = exp2_tab(tid);
+  if (tid == 0) sm.ired[31] = 0;
+  float mx = -__builtin_inff();
+#pragma unroll
+  for (int k = 0; k < PT; ++k) {
+    const int i = tid + k * NT;
+    if (i == masked) v[k] = -__builtin_inff();
+    if (i < n) mx = fmaxf(mx, v[k]);
+  }
+  STAMP(1);
+  mx = block_max<NT>(mx, sm.fred);  // its barriers also order etab / ired[31] / fred[21]
+  STAMP(3);
+  const uint64_t* et = sm.etab;
+  auto tab = [et](int j) { return et[j]; };
+  double es = 0.0;
+  float lm = -1.0f;  // every e >= 0
+#pragma unroll
+  for (int k = 0; k < PT; ++k) {
+    const int i = tid + k * NT;
+    if (i < n) {
+      const float e = glibc_expf_t(v[k] - mx, tab);
+      v[k] = e;
+      sm.p[i] = e;
+      es += (double)e;
+      lm = fmaxf(lm, e);
+    }
+  }
+  STAMP(4);
+  es = readlane_d(wave_incl_scan_d(es), 63);
+  const bool want = top_k > 0 && top_k < n && top_k <= kFastK;
+  if (want) {
+    const int kw = (top_k + NW - 1) / NW;
+    int gt = 0, ge = 0;
+#pragma unroll 16
+    for (int j = 0; j < 64; ++j) {
+      const float o = readlane_f(lm, j);
+      gt += o > lm ? 1 : 0;
+      ge += o >= lm ? 1 : 0;
+    }
+    const uint64_t selm = __ballot(gt < kw && kw <= ge);
+    const float vw = readlane_f(lm, __builtin_ctzll(selm));
+    if (lane == 0) sm.fred[8 + wave] = vw;
+  }
+  if (lane == 0) sm.dscan[wave] = es;
+  STAMP(5);
+  __syncthreads();
+  STAMP(6);
+  float L = 0.0f;
+  if (want) {
+    L = sm.fred[8];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) L = fminf(L, sm.fred[8 + w]);
+  }
+  if (L > 0.0f) {
+    const float T = L * (1.0f - 0x1p-19f);
+#pragma unroll
+    for (int k = 0; k < PT; ++k) {
+      const int i = tid + k * NT;
+      const bool c = i < n && v[k] >= T;
+      const uint64_t bm = __ballot(c);
+      if (bm) {
+        int base = 0;
+        if (lane == 0) base = atomicAdd(&sm.ired[31], __popcll(bm));
+        base = __builtin_amdgcn_readfirstlane(base);
+        const int off = base + __popcll(bm & ((1ull << lane) - 1ull));
+        if (c && off < kFastCap) sm.keys[off] = ((uint64_t)__builtin_bit_cast(uint32_t, v[k]) << 32) | (uint32_t)i;
+      }
+    }
+  }
+  if (tid == 0) {
+    double E = sm.dscan[0];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) E += sm.dscan[w];
+    sm.dscan[12] = E;
+    sm.fred[20] = L;
+  }
+  __syncthreads();
+  STAMP(10);
+}
+
 __device__ __attribute__((always_inline)) void advance_body(const AdvanceArgs& a, char* smem) {
   constexpr int NT = kSampleThreads;
   const int row = blockIdx.x;
-  const int slot = a.row_slot[row];
-  SlotCtrl* c = a.ctrl + slot;
   uint64_t* stamps = a.stamps ? a.stamps + row * 16 : nullptr;
   STAMP(0);
+  // the row's logits are requested first: they do not depend on the control block
+  constexpr int NS = RWKVTTS_EOS_TOKEN + 1, PT = (NS + NT - 1) / NT;
+  const float* lg = a.logits + (int64_t)row * a.ld;
+  float raw[PT];
+  advance_load_row<NT, PT>(a, lg, raw);
+  const int slot = a.row_slot[row];
+  SlotCtrl* c = a.ctrl + slot;
   const int phase = c->phase;  // uniform (read by all threads before any write)
   __syncthreads();
   if (phase == kPhDone) return;
@@ -1565,14 +1795,42 @@ __device__ __attribute__((always_inline)) void advance_body(const AdvanceArgs& a
     }
     return;
   }
-  const float* lg = a.logits + (int64_t)row * a.ld;
-  if (phase == kPhGlobal) {
-    const SampleSmem sm = carve<NT>(smem, 4096);
-    load_logits_row<NT>(a, lg, sm.p, 4096);
-    __syncthreads();
-    int status;
-    const int id = sample_block<NT>(sm, 4096, 1.0f, 0.95f, c->top_k_g, c->gkey, c->gdraw, false,
-                                nullptr, &status, stamps, a.cert != 0);
+  // one prepared sampling call site for both phases (one inlined sample_block instance):
+  // global rows [0, 4096), semantic rows [0, 8192] (j > 8192 and the tags are -inf in the reference)
+  const bool glob = phase == kPhGlobal;
+  const SampleSmem sm = carve<NT>(smem, NS);
+  const bool eos_masked = !glob && (c->fixed || (c->mode == 1 && c->n_sem < c->hard_min));
+  const int n = glob ? 4096 : NS, top_k = glob ? c->top_k_g : c->top_k_s;
+  const uint32_t* key = glob ? c->gkey : c->skey;
+  const uint64_t draw = glob ? c->gdraw : c->sdraw;
+  // attempt 1 (zero-shot only): EOS drawn while the window rule does not stop the request ->
+  // re-draw with EOS masked from the same logits and the next draw (zero_shot_inference.rs:287-297)
+  int id = 0, status;
+  uint64_t used = 1;
+  bool stop = false, masked = eos_masked;
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    if (glob) advance_prep<NT, 4096, PT>(raw, sm, false, top_k, key, draw + attempt, c->gblk, &c->gblk_id, stamps);
+    else advance_prep<NT, NS, PT>(raw, sm, masked, top_k, key, draw + attempt, c->sblk, &c->sblk_id, stamps);
+    id = sample_block<NT>(sm, n, 1.0f, 0.95f, top_k, key, draw + attempt, false, nullptr, &status, stamps,
+                          a.cert != 0, true);
+    used = attempt + 1;
+    if (glob || id != RWKVTTS_EOS_TOKEN) break;
+    if (c->mode == 0) {
+      stop = true;
+      break;
+    }
+    const int wl = c->win_len;
+    const int non_eos = __builtin_popcount((uint32_t)c->win_bits & ((1u << wl) - 1u));
+    const float ratio = wl > 0 ? (float)non_eos / (float)wl : 0.0f;
+    if (wl >= 12 && ratio >= 0.7f) {
+      stop = true;
+      break;
+    }
+    masked = true;
+    __syncthreads();  // every thread has read the row state before the re-draw rewrites it
+  }
+  STAMP(15);
+  if (glob) {
     if (threadIdx.x == 0) {
       c->gdraw += 1;
       c->global_out[c->n_global++] = id;
@@ -1580,40 +1838,6 @@ __device__ __attribute__((always_inline)) void advance_body(const AdvanceArgs& a
       if (c->n_global == RWKVTTS_N_GLOBAL) c->phase = kPhGFeed;
     }
     return;
-  }
-  // semantic: rows [0, 8192] (j > 8192 and the tags are -inf in the reference)
-  constexpr int NS = RWKVTTS_EOS_TOKEN + 1;
-  const SampleSmem sm = carve<NT>(smem, NS);
-  const bool eos_masked = c->fixed || (c->mode == 1 && c->n_sem < c->hard_min);
-  load_logits_row<NT>(a, lg, sm.p, NS);
-  __syncthreads();
-  if (threadIdx.x == 0 && eos_masked) sm.p[RWKVTTS_EOS_TOKEN] = -__builtin_inff();
-  __syncthreads();
-  int status;
-  int id = sample_block<NT>(sm, NS, 1.0f, 0.95f, c->top_k_s, c->skey, c->sdraw, false, nullptr, &status, stamps,
-                            a.cert != 0);
-  STAMP(15);
-  uint64_t used = 1;
-  bool stop = false;
-  if (id == RWKVTTS_EOS_TOKEN) {
-    if (c->mode == 0) {
-      stop = true;
-    } else {
-      const int wl = c->win_len;
-      const int non_eos = __builtin_popcount((uint32_t)c->win_bits & ((1u << wl) - 1u));
-      const float ratio = wl > 0 ? (float)non_eos / (float)wl : 0.0f;
-      if (wl >= 12 && ratio >= 0.7f) {
-        stop = true;
-      } else {  // re-draw with EOS masked from the same logits (zero_shot_inference.rs:287-297)
-        for (int i = threadIdx.x; i < NS; i += NT) sm.p[i] = load_logit(a, lg, i);
-        __syncthreads();
-        if (threadIdx.x == 0) sm.p[RWKVTTS_EOS_TOKEN] = -__builtin_inff();
-        __syncthreads();
-        id = sample_block<NT>(sm, NS, 1.0f, 0.95f, c->top_k_s, c->skey, c->sdraw + 1, false, nullptr,
-                          &status, nullptr, a.cert != 0);
-        used = 2;
-      }
-    }
   }
   if (threadIdx.x == 0) {
     c->sdraw += used;
@@ -1632,7 +1856,7 @@ __device__ __attribute__((always_inline)) void advance_body(const AdvanceArgs& a
   }
 }
 
-__global__ __launch_bounds__(kSampleThreads) void k_advance(AdvanceArgs a) {
+__global__ __launch_bounds__(kSampleThreads, 2) void k_advance(AdvanceArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   tl_begin(a.tl);
   advance_body(a, smem);

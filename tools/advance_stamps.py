@@ -24,10 +24,11 @@ for i in range(32):
 for rep in range(2):
     rt.generate_batch(reqs)
     st = np.fromfile(path, dtype=np.uint64).reshape(256, 16)[:32].astype(np.int64)
-    names = {(0, 1): "load logits", (1, 2): "max + exp", (2, 10): "f64 sum | collect + draw",
-             (10, 11): "sample_cert", (11, 15): "controller tail", (0, 15): "total"}
-    print(f"rep {rep}: cycles (mean over 32 rows of the last step; s_memtime)")
-    for (a, b), nm in names.items():
+    order = [k for k in range(16) if (st[:, k] != 0).all()]
+    order.sort(key=lambda k: st[:, k].mean())
+    print(f"rep {rep}: s_memtime stamps of thread 0 (mean over 32 rows of the last step), in time order")
+    for a, b in zip(order, order[1:]):
         d = st[:, b] - st[:, a]
-        print(f"  {nm:26s} mean {d.mean():8.0f}  min {d.min():8d}  max {d.max():8d}")
+        print(f"  {a:2d} -> {b:2d}  mean {d.mean():8.0f}  min {d.min():8d}  max {d.max():8d}")
+    print(f"  total {(st[:, order[-1]] - st[:, order[0]]).mean():.0f}")
 rt.close()
