@@ -100,10 +100,11 @@ __device__ inline float draw_f32(const uint32_t* key, uint64_t index) {
   return (float)(chacha12_word(key, index) >> 8) * (1.0f / 16777216.0f);
 }
 
-// Optional phase stamps (debug builds of a call only: pointer is null in production).
+// Optional phase stamps (debug builds of a call only: pointer is null in production), in
+// s_memrealtime ticks (100 MHz, one clock for every CU: the unit of the TL=1 launch timeline).
 #define STAMP(k)                                                         \
   do {                                                                   \
-    if (stamps && threadIdx.x == 0) stamps[k] = __builtin_amdgcn_s_memtime(); \
+    if (stamps && threadIdx.x == 0) stamps[k] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 
 __device__ inline float readlane_f(float v, int l) {
@@ -1035,9 +1036,14 @@ __device__ __attribute__((always_inline)) int sample_fast(const SampleSmem& sm, 
 // the result equals the exact algorithm's for EVERY S in the interval, hence for the exact S;
 // otherwise the caller runs the exact sum. Returns the index, or -1 (not certified).
 // sm.keys[0, nc): candidates (e bits << 32 | index); E: f64 sum of e over the row; r: the draw.
+// The crude relative bound on the sequential f32 sum S of n non-negative terms around their real
+// sum E: recursive summation errs by at most (n - 1) 2^-24 E, widened to n 2^-23, plus the f64
+// sum's own error.
+__device__ inline double crude_sum_eps(int n) { return (double)n * 0x1p-23 + 0x1p-36; }
+
 template <int NT>
 __device__ __attribute__((always_inline)) int sample_cert(const SampleSmem& sm, int n, int nc, double E, float r, float top_p, int top_k,
-                           uint64_t* stamps = nullptr) {
+                           double eps, uint64_t* stamps = nullptr) {
   const int tid = threadIdx.x;
   STAMP(7);
   uint64_t* srt = sm.keys + 2048;  // candidates ranked by (e desc, index asc)
@@ -1071,7 +1077,6 @@ __device__ __attribute__((always_inline)) int sample_cert(const SampleSmem& sm, 
   STAMP(9);
   int ret = -1;
   if (tid < 64) {
-    const double eps = (double)n * 0x1p-23 + 0x1p-36;  // recursive f32 summation (2x) + the f64 sum's own error
     const double s_lo = E * (1.0 - eps), s_hi = E * (1.0 + eps);
     const double u = 0x1p-24, ua = 0x1p-23;
     bool ok = E > 0.0 && s_lo > 0.0 && E < 3.0e38;
@@ -1239,7 +1244,7 @@ __device__ __attribute__((always_inline)) int sample_block(const SampleSmem& sm,
     const int nc = sm.ired[31];
     const float L = sm.fred[20];
     if (want_fast && !dbg && cert && n <= kSampleMaxN && L > 0.0f && nc >= top_k && nc <= kFastCap) {
-      const int ret = sample_cert<NT>(sm, n, nc, sm.dscan[12], sm.fred[21], top_p, top_k, stamps);
+      const int ret = sample_cert<NT>(sm, n, nc, sm.dscan[12], sm.fred[21], top_p, top_k, sm.dscan[13], stamps);
       STAMP(11);
       if (ret >= 0) return ret;
     }
@@ -1258,7 +1263,7 @@ __device__ __attribute__((always_inline)) int sample_block(const SampleSmem& sm,
     const int nc = sm.ired[31];
     const float L = sm.fred[20];
     if (L > 0.0f && nc >= top_k && nc <= kFastCap) {
-      const int ret = sample_cert<NT>(sm, n, nc, sm.dscan[12], sm.fred[21], top_p, top_k);
+      const int ret = sample_cert<NT>(sm, n, nc, sm.dscan[12], sm.fred[21], top_p, top_k, crude_sum_eps(n));
       STAMP(11);
       if (ret >= 0) return ret;
     }
@@ -1760,10 +1765,59 @@ __device__ __attribute__((always_inline)) void advance_prep(const float* raw, co
       }
     }
   }
-  if (tid == 0) {
-    double E = sm.dscan[0];
+  // A tight rigorous bound on S (the crude one put 1.4 % of the bench's rows' draws inside a
+  // cumulative's uncertainty band -- and a row that falls back to the exact sum holds the whole
+  // launch, ~1 step in 3): S = sum e_i in index order, addition i (i >= 1) rounds by at most half
+  // an ulp of its result s_i, and s_i <= P_i (1 + eps0) with P_i the real prefix sum and eps0 the
+  // crude bound, so |S - E| <= B = sum_i 2^(floor(log2(P_i (1 + eps0))) - 24) (the f32 half-ulp at
+  // that binade, >= 2^-150); B is typically ~5x below n 2^-23 E. Threads take contiguous chunks of
+  // p; the index list region (unused on this path) holds the f64 partials.
+  double E = sm.dscan[0];
 #pragma unroll
-    for (int w = 1; w < NW; ++w) E += sm.dscan[w];
+  for (int w = 1; w < NW; ++w) E += sm.dscan[w];
+  {
+    double* dbuf = (double*)sm.list;  // 2 NT doubles
+    constexpr int C = (N + NT - 1) / NT, G = NT / 64;
+    const int b = min(n, tid * C), e = min(n, b + C);
+    double ts = 0.0;
+    for (int i = b; i < e; ++i) ts += (double)sm.p[i];
+    dbuf[tid] = ts;
+    __syncthreads();
+    if (tid < 64) {  // exclusive prefix of the chunk sums
+      double g[G], acc = 0.0;
+#pragma unroll
+      for (int q = 0; q < G; ++q) {
+        g[q] = dbuf[lane * G + q];
+        acc += g[q];
+      }
+      double run = wave_incl_scan_d(acc) - acc;
+#pragma unroll
+      for (int q = 0; q < G; ++q) {
+        dbuf[NT + lane * G + q] = run;
+        run += g[q];
+      }
+    }
+    __syncthreads();
+    const double up = 1.0 + crude_sum_eps(n) + 0x1p-30;
+    double P = dbuf[NT + tid], bp = 0.0;
+    for (int i = b; i < e; ++i) {
+      P += (double)sm.p[i];
+      if (i > 0) {
+        const int k = max((int)((__builtin_bit_cast(uint64_t, P * up) >> 52) & 0x7FF) - 1023, -126);
+        bp += __builtin_bit_cast(double, (uint64_t)(k - 24 + 1023) << 52);
+      }
+    }
+    dbuf[tid] = bp;
+    __syncthreads();
+    if (tid < 64) {
+      double acc = 0.0;
+#pragma unroll
+      for (int q = 0; q < G; ++q) acc += dbuf[lane * G + q];
+      const double B = readlane_d(wave_incl_scan_d(acc), 63);
+      if (tid == 0) sm.dscan[13] = B / E * (1.0 + 0x1p-30) + 0x1p-36;
+    }
+  }
+  if (tid == 0) {
     sm.dscan[12] = E;
     sm.fred[20] = L;
   }

@@ -1,4 +1,4 @@
-"""Per-phase s_memtime stamps of k_advance (the device sampler + phase controller) in the last
+"""Per-phase s_memrealtime stamps (10 ns ticks) of k_advance (the device sampler + phase controller) in the last
 decode step of a 32-request 0.4B batch (RWKVTTS_ADV_STAMPS debug hook). Usage: advance_stamps.py [S]"""
 import os
 import sys
@@ -23,12 +23,19 @@ for i in range(32):
                                         args=rwkvtts.SamplerArgs(seed=i), fixed_semantic=S))
 for rep in range(2):
     rt.generate_batch(reqs)
-    st = np.fromfile(path, dtype=np.uint64).reshape(256, 16)[:32].astype(np.int64)
+    allst = np.fromfile(path, dtype=np.uint64).reshape(256, 16).astype(np.int64)
+    st = allst[:32]
+    acc = allst[255]
+    print(f"all steps so far: per-row kernel time mean {acc[0] / max(acc[1], 1) * 0.01:.2f} us over {acc[1]} rows, "
+          f"max {acc[2] * 0.01:.2f} us; not certifiable {acc[3]}, rejected by the certificate {acc[4]}, "
+          f"mean candidates {acc[5] / max(acc[1], 1):.0f}; rejections by reason: top-k boundary {acc[7]}, "
+          f"top-p cut {acc[8]}, draw in band {acc[9]}, sum {acc[10]}")
     order = [k for k in range(16) if (st[:, k] != 0).all()]
     order.sort(key=lambda k: st[:, k].mean())
-    print(f"rep {rep}: s_memtime stamps of thread 0 (mean over 32 rows of the last step), in time order")
+    print(f"rep {rep}: s_memrealtime stamps of thread 0 (10 ns ticks; mean over 32 rows of the last step), in time order")
     for a, b in zip(order, order[1:]):
         d = st[:, b] - st[:, a]
         print(f"  {a:2d} -> {b:2d}  mean {d.mean():8.0f}  min {d.min():8d}  max {d.max():8d}")
-    print(f"  total {(st[:, order[-1]] - st[:, order[0]]).mean():.0f}")
+    print(f"  total {(st[:, order[-1]] - st[:, order[0]]).mean():.0f}; first row start -> last row end "
+          f"{st[:, order[-1]].max() - st[:, order[0]].min()}")
 rt.close()

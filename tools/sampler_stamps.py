@@ -1,4 +1,4 @@
-"""Per-phase cycle breakdown of the device sampler (s_memtime stamps via rwkvtts_debug_sample)."""
+"""Per-phase breakdown of the device sampler (s_memrealtime stamps, 10 ns ticks, via rwkvtts_debug_sample)."""
 import ctypes
 import os
 import sys
@@ -25,7 +25,7 @@ for n, p, k in [(8193, 0.95, 80), (4096, 0.95, 20), (1024, 0.95, 80), (8193, 1.0
           out.ctypes.data_as(ctypes.c_void_p), dbg.ctypes.data_as(ctypes.c_void_p))
     st = dbg[64:].view(np.uint64).reshape(32, 16)[:, :10].astype(np.int64)
     d = np.diff(st, axis=1).mean(axis=0)
-    print(f"n={n} p={p} k={k}: total {st[:, 9].mean() - st[:, 0].mean():.0f} cyc ;",
+    print(f"n={n} p={p} k={k}: total {st[:, 9].mean() - st[:, 0].mean():.0f} ticks ;",
           " ".join(f"{nm}={x:.0f}" for nm, x in zip(names, d)))
     s2 = dbg[64:].view(np.uint64).reshape(32, 16).astype(np.int64)
     print("   sum: scan", (s2[:, 10] - s2[:, 2]).mean(), "sim", (s2[:, 11] - s2[:, 10]).mean(), "compose",
