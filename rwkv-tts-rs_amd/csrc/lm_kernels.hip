@@ -628,7 +628,15 @@ __global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
   const int g = lane >> 4, li = lane & 15;
   const int col0 = (tile - tstart) * 64 + wave * 16;
   const int kbeg = split * KS;
-  const int row0 = a.xmap ? 0 : blockIdx.z * ROWS;
+  // row groups: a workgroup runs row groups blockIdx.z, blockIdx.z + gridDim.z, ... (prefill
+  // steps; decode steps have one) with its weight fragments loaded once, and requests the next
+  // group's X while the current one computes. Every output element takes the same MFMA sequence
+  // as with one row group per workgroup: bit-identical.
+  // (quantised launches keep one row group per workgroup: the loop's live registers spill there)
+  int rg = a.xmap ? 0 : (int)blockIdx.z;
+  const int nrg = (a.xmap || QW) ? rg + 1 : (e_M + ROWS - 1) / ROWS;
+  int row0 = rg * ROWS;
+  int xrow0 = row0;  // the row group load_x requests
   // X slice (activations of the previous launch, L2-resident) and weight stream (packed
   // fragment blocks, 1 KB per wave instruction). X is requested first: staging waits only for X
   // (vmcnt retires in order) while the weights are still in flight.
@@ -655,7 +663,7 @@ __global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
     for (int u = 0; u < PERP; ++u) {
       const int c = threadIdx.x + u * 256;
       const int r = c / CH, k8 = (c % CH) * 8;
-      const int src = min(row0 + r, a.M - 1);
+      const int src = min(xrow0 + r, a.M - 1);
       const int64_t o = (int64_t)src * ldx + kbeg + k8;
       vh[u] = *(const short8*)(Xhi + o);
       vl[u] = *(const short8*)(Xlo + o);
@@ -667,7 +675,7 @@ __global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
       for (int u = 0; u < PERR; ++u) {
         const int c = threadIdx.x + u * 256;
         const int r = c / (KS / 4), k4 = (c % (KS / 4)) * 4;
-        const int src = min(row0 + r, a.M - 1);
+        const int src = min(xrow0 + r, a.M - 1);
         xr[p][u] = *(const float4_*)(a.x_part + p * a.x_part_stride + (int64_t)src * a.x_ld + kbeg + k4);
       }
   }
@@ -705,6 +713,7 @@ __global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
   };
   load_x();
   load_w();
+  for (;;) {
   // 3) X -> LDS (rows past M hold a copy of row M-1; their outputs are not stored)
   if constexpr (XMODE == kXPlanes) {
 #pragma unroll
@@ -760,6 +769,11 @@ __global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
     }
   }
   __syncthreads();
+  const int rg_next = rg + (int)gridDim.z;
+  if (!QW && rg_next < nrg) {  // the next row group's X, in flight during this group's MFMAs and stores
+    xrow0 = rg_next * ROWS;
+    load_x();
+  }
   // 4) MFMA: hi and lo chains separate
   float4_ acc_h[MT], acc_l[MT];
 #pragma unroll
@@ -881,6 +895,11 @@ __global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
         const int row = row0 + m * 16 + 4 * g + j;
         if (row < e_M) out[(int64_t)row * e_ldo] = result(m, j);
       }
+  }
+  if (QW || rg_next >= nrg) break;
+  rg = rg_next;
+  row0 = rg * ROWS;
+  __syncthreads();  // every wave is done with the LDS X image / store staging
   }
   tl_end(a.tl);
 }
@@ -1153,6 +1172,17 @@ static void launch_gemm_t(const GemmArgs& a, dim3 grid, hipStream_t st) {
         b.tiles_per_xcd = (int)((grid.x * a.k_split + 7) / 8);
         grid = dim3(8 * b.tiles_per_xcd);
       }
+    }
+    // prefill steps: several row groups per workgroup (weights loaded once); RWKVTTS_GEMM_RPW
+    // sets the groups per workgroup (1: one each), default: as many as keep >= 4 workgroups per CU
+    if (grid.z > 1 && !a.q_fmt) {
+      static const int rpw_env = getenv("RWKVTTS_GEMM_RPW") ? atoi(getenv("RWKVTTS_GEMM_RPW")) : 0;
+      int rpw = rpw_env;
+      if (rpw <= 0) {
+        const int per_group = (int)(grid.x * grid.y);
+        rpw = std::max(1, (int)grid.z * per_group / 1024);
+      }
+      grid.z = (grid.z + rpw - 1) / rpw;
     }
 #define G2(F, XM, NX_, MS_)                                                               \
   do {                                                                                    \
