@@ -793,7 +793,8 @@ class Codec {
     // the default order (2x slower remapped)
     static const int xm = getenv("RWKVTTS_CODEC_XMAP") ? atoi(getenv("RWKVTTS_CODEC_XMAP")) : 3;
     a.xmap = 0;
-    if (grid.y > 1 && mode == 0 && grid.x >= 32 && (((xm & 1) && K == 7) || ((xm & 2) && K == 1))) {
+    if (grid.y > 1 && grid.x >= 32 &&
+        ((mode == 0 && (((xm & 1) && K == 7) || ((xm & 2) && K == 1))) || (mode == 1 && (xm & 4)))) {
       a.xmap = 1;
       a.gx = (int)grid.x;
       a.gy = (int)grid.y;
