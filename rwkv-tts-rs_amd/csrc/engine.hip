@@ -440,11 +440,18 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
   // state in place: no parity refresh / flip kernels (rows[].w was set once at upload)
   const bool inplace = tok_from_ctrl;
   if (!inplace) hipLaunchKernelGGL(k_rows_parity, dim3(nb), dim3(256), 0, stream_, d_rows_, slot_par_, R);
-  prof_begin(&ev);
   tl_n_ = 0;
-  launch_embed(d_tok_, d_rows_, &d_ctrl_[0].next_token, (int)(sizeof(SlotCtrl) / 4), emb_,
-               ln0_w_, ln0_b_, h0_, R, C, f16_, stream_, tl_next("embed"), dims.n_vocab);
-  prof_end("embed", ev);
+  // decode steps: the embedding (token -> row -> LN0) runs inside layer 0's LayerNorm launch (one
+  // launch and one boundary fewer per step; k_embed's arithmetic, bit for bit). Prefill steps keep
+  // k_embed (their token-shift rows need the previous token's embedding as well).
+  static const bool no_emb_fuse = getenv("RWKVTTS_NO_EMB_FUSE") != nullptr;  // A/B timing switch
+  const bool emb_fused = inplace && C == 1024 && !no_emb_fuse;
+  if (!emb_fused) {
+    prof_begin(&ev);
+    launch_embed(d_tok_, d_rows_, &d_ctrl_[0].next_token, (int)(sizeof(SlotCtrl) / 4), emb_,
+                 ln0_w_, ln0_b_, h0_, R, C, f16_, stream_, tl_next("embed"), dims.n_vocab);
+    prof_end("embed", ev);
+  }
   const int64_t RC = (int64_t)Rmax_ * C;
   for (int l = 0; l < Lc; ++l) {
     const LayerW& w = L_[l];
@@ -474,9 +481,19 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     m.row_map = nullptr;
     m.inplace = inplace ? 1 : 0;
     m.wt = (wt_mask_ >> 6) & 1;
+    if (l == 0 && emb_fused) {
+      m.emb_tok = d_tok_;
+      m.emb_ctrl = &d_ctrl_[0].next_token;
+      m.emb_ctrl_stride = (int)(sizeof(SlotCtrl) / 4);
+      m.emb = emb_;
+      m.ln0_w = ln0_w_;
+      m.ln0_b = ln0_b_;
+      m.n_vocab = dims.n_vocab;
+    }
     m.tl = tl_next("ln_att");
     prof_begin(&ev);
-    if (!(dbg_exp_ & 0x10000)) launch_ln_mix(m, R, stream_);
+    if (!(dbg_exp_ & 0x10000))
+      RT_CHECK(launch_ln_mix(m, R, stream_) >= 0, RWKVTTS_EUNSUPPORTED, "layer-0 embedding fusion: unsupported shape");
     prof_end("ln_mix_att", ev);
     // ---- r, k, v and the LoRA-down projections (w, a, v, g) in one launch (7 segments)
     GemmArgs g{};
@@ -549,6 +566,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     prof_end("gemm_wo", ev);
     // ---- ffn: residual + Wo partials -> LN2 -> mix
     LnMixArgs f = m;
+    f.emb = nullptr;  // (layer 0's embedding fusion belongs to the attention LayerNorm only)
     f.h_in = h1_;
     f.h_out = h0_;
     f.part = partO_;

@@ -38,6 +38,16 @@ struct LnMixArgs {
   int wt;              // k_ln1024: write-through (sc1) plane / residual / shift stores
   int inplace;         // decode step (one row per slot): the shift update overwrites the parity it
                        // read (same thread, read before write) and the parity is not flipped
+  // layer 0 of a decode step with the embedding fused in (emb != null: k_ln1024's EMB form): the
+  // row's token (rows[r] flagged kRowCtrl: emb_ctrl[slot * emb_ctrl_stride], else emb_tok[r]),
+  // its embedding row and LN0 (k_embed's arithmetic, bit for bit) replace the h_in load
+  const uint32_t* emb_tok;
+  const int* emb_ctrl;
+  int emb_ctrl_stride;
+  const bf16_t* emb;
+  const float* ln0_w;
+  const float* ln0_b;
+  int n_vocab;
 };
 
 struct GemmSeg {

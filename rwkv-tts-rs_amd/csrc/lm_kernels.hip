@@ -286,10 +286,12 @@ __global__ __launch_bounds__(256) void k_ln_mix(LnMixArgs a) {
 // MODE 0: ln_out (x = LN(h) planes only). Loads that need only the row (residual, slabs, LN and
 // mix vectors) are issued before the row descriptor that addresses the shift state.
 // ------------------------------------------------------------------------------------
-template <bool F16, int MODE, int NMIX, int NP>
+template <bool F16, int MODE, int NMIX, int NP, bool EMB = false>
 __global__ __launch_bounds__(256) void k_ln1024(LnMixArgs a) {
   constexpr int C = 1024;
+  static_assert(!EMB || (MODE == 1 && NP == 0), "embedding fusion: layer 0's LN + mixes");
   __shared__ float red[16];
+  __shared__ __attribute__((aligned(16))) float s_h[EMB ? C : 1];
   tl_begin(a.tl);
   bf16_t* e_xhi = a.x_hi;
   bf16_t* e_xlo = a.x_lo;
@@ -314,7 +316,42 @@ __global__ __launch_bounds__(256) void k_ln1024(LnMixArgs a) {
   for (int m = 0; m < NMIX; ++m) mu[m] = ld4(a.mu[m] + c);
   // the residual and the partial slabs (the previous launch's output) go out before the row
   // descriptor, whose dependent round trip only addresses the shift state
-  float4_ v = ld4(e_hin + (int64_t)row * C + c);
+  float4_ v;
+  if constexpr (EMB) {
+    // k_embed's arithmetic for this row (thread t: columns t + 256 i, sums in that order, the same
+    // block reductions; its zero-padded columns 1024.. add exact zeros), LN0 into LDS, then the
+    // row in this kernel's column order
+    const int4 info = a.rows[row];
+    uint32_t tok = (info.y & kRowCtrl) ? (uint32_t)a.emb_ctrl[(int64_t)info.x * a.emb_ctrl_stride] : a.emb_tok[row];
+    if (tok >= (uint32_t)a.n_vocab) tok = 0;
+    const bf16_t* er = a.emb + (int64_t)tok * C;
+    float ev[4];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      ev[i] = w16_to_f32(er[threadIdx.x + i * 256], F16);
+      s += ev[i];
+    }
+#pragma unroll
+    for (int i = 4; i < kMaxPerThread; ++i) s += 0.f;  // k_embed's padded columns (-0 + 0 = +0)
+    const float mean0 = block_sum256(s, red) / (float)C;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float d = ev[i] - mean0;
+      q += d * d;
+    }
+    const float rstd0 = 1.0f / sqrtf(block_sum256(q, red) / (float)C + 1e-5f);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int cc = threadIdx.x + i * 256;
+      s_h[cc] = (ev[i] - mean0) * rstd0 * a.ln0_w[cc] + a.ln0_b[cc];
+    }
+    __syncthreads();
+    v = *(const float4_*)(s_h + c);
+  } else {
+    v = ld4(e_hin + (int64_t)row * C + c);
+  }
   float4_ t[NP > 0 ? NP : 1];
 #pragma unroll
   for (int p = 0; p < NP; ++p) t[p] = ld4(e_part + p * e_pstride + (int64_t)row * e_ldp + c);
@@ -1117,6 +1154,12 @@ int launch_ln_mix(const LnMixArgs& a, int n_out_rows, hipStream_t st) {
   LnMixArgs b = a;
   b.n_rows = n_out_rows;
   const dim3 grid(n_out_rows);
+  if (a.emb) {  // layer 0 of a decode step with the embedding fused in
+    if (!(a.C == 1024 && a.shift && a.n_mix == 6 && a.n_part == 0)) return -1;
+    if (a.f16) RT_LAUNCH((k_ln1024<true, 1, 6, 0, true>), grid, dim3(256), 0, st, b);
+    else RT_LAUNCH((k_ln1024<false, 1, 6, 0, true>), grid, dim3(256), 0, st, b);
+    return n_out_rows;
+  }
   if (a.C == 1024 && (a.shift ? (a.n_mix == 6 || a.n_mix == 1) : true) &&
       (a.n_part == 0 || a.n_part == 8 || a.n_part == 16)) {
 #define LN_CASE(F, MO, NM)                                                                                  \
