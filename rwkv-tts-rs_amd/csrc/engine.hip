@@ -441,6 +441,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
   const bool inplace = tok_from_ctrl;
   if (!inplace) hipLaunchKernelGGL(k_rows_parity, dim3(nb), dim3(256), 0, stream_, d_rows_, slot_par_, R);
   tl_n_ = 0;
+  if (d_tl_) tl_names_.clear();  // the names of this forward's launches (decode steps have one fewer)
   // decode steps: the embedding (token -> row -> LN0) runs inside layer 0's LayerNorm launch (one
   // launch and one boundary fewer per step; k_embed's arithmetic, bit for bit). Prefill steps keep
   // k_embed (their token-shift rows need the previous token's embedding as well).
