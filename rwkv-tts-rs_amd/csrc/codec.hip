@@ -742,10 +742,15 @@ class Codec {
     const int ntaps_max = mode == 1 ? (K + s - 1) / s : K;
     const int span = (ntaps_max - 1) * (mode == 1 ? 1 : dil);
     const int KT = ntaps_max <= 1 ? 1 : (ntaps_max <= 3 ? 3 : 7);
-    {  // 7-tap convs: 96-wide column tiles wherever the double-buffered chunk (window + 7 taps'
-       // weights) fits the LDS: fewer column tiles re-reading each window (residual conv7 33.4 ->
-       // 31.1 ms per batch; tests bit-identical: the per-element accumulation order is unchanged)
-      static const int tn7 = getenv("RWKVTTS_CONV7_TN") ? atoi(getenv("RWKVTTS_CONV7_TN")) : 96;  // A/B switch
+    {  // 7-tap convs: 64-wide column tiles by default. 96-wide ones (where the double-buffered
+       // chunk fits: RWKVTTS_CONV7_TN=96) make the vocoder alone faster (residual conv7 33.4 ->
+       // 31.1 ms per batch) but their 155 KB of LDS leaves no room on the CU for a decode GEMM
+       // workgroup (34 KB): beside the next batch's token generator -- the serving shape, the
+       // bench -- every GEMM launch then waits for whole vocoder workgroups to retire. 64-wide
+       // tiles (124 KB) let them share the CU: decode step 0.883 -> 0.875 ms in the bench, +0.7 %
+       // samples/s (same-box A/B x2, tools/bench_ab.sh) for +1 ms of vocoder time. Tests
+       // bit-identical either way: the per-element accumulation order does not depend on TN.
+      static const int tn7 = getenv("RWKVTTS_CONV7_TN") ? atoi(getenv("RWKVTTS_CONV7_TN")) : 64;  // A/B switch
       const int wr = (256 + span + 15) & ~15;
       if (KT == 7 && mode == 0 && tn7 == 96 && Co % 96 == 0 && 2 * (size_t)(2 * wr + ntaps_max * 96) * 64 <= 160 * 1024)
         TN = 96;
