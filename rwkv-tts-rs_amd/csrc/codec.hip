@@ -833,7 +833,8 @@ class Codec {
     if (off || wlo || C != 96) return RWKVTTS_OK;
     const int span = 6 * dil;
     int nwv = 0;
-    for (int nw : {8, 4}) {
+    static const int nw_pref = getenv("RWKVTTS_RESFUSE_NW") ? atoi(getenv("RWKVTTS_RESFUSE_NW")) : 8;  // A/B switch
+    for (int nw : {nw_pref == 4 ? 4 : 8, 4}) {
       const int wr = (32 * nw + span + 15) & ~15;
       const size_t chunk = 2 * (size_t)(2 * wr + 7 * 96) * 64;
       const size_t fused = (size_t)3 * 2 * 32 * nw * 64 + 3 * 96 * 64;
