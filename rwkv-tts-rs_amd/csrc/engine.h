@@ -187,6 +187,7 @@ class Engine {
   uint64_t* dbg_stamps_ = nullptr;  // RWKVTTS_WKV_STAMPS=<file>: layer-5 WKV phase stamps
   std::string dbg_stamp_path_;
   int dbg_exp_ = 0;
+  bool no_emb_fuse_ = false;  // RWKVTTS_NO_EMB_FUSE at creation: decode steps launch k_embed separately
   uint64_t* dbg_astamps_ = nullptr;  // RWKVTTS_ADV_STAMPS=<file>: k_advance phase stamps, [rows][16]
   std::string dbg_astamp_path_;
   uint64_t* dbg_gstamps_ = nullptr;  // RWKVTTS_GEMM_STAMPS=<file>: layer-5 rkv / ffn_value GEMM stamps

@@ -94,6 +94,7 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
   RT_CHECK(splitA_ <= kMaxParts, RWKVTTS_EUNSUPPORTED, "n_embd too large for the WKV partial sum (raise kMaxParts)");
   state_perm_ = wkv_perm_layout(dims.d_decay, dims.d_aaa, dims.d_mv, dims.d_gate, splitA_, S_, desc.wkv_variant);
   if (const char* ex = getenv("RWKVTTS_DEBUG_EXP")) dbg_exp_ = atoi(ex);
+  no_emb_fuse_ = getenv("RWKVTTS_NO_EMB_FUSE") != nullptr;  // A/B switch (read per engine: tests compare)
   if (const char* xm = getenv("RWKVTTS_XMAP_MASK")) xmap_mask_ = (int)strtol(xm, nullptr, 0);
   if (const char* wm = getenv("RWKVTTS_WT_MASK")) wt_mask_ = (int)strtol(wm, nullptr, 0);
   if (const char* xa = getenv("RWKVTTS_XALIGN_MASK")) xalign_mask_ = (int)strtol(xa, nullptr, 0);
@@ -445,8 +446,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
   // decode steps: the embedding (token -> row -> LN0) runs inside layer 0's LayerNorm launch (one
   // launch and one boundary fewer per step; k_embed's arithmetic, bit for bit). Prefill steps keep
   // k_embed (their token-shift rows need the previous token's embedding as well).
-  static const bool no_emb_fuse = getenv("RWKVTTS_NO_EMB_FUSE") != nullptr;  // A/B timing switch
-  const bool emb_fused = inplace && C == 1024 && !no_emb_fuse;
+  const bool emb_fused = inplace && C == 1024 && !no_emb_fuse_;
   if (!emb_fused) {
     prof_begin(&ev);
     launch_embed(d_tok_, d_rows_, &d_ctrl_[0].next_token, (int)(sizeof(SlotCtrl) / 4), emb_,
