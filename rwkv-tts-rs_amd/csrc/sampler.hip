@@ -1677,6 +1677,16 @@ __device__ __attribute__((always_inline)) void advance_load_row(const AdvanceArg
     for (int k = 0; k < PT; ++k) w[k] = lg[a.part_stride + min(tid + k * NT, last)];
 #pragma unroll
     for (int k = 0; k < PT; ++k) v[k] += w[k];
+  } else if (a.n_part == 4) {
+    float w[3][PT];
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+#pragma unroll
+      for (int k = 0; k < PT; ++k) w[q][k] = lg[(q + 1) * a.part_stride + min(tid + k * NT, last)];
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+#pragma unroll
+      for (int k = 0; k < PT; ++k) v[k] += w[q][k];
   } else {
     for (int q = 1; q < a.n_part; ++q)
 #pragma unroll
