@@ -295,12 +295,20 @@ typedef struct {
 } rwkvtts_manager_desc;
 /* weights: one host blob. It crosses PCIe once, into the first engine's device; the manager then
  * broadcasts it over RCCL (ncclBroadcast over xGMI, one rank per distinct device, ncclCommInitAll)
- * to the other devices, and engines that share a device copy it device-to-device. This replaces
+ * to the other devices, and engines that share a device copy it device-to-device. With a single
+ * distinct device RCCL is never loaded; if RCCL is missing or cannot initialise, the blob goes to
+ * the other devices by hipMemcpyPeer (stats.bcast_rccl = 0). RWKVTTS_MANAGER_NO_RCCL=1 disables
+ * RCCL; RWKVTTS_MANAGER_FORCE_RCCL=1 runs it even for one device (and fails create if it fails).
+ * The caller's current HIP device is unchanged on return. This replaces
  * the reference's single model load handed to every infer worker (src/shared_runtime.rs:143-184,
  * src/dynamic_batch_manager.rs:33-87). */
 int rwkvtts_manager_create(const rwkvtts_manager_desc* desc, const void* weights, size_t bytes,
                            rwkvtts_manager** out);
-/* Stops the collector and the engine threads after the requests already submitted finish. */
+/* Stops the collector and the engine threads after the requests already submitted finish.
+ * Threads blocked in rwkvtts_manager_wait when destroy starts return (their result, or
+ * RWKVTTS_ECLOSED) before destroy frees the handle. No call on the handle may START while
+ * destroy runs or after it: the caller serialises destroy against new submit / wait /
+ * get_stats calls (as dropping the reference's manager requires no outstanding borrow). */
 int rwkvtts_manager_destroy(rwkvtts_manager* m);
 /* generate_tts (dynamic_batch_manager.rs:90-121) split in two: submit copies the request
  * (token arrays included) and returns a ticket; wait blocks up to timeout_ms (< 0: forever) and
@@ -321,6 +329,8 @@ typedef struct {
   int32_t bcast_ranks;                      /* distinct devices in the weight broadcast (RCCL ranks) */
   int32_t bcast_rccl;                       /* 1: the weights went out by ncclBroadcast */
   double bcast_ms;                          /* upload + broadcast wall time at create */
+  int32_t waiters;                          /* threads blocked in rwkvtts_manager_wait now */
+  int32_t reserved;
 } rwkvtts_manager_stats;
 int rwkvtts_manager_get_stats(rwkvtts_manager* m, rwkvtts_manager_stats* out);
 

@@ -111,6 +111,20 @@ int rwkvtts_debug_sample(rwkvtts_engine* e, const float* logits, int n_rows, int
   GUARD({ return e->eng.sample(logits, n_rows, row_len, args, rngs, out_tokens, dbg); })
 }
 
+// Test hook (not part of the drop-in surface): the production decode-step sampler k_advance
+// (advance_prep + the prepped sample_block; exact = 1 forces the exact sequential-sum walk) on
+// caller-given logit rows [n_rows][8193] and controller states (engine.h DebugAdvanceRow), for
+// n_steps launches; outputs are [n_steps][n_rows].
+int rwkvtts_debug_advance(rwkvtts_engine* e, const float* logits, int n_rows, const void* rows, int exact,
+                          int n_steps, int32_t* out_tok, int32_t* out_used, int32_t* out_phase) {
+  RT_CHECK(e && logits && rows && out_tok && out_used && out_phase, RWKVTTS_EINVAL, "debug_advance: bad arguments");
+  LOCK(e);
+  GUARD({
+    return e->eng.debug_advance(logits, n_rows, (const DebugAdvanceRow*)rows, exact, n_steps, out_tok, out_used,
+                                out_phase);
+  })
+}
+
 int rwkvtts_generate_batch(rwkvtts_engine* e, const rwkvtts_request* reqs, int n,
                            rwkvtts_result* results) {
   RT_CHECK(e && reqs && results && n >= 0, RWKVTTS_EINVAL, "generate_batch: bad arguments");

@@ -515,7 +515,7 @@ __global__ void k_f32_split_bf16(const float* in, bf16_t* hi, bf16_t* lo, int64_
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const uint16_t h = f32_to_bf16(in[i]);
     hi[i] = h;
-    lo[i] = f32_to_bf16(in[i] - bf16_to_f32(h));
+    if (lo) lo[i] = f32_to_bf16(in[i] - bf16_to_f32(h));
   }
 }
 
@@ -626,13 +626,13 @@ class Codec {
     const int64_t n = rwkvtts_codec_offset(&d, -1, 0, 0);
     RT_HIP(hipMalloc(&wf, n * sizeof(float)));
     RT_HIP(hipMalloc(&wb, n * sizeof(bf16_t)));
-    RT_HIP(hipMalloc(&wlb, n * sizeof(bf16_t)));
-    RT_HIP(hipMemcpy(wf, host_w, n * sizeof(float), hipMemcpyHostToDevice));
-    k_f32_split_bf16<<<2048, 256, 0, stream>>>(wf, wb, wlb, n);
     // the MFMA convs take the three-product path when any of their weights is not bf16-exact
-    // (RWKVTTS_CODEC_WLO=0 / 1 forces the choice: A/B timing)
+    // (RWKVTTS_CODEC_WLO=0 / 1 forces the choice: A/B timing); the lo plane exists only then
     wlo = !conv_weights_bf16_exact(host_w);
     if (const char* e = getenv("RWKVTTS_CODEC_WLO")) wlo = atoi(e) != 0;
+    if (wlo) RT_HIP(hipMalloc(&wlb, n * sizeof(bf16_t)));
+    RT_HIP(hipMemcpy(wf, host_w, n * sizeof(float), hipMemcpyHostToDevice));
+    k_f32_split_bf16<<<2048, 256, 0, stream>>>(wf, wb, wlb, n);
     RT_HIP(hipGetLastError());
     RT_HIP(hipStreamSynchronize(stream));
     // largest per-frame activation of the WaveGenerator (conv_in or any up stage)
@@ -768,7 +768,7 @@ class Codec {
     auto fits = [&](int tn, int nw) {
       return Co % tn == 0 && shm_of(tn, nw) <= 160 * 1024 && chunk_rows(tn, nw) / 16 <= 16 * nw;
     };
-    if (wlo && !fits(TN, nwv)) {
+    if (wlo && (!fits(TN, nwv) || TN > 96)) {  // (no weight-lo kernel wider than 96 columns)
       // the weight lo plane doubles the staged weights: the (tile width, waves) that fits and
       // stages the fewest LDS rows per output element
       int bt = 0, bw = 0;
@@ -787,7 +787,7 @@ class Codec {
     const size_t shm = shm_of(TN, nwv);
     RT_CHECK(fits(TN, nwv) && ntaps_max <= 7 && Ci <= 4096, RWKVTTS_EINVAL, "codec conv: tile window too large");
     ConvArgs a{};
-    a.xh = x.h; a.xl = x.l; a.x_bs = bs; a.Ci = Ci; a.tin_mul = tin_mul; a.w = w; a.wl = wlb + (w - wb); a.K = K; a.Co = Co;
+    a.xh = x.h; a.xl = x.l; a.x_bs = bs; a.Ci = Ci; a.tin_mul = tin_mul; a.w = w; a.wl = wlb ? wlb + (w - wb) : nullptr; a.K = K; a.Co = Co;
     a.mode = mode; a.dil = dil; a.pad = pad; a.s = s; a.bias = bias; a.rbias = o.rbias; a.rb_bs = o.rb_bs;
     a.gamma = o.gamma; a.res = o.res; a.act = o.act; a.y = o.y; a.yh = o.p.h; a.yl = o.p.l;
     a.y_alpha = o.alpha; a.y_bs = o.y_bs >= 0 ? o.y_bs : bs; a.ntok = d_ntok; a.zeros = zeros;
@@ -849,7 +849,7 @@ class Codec {
     const size_t shm = std::max(std::max(2 * (size_t)(2 * wr + 7 * 96) * 64, (size_t)3 * 2 * TM * 64 + 3 * 96 * 64),
                                 (size_t)nwv * 32 * 100 * sizeof(float));
     ConvArgs a{};
-    a.xh = x.h; a.xl = x.l; a.x_bs = bs; a.Ci = C; a.tin_mul = tin_mul; a.w = w7; a.wl = wlb + (w7 - wb); a.K = 7; a.Co = C;
+    a.xh = x.h; a.xl = x.l; a.x_bs = bs; a.Ci = C; a.tin_mul = tin_mul; a.w = w7; a.wl = wlb ? wlb + (w7 - wb) : nullptr; a.K = 7; a.Co = C;
     a.mode = 0; a.dil = dil; a.pad = 3 * dil; a.s = 1; a.bias = b7; a.rbias = nullptr; a.rb_bs = 0;
     a.gamma = nullptr; a.res = o.res; a.act = 0; a.y = o.y; a.yh = o.p.h; a.yl = o.p.l;
     a.y_alpha = o.alpha; a.y_bs = o.y_bs >= 0 ? o.y_bs : bs; a.ntok = d_ntok; a.zeros = zeros;

@@ -11,6 +11,20 @@
 
 namespace rwkvtts {
 
+// one row of the k_advance test hook (plain layout, mirrored by tests/test_gpu_advance.py)
+struct DebugAdvanceRow {
+  int32_t mode;      // 0 normal, 1 zero-shot
+  int32_t phase;     // 0 global, 2 semantic
+  int32_t top_k;
+  int32_t fixed;     // EOS always masked
+  int32_t n_sem;     // semantic tokens already emitted
+  int32_t hard_min;  // zero-shot: EOS masked while n_sem < hard_min
+  int32_t win_bits;  // zero-shot EOS window (newest at bit 0)
+  int32_t win_len;
+  uint32_t key[8];   // ChaCha12 key of the phase's stream
+  uint64_t draw;     // index of the next u32 draw
+};
+
 struct LayerW {
   const float *ln1_w, *ln1_b, *ln2_w, *ln2_b;
   const float* mu[6];  // x_r x_w x_k x_v x_a x_g
@@ -85,6 +99,11 @@ class Engine {
   int sample(const float* logits, int n_rows, int row_len, const rwkvtts_sample_args* args,
              rwkvtts_rng* const* rngs, int32_t* out, float* dbg_host = nullptr);
   int generate(const rwkvtts_request* reqs, int n, rwkvtts_result* res);
+  // Test hook (rwkvtts_debug_advance): k_advance itself -- advance_prep + the prepped
+  // sample_block, the certified fast path or the exact walk -- on caller-given logit rows and
+  // per-row controller states, for n_steps consecutive launches on the same rows.
+  int debug_advance(const float* logits, int n_rows, const struct DebugAdvanceRow* rows, int exact, int n_steps,
+                    int32_t* out_tok, int32_t* out_used, int32_t* out_phase);
   // Continuous batching until `src` is closed and every admitted job has finished.
   int serve(JobSource& src);
   // Checks a request before admission; fills `why` and returns false for a bad one.

@@ -539,7 +539,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     k.lnx_w = w.lnx_w; k.lnx_b = w.lnx_b;
     k.state = wkv_; k.slot_stride = (int64_t)Lc * H_ * 64 * 64; k.layer_off = (int64_t)l * H_ * 64 * 64;
     k.v_first = vfirst_; k.ldv = C; k.z_hi = z_hi_; k.z_lo = z_lo_; k.ldz = C;
-    k.segs = d_segs_; k.layer = l; k.C = C; k.n_slots = S_; k.n_seg = n_seg;
+    k.segs = d_segs_; k.layer = l; k.C = C; k.n_slots = S_; k.n_seg = n_seg; k.multi_row = R > n_seg;
     k.perm = state_perm_;
     k.allow_xmap = (xmap_mask_ >> 5) & 1;
     k.wt = (wt_mask_ >> 5) & 1;
@@ -798,6 +798,107 @@ int Engine::infer(const rwkvtts_input* in, int n, int head_rows, float* logits, 
 // ------------------------------------------------------------------------------------------
 // sample_logits_with_top_p_k on the device
 // ------------------------------------------------------------------------------------------
+// Test hook: k_advance on caller-given rows (see engine.h). Each row gets its own slot control
+// block; logits are [n_rows][8193] host floats (one partial). Per step and row: out_tok = the
+// token the step emitted (global or semantic; -1 if it emitted none: finished or stopped),
+// out_used = draws the step consumed, out_phase = the phase after the step.
+int Engine::debug_advance(const float* logits, int n_rows, const DebugAdvanceRow* rows, int exact, int n_steps,
+                          int32_t* out_tok, int32_t* out_used, int32_t* out_phase) {
+  RT_HIP(hipSetDevice(device_));
+  RT_CHECK(n_rows > 0 && n_rows <= 4096 && n_steps > 0 && n_steps <= 64, RWKVTTS_EINVAL, "debug_advance: bad sizes");
+  constexpr int LD = RWKVTTS_EOS_TOKEN + 1;
+  std::vector<SlotCtrl> c(n_rows);
+  for (int i = 0; i < n_rows; ++i) {
+    const DebugAdvanceRow& r = rows[i];
+    RT_CHECK((r.phase == kPhGlobal || r.phase == kPhSemantic) && r.top_k > 0 && r.n_sem >= 0 &&
+                 r.n_sem + n_steps <= RWKVTTS_SEMANTIC_LIMIT && (r.mode == 0 || r.mode == 1),
+             RWKVTTS_EINVAL, "debug_advance: bad row");
+    SlotCtrl& x = c[i];
+    memset(&x, 0, sizeof(x));
+    x.mode = r.mode;
+    x.phase = r.phase;
+    x.n_sem = r.n_sem;
+    x.sem_limit = RWKVTTS_SEMANTIC_LIMIT;
+    x.hard_min = r.hard_min;
+    x.fixed = r.fixed;
+    x.top_k_g = x.top_k_s = r.top_k;
+    x.win_bits = r.win_bits;
+    x.win_len = r.win_len;
+    memcpy(x.gkey, r.key, 32);
+    memcpy(x.skey, r.key, 32);
+    x.gdraw = x.sdraw = r.draw;
+  }
+  float* d_lg = nullptr;
+  SlotCtrl* d_c = nullptr;
+  int32_t *d_slot = nullptr, *d_sem = nullptr;
+  auto cleanup = [&] {
+    for (void* p : {(void*)d_lg, (void*)d_c, (void*)d_slot, (void*)d_sem})
+      if (p) hipFree(p);
+  };
+  int rc = RWKVTTS_OK;
+  do {
+    if (hipMalloc(&d_lg, (size_t)n_rows * LD * 4) != hipSuccess || hipMalloc(&d_c, sizeof(SlotCtrl) * n_rows) != hipSuccess ||
+        hipMalloc(&d_slot, 4 * (size_t)n_rows) != hipSuccess ||
+        hipMalloc(&d_sem, 4 * (size_t)n_rows * RWKVTTS_SEMANTIC_LIMIT) != hipSuccess) {
+      set_error("debug_advance: allocation");
+      rc = RWKVTTS_ENOMEM;
+      break;
+    }
+    std::vector<int32_t> slot(n_rows);
+    for (int i = 0; i < n_rows; ++i) slot[i] = i;
+    if (hipMemcpy(d_lg, logits, (size_t)n_rows * LD * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(d_c, c.data(), sizeof(SlotCtrl) * n_rows, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(d_slot, slot.data(), 4 * (size_t)n_rows, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemset(d_sem, 0xFF, 4 * (size_t)n_rows * RWKVTTS_SEMANTIC_LIMIT) != hipSuccess) {
+      set_error("debug_advance: upload");
+      rc = RWKVTTS_EHIP;
+      break;
+    }
+    AdvanceArgs a{};
+    a.logits = d_lg;
+    a.ld = LD;
+    a.n_part = 1;
+    a.part_stride = 0;
+    a.row_slot = d_slot;
+    a.ctrl = d_c;
+    a.sem_out = d_sem;
+    a.n_rows = n_rows;
+    std::vector<SlotCtrl> prev = c, now(n_rows);
+    for (int s = 0; s < n_steps && rc == RWKVTTS_OK; ++s) {
+      launch_advance(a, stream_, exact ? 0 : 1);
+      if (hipStreamSynchronize(stream_) != hipSuccess ||
+          hipMemcpy(now.data(), d_c, sizeof(SlotCtrl) * n_rows, hipMemcpyDeviceToHost) != hipSuccess) {
+        set_error("debug_advance: launch");
+        rc = RWKVTTS_EHIP;
+        break;
+      }
+      for (int i = 0; i < n_rows; ++i) {
+        const SlotCtrl &p = prev[i], &q = now[i];
+        const int64_t o = (int64_t)s * n_rows + i;
+        out_phase[o] = q.phase;
+        if (p.phase == kPhGlobal) {
+          out_tok[o] = q.n_global > p.n_global ? q.global_out[p.n_global] : -1;
+          out_used[o] = (int32_t)(q.gdraw - p.gdraw);
+        } else {
+          out_used[o] = (int32_t)(q.sdraw - p.sdraw);
+          out_tok[o] = -1;
+          if (q.n_sem > p.n_sem) {
+            int32_t t = -1;
+            if (hipMemcpy(&t, d_sem + (int64_t)i * RWKVTTS_SEMANTIC_LIMIT + p.n_sem, 4, hipMemcpyDeviceToHost) != hipSuccess) {
+              set_error("debug_advance: read-back");
+              rc = RWKVTTS_EHIP;
+            }
+            out_tok[o] = t;
+          }
+        }
+      }
+      prev = now;
+    }
+  } while (false);
+  cleanup();
+  return rc;
+}
+
 int Engine::sample(const float* logits, int n_rows, int row_len, const rwkvtts_sample_args* args,
                    rwkvtts_rng* const* rngs, int32_t* out, float* dbg_host) {
   RT_HIP(hipSetDevice(device_));

@@ -141,6 +141,8 @@ struct WkvArgs {
   int f16;             // fp16 model: LoRA-up rows and the z planes are f16
   uint64_t* stamps;    // debug: 8 s_memtime stamps per workgroup (null in production)
   int exp;             // debug experiment bits (0 in production)
+  int multi_row;       // some segment has > 1 row (prefill / mixed step): a separate kernel
+                       // instantiation, so profiles separate decode launches from prefill ones
   unsigned long long* tl;  // debug timeline slot (null in production)
 };
 

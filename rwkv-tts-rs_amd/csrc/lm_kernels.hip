@@ -1907,7 +1907,7 @@ __global__ __launch_bounds__(128) void k_wkv4(WkvArgs a) {
 // State blocks: thread t's q-th float4 at float4 index q * 256 + t (engine.hip perm_index,
 // layout 2); LoRA-up rows: entry u of thread t at uint4 index u * 256 + t (launch_pack_lora6).
 // ------------------------------------------------------------------------------------
-template <bool F16>
+template <bool F16, bool MULTI_ROW = false>  // MULTI_ROW: the same code, a distinct symbol for prefill steps
 __global__ __launch_bounds__(256) void k_wkv6(WkvArgs a) {
   constexpr int N = 64, DW = 64, DA = 64, DV = 32, DG = 128, DALL = DW + DA + DV + DG, NP = 4;
   __shared__ __attribute__((aligned(16))) float s_hid[DALL];
@@ -2117,8 +2117,13 @@ int launch_wkv(const WkvArgs& a, int n_seg, int H, hipStream_t st) {
     b.n_seg = n_seg;
     const dim3 g = b.xmap ? dim3(n_seg * H) : grid;
     if (a.perm == 2) {
-      if (a.f16) RT_LAUNCH((k_wkv6<true>), g, dim3(256), 0, st, b);
-      else RT_LAUNCH((k_wkv6<false>), g, dim3(256), 0, st, b);
+      if (a.multi_row) {
+        if (a.f16) RT_LAUNCH((k_wkv6<true, true>), g, dim3(256), 0, st, b);
+        else RT_LAUNCH((k_wkv6<false, true>), g, dim3(256), 0, st, b);
+      } else {
+        if (a.f16) RT_LAUNCH((k_wkv6<true>), g, dim3(256), 0, st, b);
+        else RT_LAUNCH((k_wkv6<false>), g, dim3(256), 0, st, b);
+      }
     } else {
       if (a.f16) RT_LAUNCH((k_wkv4<true>), g, dim3(128), 0, st, b);
       else RT_LAUNCH((k_wkv4<false>), g, dim3(128), 0, st, b);

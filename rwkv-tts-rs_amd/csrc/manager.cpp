@@ -14,6 +14,7 @@
 // has one owner thread running Engine::serve, which admits queued requests into free state slots
 // between forward steps (continuous batching). One engine per GPU = request-level data
 // parallelism over the node; no collective is needed on this path.
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -139,6 +140,7 @@ class Worker : public JobSource {
 
 class Manager {
  public:
+  ~Manager() { free_dev_blobs(); }
   int create(const rwkvtts_manager_desc& d, const void* w, size_t bytes) {
     desc_ = d;
     RT_CHECK(d.n_engines >= 1 && d.n_engines <= RWKVTTS_MAX_ENGINES, RWKVTTS_EINVAL, "manager: 1..16 engines");
@@ -173,10 +175,28 @@ class Manager {
 
   // The weight blob crosses PCIe once (host -> the first device), then goes to every other
   // distinct device by ncclBroadcast over xGMI (RCCL, one rank per device in one process:
-  // ncclCommInitAll). With a single distinct device the broadcast is a one-rank RCCL call (the
-  // same code path, a no-op transfer); engines sharing a device read that device's copy.
+  // ncclCommInitAll). With a single distinct device there is nothing to broadcast: RCCL is not
+  // loaded at all (RWKVTTS_MANAGER_FORCE_RCCL=1 still runs the one-rank call, so the RCCL code
+  // path can be exercised on a one-GPU box). If RCCL is missing or fails to initialise with
+  // several devices, the blob goes out by hipMemcpyPeer instead (bcast_rccl = 0 then; the
+  // reason is kept in bcast_note_). Engines sharing a device read that device's copy.
+  // The caller's current device is restored on return, and every device blob is freed on any
+  // error path.
   int broadcast_weights(const rwkvtts_manager_desc& d, const void* w, size_t bytes) {
     const auto t0 = Clock::now();
+    int prev_dev = 0;
+    RT_HIP(hipGetDevice(&prev_dev));
+    struct Restore {
+      int dev;
+      ~Restore() { hipSetDevice(dev); }
+    } restore{prev_dev};
+    struct FreeOnError {
+      Manager* m;
+      bool armed = true;
+      ~FreeOnError() {
+        if (armed) m->free_dev_blobs();
+      }
+    } guard{this};
     std::vector<int> devs;
     rank_of_.assign(d.n_engines, 0);
     for (int i = 0; i < d.n_engines; ++i) {
@@ -193,23 +213,48 @@ class Manager {
     }
     RT_HIP(hipSetDevice(devs[0]));
     RT_HIP(hipMemcpy(dev_blob_[0], w, bytes, hipMemcpyHostToDevice));
-    std::vector<ncclComm_t> comms(n, nullptr);
-    std::vector<hipStream_t> streams(n, nullptr);
+    const bool no_rccl = env_flag("RWKVTTS_MANAGER_NO_RCCL");
+    const bool force_rccl = env_flag("RWKVTTS_MANAGER_FORCE_RCCL");
+    bcast_rccl_ = 0;
+    if (!no_rccl && (n > 1 || force_rccl)) {
+      const int rc = rccl_broadcast(devs, bytes);
+      if (rc == RWKVTTS_OK) bcast_rccl_ = 1;
+      else if (force_rccl) return rc;  // asked for RCCL explicitly: report why it failed
+    } else if (n > 1) {
+      bcast_note_ = "RCCL disabled (RWKVTTS_MANAGER_NO_RCCL)";
+    }
+    if (!bcast_rccl_)
+      for (int r = 1; r < n; ++r)
+        RT_HIP(hipMemcpyPeer(dev_blob_[r], devs[r], dev_blob_[0], devs[0], bytes));
+    guard.armed = false;
+    bcast_ranks_ = n;
+    bcast_ms_ = std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
+    return RWKVTTS_OK;
+  }
+
+  // One grouped ncclBroadcast from dev_blob_[0] to every distinct device's buffer. On failure
+  // returns an error code with the reason in bcast_note_ (and last_error); nothing is freed here.
+  int rccl_broadcast(const std::vector<int>& devs, size_t bytes) {
+    const int n = (int)devs.size();
     const Rccl& R = rccl();
     if (!R.ok) {
-      free_dev_blobs();
-      set_error("manager: RCCL (librccl.so.1) not available for the weight broadcast");
+      bcast_note_ = "RCCL (librccl.so.1) not available";
+      set_error("manager: " + bcast_note_);
       return RWKVTTS_EUNSUPPORTED;
     }
-    auto nccl_ok = [&R](ncclResult_t r, const char* what) {
+    std::vector<ncclComm_t> comms(n, nullptr);
+    std::vector<hipStream_t> streams(n, nullptr);
+    auto nccl_ok = [&](ncclResult_t r, const char* what) {
       if (r == ncclSuccess) return true;
-      set_error(std::string("manager: ") + what + ": " + R.GetErrorString(r));
+      bcast_note_ = std::string(what) + ": " + R.GetErrorString(r);
+      set_error("manager: " + bcast_note_);
       return false;
     };
     int rc = RWKVTTS_OK;
     if (!nccl_ok(R.CommInitAll(comms.data(), n, devs.data()), "ncclCommInitAll")) rc = RWKVTTS_EHIP;
     for (int r = 0; r < n && rc == RWKVTTS_OK; ++r) {
       if (hipSetDevice(devs[r]) != hipSuccess || hipStreamCreateWithFlags(&streams[r], hipStreamNonBlocking) != hipSuccess) {
+        bcast_note_ = "broadcast stream";
         set_error("manager: broadcast stream");
         rc = RWKVTTS_EHIP;
       }
@@ -222,7 +267,10 @@ class Manager {
       for (int r = 0; r < n && ok; ++r) {
         hipSetDevice(devs[r]);
         ok = hipStreamSynchronize(streams[r]) == hipSuccess;
-        if (!ok) set_error("manager: broadcast synchronisation");
+        if (!ok) {
+          bcast_note_ = "broadcast synchronisation";
+          set_error("manager: broadcast synchronisation");
+        }
       }
       if (!ok) rc = RWKVTTS_EHIP;
     }
@@ -233,13 +281,12 @@ class Manager {
       }
       if (comms[r]) R.CommDestroy(comms[r]);
     }
-    if (rc != RWKVTTS_OK) {
-      free_dev_blobs();
-      return rc;
-    }
-    bcast_ranks_ = n;
-    bcast_ms_ = std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
-    return RWKVTTS_OK;
+    return rc;
+  }
+
+  static bool env_flag(const char* name) {
+    const char* v = getenv(name);
+    return v && *v && strcmp(v, "0") != 0;
   }
 
   void free_dev_blobs() {
@@ -363,8 +410,12 @@ class Manager {
     }
     s->batches = batches_.load();
     s->bcast_ranks = bcast_ranks_;
-    s->bcast_rccl = bcast_ranks_ > 0 ? 1 : 0;
+    s->bcast_rccl = bcast_rccl_;
     s->bcast_ms = bcast_ms_;
+    {
+      std::lock_guard<std::mutex> lk(t_mu_);
+      s->waiters = waiters_;
+    }
     for (size_t i = 0; i < workers_.size(); ++i) {
       s->served[i] = workers_[i]->served.load();
       s->max_active[i] = workers_[i]->max_active.load();
@@ -447,6 +498,8 @@ class Manager {
   std::vector<int> dev_of_;      // distinct devices, RCCL rank order
   std::vector<int> rank_of_;     // engine -> its device's rank
   int bcast_ranks_ = 0;
+  int bcast_rccl_ = 0;       // 1 only when ncclBroadcast actually moved the blob
+  std::string bcast_note_;   // why RCCL was not used (when it was not)
   double bcast_ms_ = 0.0;
   std::vector<std::unique_ptr<Worker>> workers_;
   std::thread collector_;

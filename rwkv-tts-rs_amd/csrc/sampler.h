@@ -73,6 +73,7 @@ struct AdvanceArgs {
 
 size_t wide_scratch_bytes(int n);
 void launch_sample_rows(const SampleRowArgs& a, int rows, hipStream_t st);
-int launch_advance(const AdvanceArgs& a, hipStream_t st);
+// cert_override: -1 = RWKVTTS_SAMPLER_EXACT decides; 0 = exact walk; 1 = certified fast path allowed
+int launch_advance(const AdvanceArgs& a, hipStream_t st, int cert_override = -1);
 
 }  // namespace rwkvtts

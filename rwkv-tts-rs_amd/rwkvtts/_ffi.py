@@ -90,7 +90,8 @@ class ManagerStats(ctypes.Structure):
     _fields_ = [("submitted", ctypes.c_int64), ("completed", ctypes.c_int64), ("batches", ctypes.c_int64),
                 ("served", ctypes.c_int64 * MAX_ENGINES), ("max_active", ctypes.c_int64 * MAX_ENGINES),
                 ("steps", ctypes.c_int64 * MAX_ENGINES), ("bcast_ranks", ctypes.c_int32),
-                ("bcast_rccl", ctypes.c_int32), ("bcast_ms", ctypes.c_double)]
+                ("bcast_rccl", ctypes.c_int32), ("bcast_ms", ctypes.c_double),
+                ("waiters", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 class CodecDims(ctypes.Structure):

@@ -389,6 +389,24 @@ class DynamicBatchManager:
         # per calling thread: concurrent generate_tts callers (the server's worker threads) never
         # see each other's status codes
         self._tls = threading.local()
+        # close() must not race a call that has not yet entered the native manager (rwkvtts.h:
+        # destroy may not overlap the START of another call): calls are counted here, close()
+        # refuses new ones and waits until every call still in flight is a waiter the native
+        # manager has registered (those return inside destroy, before the handle is freed)
+        self._gate = threading.Condition()
+        self._inflight = 0
+        self._closing = False
+
+    def _enter(self):
+        with self._gate:
+            if self._closing or not getattr(self, "_h", None):
+                raise _ffi.RwkvTtsError(_ffi.ECLOSED, "manager is closed")
+            self._inflight += 1
+
+    def _leave(self):
+        with self._gate:
+            self._inflight -= 1
+            self._gate.notify_all()
 
     @property
     def last_status(self):
@@ -396,8 +414,21 @@ class DynamicBatchManager:
         return getattr(self._tls, "last_status", [])
 
     def close(self):
-        if getattr(self, "_h", None):
-            lib().rwkvtts_manager_destroy(self._h)
+        gate = getattr(self, "_gate", None)
+        if gate is None:
+            return
+        with gate:
+            if self._closing or not getattr(self, "_h", None):
+                return
+            self._closing = True
+            while True:
+                s = _ffi.ManagerStats()
+                check(lib().rwkvtts_manager_get_stats(self._h, ctypes.byref(s)), "manager_get_stats")
+                if self._inflight <= s.waiters:
+                    break
+                gate.wait(0.005)
+        lib().rwkvtts_manager_destroy(self._h)
+        with gate:
             self._h = None
 
     def __del__(self):
@@ -416,7 +447,11 @@ class DynamicBatchManager:
     def submit(self, request: "TtsBatchRequest") -> int:
         q, keep = request_struct(request)
         t = ctypes.c_uint64()
-        check(lib().rwkvtts_manager_submit(self._h, ctypes.byref(q), ctypes.byref(t)), "manager_submit")
+        self._enter()
+        try:
+            check(lib().rwkvtts_manager_submit(self._h, ctypes.byref(q), ctypes.byref(t)), "manager_submit")
+        finally:
+            self._leave()
         return int(t.value)
 
     def wait(self, ticket: int, timeout_ms: int = -1):
@@ -430,7 +465,11 @@ class DynamicBatchManager:
         r = _ffi.Result()
         sb = np.zeros(_ffi.SEMANTIC_LIMIT, dtype=np.int32)
         r.semantic_tokens = sb.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
-        rc = lib().rwkvtts_manager_wait(self._h, ctypes.c_uint64(ticket), timeout_ms, ctypes.byref(r))
+        self._enter()
+        try:
+            rc = lib().rwkvtts_manager_wait(self._h, ctypes.c_uint64(ticket), timeout_ms, ctypes.byref(r))
+        finally:
+            self._leave()
         if rc == _ffi.EBUSY:
             return None, None
         check(rc, "manager_wait")
@@ -456,8 +495,13 @@ class DynamicBatchManager:
 
     def stats(self):
         s = _ffi.ManagerStats()
-        check(lib().rwkvtts_manager_get_stats(self._h, ctypes.byref(s)), "manager_get_stats")
+        self._enter()
+        try:
+            check(lib().rwkvtts_manager_get_stats(self._h, ctypes.byref(s)), "manager_get_stats")
+        finally:
+            self._leave()
         n = len(self.devices)
         return {"submitted": s.submitted, "completed": s.completed, "batches": s.batches,
                 "served": list(s.served[:n]), "max_active": list(s.max_active[:n]), "steps": list(s.steps[:n]),
-                "bcast_ranks": s.bcast_ranks, "bcast_rccl": s.bcast_rccl, "bcast_ms": s.bcast_ms}
+                "bcast_ranks": s.bcast_ranks, "bcast_rccl": s.bcast_rccl, "bcast_ms": s.bcast_ms,
+                "waiters": s.waiters}

@@ -93,6 +93,30 @@ def test_full_dims_batch_of_32_vs_oracle(oracle_mod):
         c.close()
 
 
+def test_full_dims_bench_shape_512_frames_vs_oracle(oracle_mod):
+    """The bench's vocoder launch at its full shape: 32 utterances x 512 frames
+    (163,840 samples each) in ONE batched decode at the full dims -- long-T tiling, halo windows
+    across many time tiles and the blockIdx.z batching at T = 512 -- with the first and last
+    utterance compared against the oracle over all 163,840 samples (~10 s of oracle time each at
+    16 threads)."""
+    d = codec.CODEC_DIMS_FULL
+    w = codec.synth_codec_blob(d)
+    c = codec.BiCodecDetokenizer(w, d)
+    rs = np.random.default_rng(512)
+    items = [(rs.integers(0, 4096, 32), rs.integers(0, 8192, 512)) for _ in range(32)]
+    try:
+        outs = c.decode_audio_batch(items)
+        assert all(o.size == 512 * 320 for o in outs)
+        cd = codec.make_codec_dims(d)
+        for i in (0, 31):
+            g, s = items[i]
+            _check(outs[i], oracle_mod.codec_decode(cd, w, s, g, threads=16))
+        # and the same utterance decoded alone is bitwise the batched one
+        assert np.array_equal(outs[31], c.decode_audio(*items[31]))
+    finally:
+        c.close()
+
+
 def _decoder(w, d, wlo=None):
     """A decoder with the conv path forced (RWKVTTS_CODEC_WLO, read at creation) or automatic."""
     old = os.environ.pop("RWKVTTS_CODEC_WLO", None)

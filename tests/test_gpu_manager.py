@@ -2,10 +2,14 @@
 benchmarked shape and under failure:
 
 * config 4's per-GPU path: DIMS_04B weights, 32 slots per engine, two engines, 48 requests from
-  concurrent submitter threads, the weight blob uploaded once and ncclBroadcast (RCCL) to the
-  engines' devices -- on a one-GPU box both engines share device 0, so the broadcast is a one-rank
-  RCCL call and the second engine copies device-to-device; sampled requests token-exact against
-  the oracle; live statistics while the manager runs;
+  concurrent submitter threads, the weight blob uploaded once and (RWKVTTS_MANAGER_FORCE_RCCL)
+  ncclBroadcast to the engines' devices -- on a one-GPU box both engines share device 0, so the
+  broadcast is a one-rank RCCL call and the second engine copies device-to-device; sampled
+  requests token-exact against the oracle; live statistics while the manager runs;
+* config 4's whole workload on the one GPU: 8 engines x 32 slots (the 8-GPU node's engine count,
+  all on device 0), 256 requests from 8 submitter threads, every engine serving, sampled
+  requests token-exact against the oracle; one distinct device -> RCCL is not loaded;
+* RCCL disabled (RWKVTTS_MANAGER_NO_RCCL): the manager still creates and serves;
 * an injected admission failure (RWKVTTS_TEST_FAIL_ADMIT): every ticket still resolves;
 * a second waiter on one ticket is refused; destroy with a waiter blocked returns its result;
 * two engines on one device capturing their first decode graphs at the same moment.
@@ -49,11 +53,28 @@ def _run_concurrent(fns, timeout):
     return out
 
 
+class _env:
+    def __init__(self, **kv):
+        self.kv = kv
+
+    def __enter__(self):
+        self.old = {k: os.environ.get(k) for k in self.kv}
+        os.environ.update({k: str(v) for k, v in self.kv.items()})
+
+    def __exit__(self, *a):
+        for k, v in self.old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
 def test_manager_04b_32_slots_two_engines_rccl():
     blob = W.synth_blob(W.DIMS_04B, seed=20251205)
     import oracle
-    m = rwkvtts.DynamicBatchManager(blob, rwkvtts.DynamicBatchConfig(max_batch_size=50, collect_timeout_ms=20),
-                                    devices=[0, 0], max_slots=32, token_chunk_size=512)
+    with _env(RWKVTTS_MANAGER_FORCE_RCCL=1):
+        m = rwkvtts.DynamicBatchManager(blob, rwkvtts.DynamicBatchConfig(max_batch_size=50, collect_timeout_ms=20),
+                                        devices=[0, 0], max_slots=32, token_chunk_size=512)
     try:
         st0 = m.stats()
         assert st0["bcast_rccl"] == 1 and st0["bcast_ranks"] == 1, st0
@@ -82,6 +103,63 @@ def test_manager_04b_32_slots_two_engines_rccl():
             assert len(got[i][0]) == 32 and len(got[i][1]) == 6 + i % 5
     finally:
         m.close()
+
+
+def test_manager_config4_eight_engines_256_requests():
+    """Config 4's request-level data parallelism (dynamic_batch_manager.rs:33-87,185-405) at its
+    full shape, on the one GPU: 8 engines x 32 slots, 256 requests, 8 submitter threads."""
+    blob = W.synth_blob(W.DIMS_04B, seed=20251205)
+    import oracle
+    n_eng, n_req, n_thr = 8, 256, 8
+    m = rwkvtts.DynamicBatchManager(blob, rwkvtts.DynamicBatchConfig(max_batch_size=64, collect_timeout_ms=20),
+                                    devices=[0] * n_eng, max_slots=32, token_chunk_size=512)
+    try:
+        st0 = m.stats()
+        # one distinct device: nothing to broadcast, RCCL is not even loaded
+        assert st0["bcast_ranks"] == 1 and st0["bcast_rccl"] == 0, st0
+        reqs = [make_request(synth_text(9000 + i), seed=4000 + i, fixed=3 + i % 4) for i in range(n_req)]
+        got = [None] * n_req
+
+        def submitter(k):
+            def run():
+                tickets = [(i, m.submit(reqs[i])) for i in range(k, n_req, n_thr)]
+                for i, t in tickets:
+                    got[i] = m.wait(t, timeout_ms=240000)
+            return run
+        _run_concurrent([submitter(k) for k in range(n_thr)], timeout=280)
+        missing = [i for i in range(n_req) if got[i] is None]
+        assert not missing, ("tickets not resolved", missing[:8], m.stats())
+        st = m.stats()
+        assert st["completed"] == n_req and sum(st["served"]) == n_req, st
+        assert all(n > 0 for n in st["served"]), ("an engine served nothing", st["served"])
+        assert max(st["max_active"]) <= 32, st
+        for i in range(n_req):
+            assert len(got[i][0]) == 32 and len(got[i][1]) == 3 + i % 4, i
+        om = oracle.Model(blob)
+        for i in (0, 31, 64, 100, 127, 170, 222, 255):
+            assert got[i] == _oracle(om, reqs[i]), i
+    finally:
+        m.close()
+
+
+def test_manager_without_rccl():
+    """RCCL disabled: a one-device manager never needs it; a multi-engine one still creates,
+    serves and reports bcast_rccl = 0 (single-GPU deployments carry no RCCL)."""
+    blob = W.synth_blob(W.DIMS_TINY, seed=99)
+    import oracle
+    with _env(RWKVTTS_MANAGER_NO_RCCL=1):
+        m = rwkvtts.DynamicBatchManager(blob, devices=[0, 0], max_slots=2, token_chunk_size=64)
+    try:
+        st = m.stats()
+        assert st["bcast_rccl"] == 0 and st["bcast_ranks"] == 1, st
+        reqs = [make_request(synth_text(8100 + i), seed=50 + i, max_tokens=10) for i in range(4)]
+        got = m.generate_tts_batch(reqs)
+        om = oracle.Model(blob)
+        assert got == [_oracle(om, r) for r in reqs]
+    finally:
+        m.close()
+    import torch
+    assert torch.cuda.current_device() == 0
 
 
 def test_manager_admission_failure_resolves_every_ticket():
@@ -129,7 +207,16 @@ def test_manager_ticket_waiters():
         second = []
         th2 = threading.Thread(target=lambda: second.append(m.wait_status(t2, timeout_ms=120000)), daemon=True)
         th2.start()
-        time.sleep(0.05)
+        # every waiter that has not returned yet is blocked inside the native wait (not merely
+        # started) before destroy
+        t_end = time.time() + 30
+        while time.time() < t_end:
+            need = (0 if first else 1) + (0 if second else 1)
+            if m.stats()["waiters"] >= need:
+                break
+            time.sleep(0.005)
+        else:
+            raise AssertionError("waiter threads never blocked in rwkvtts_manager_wait")
         m.close()
         closed = True
         th.join(60)

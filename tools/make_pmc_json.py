@@ -7,16 +7,8 @@ import os
 import sys
 from collections import defaultdict
 
-# (kernel symbol prefix, grid size) of each decode-step launch at 32 rows (0.4B dims)
-DECODE = {
-    "gemm_rkv_lora": ("k_gemm2<2, 8, 0, false, 1, 2, false>", 54272),
-    "gemm_ffn_key": ("k_gemm2<2, 8, 0, false, 1, 0, false>", 65536),
-    "gemm_wo": ("k_gemm2<2, 4, 0, false, 1, 0, false>", 32768),
-    "gemm_ffn_value": ("k_gemm2<2, 8, 1, false, 4, 0, false>", 65536),
-    "wkv": ("k_wkv6<false>", 131072),
-    "ln_mix_att": ("k_ln1024<false, 1, 6, 16>", 8192),
-    "ln_mix_ffn": ("k_ln1024<false, 1, 1, 8>", 8192),
-}
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from decode_kernels import DECODE, match  # noqa: E402
 
 
 def load(path, counter):
@@ -34,12 +26,19 @@ w = load(sys.argv[2], "WRITE_SIZE")
 out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, tools/lm_short.py (eager)",
        "correction": "FETCH_SIZE x2 (gfx950 reports half of 16-B/lane streaming reads); values in bytes per launch",
        "kernels": {}}
-for name, key in DECODE.items():
-    if key in f:
-        fb = 2 * 1024 * sum(f[key]) / len(f[key])
-        wb = 1024 * sum(w.get(key, [0.0])) / max(len(w.get(key, [1])), 1)
-        out["kernels"][name] = {"symbol": key[0], "grid": key[1], "launches": len(f[key]),
-                                "fetch_bytes": round(fb), "write_bytes": round(wb), "traffic_bytes": round(fb + wb)}
+for name, (prefixes, grid) in DECODE.items():
+    fv, syms = match(f, prefixes, grid)
+    wv, _ = match(w, prefixes, grid)
+    if not fv:
+        print(f"WARNING: no FETCH_SIZE launches for {name} ({prefixes}, grid {grid})", file=sys.stderr)
+        continue
+    fb = 2 * 1024 * sum(fv) / len(fv)
+    wb = 1024 * sum(wv) / max(len(wv), 1)
+    out["kernels"][name] = {"symbols": syms, "grid": grid, "launches": len(fv),
+                            "fetch_bytes": round(fb), "write_bytes": round(wb), "traffic_bytes": round(fb + wb)}
+missing = [n for n in DECODE if n not in out["kernels"]]
+if missing:
+    print("WARNING: kernels missing from the PMC summary:", missing, file=sys.stderr)
 # ratio to the bench's algorithmic bytes (SURVEY §8d model)
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "rwkv-tts-rs_amd"))
