@@ -136,6 +136,8 @@ class Engine {
   // write-through (sc1) output stores per launch class, same bit order as xmap_mask_, plus
   // bit 6 ln_att, bit 7 ln_ffn
   int wt_mask_ = 0xFF;
+  int ffn_persist_ = 0;     // RWKVTTS_FFN_PERSIST: decode steps' FFN half as one launch (k_ffn_persist)
+  int* ffn_sync_ = nullptr; // its hand-off counters: [L][kFfnSyncInts] (give-up code: d_ctrl_[S_])
   int xalign_mask_ = 4;     // GemmArgs::xalign per class: bit 0 rkv (-> WKV heads), bit 2 ffn key (-> value K-slices)
   int device_ = 0;
   int f16_ = 0;  // fp16 matrices (else bf16): MFMA f16 and f16 activation planes

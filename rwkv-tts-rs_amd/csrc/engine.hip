@@ -98,6 +98,7 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
   if (const char* xm = getenv("RWKVTTS_XMAP_MASK")) xmap_mask_ = (int)strtol(xm, nullptr, 0);
   if (const char* wm = getenv("RWKVTTS_WT_MASK")) wt_mask_ = (int)strtol(wm, nullptr, 0);
   if (const char* xa = getenv("RWKVTTS_XALIGN_MASK")) xalign_mask_ = (int)strtol(xa, nullptr, 0);
+  if (const char* fp = getenv("RWKVTTS_FFN_PERSIST")) ffn_persist_ = atoi(fp);
   if (const char* gp = getenv("RWKVTTS_GEMM_STAMPS")) {
     dbg_gstamp_path_ = gp;
     RT_OK(alloc(&dbg_gstamps_, 2 * 4096 * 4));
@@ -272,13 +273,20 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
   }
   RT_OK(alloc(&partK_, (size_t)splitK_ * Rmax_ * F));
   RT_OK(alloc(&partF_, (size_t)splitF_ * RC));
+  // k_ffn_persist hand-off counters: one block per layer (zeroed here; each launch zeroes the
+  // previous layer's block)
+  RT_OK(alloc(&ffn_sync_, (size_t)Lc * kFfnSyncInts));
+  RT_HIP(hipMemset(ffn_sync_, 0, (size_t)Lc * kFfnSyncInts * sizeof(int)));
   RT_OK(alloc(&vfirst_, RC));
   RT_OK(alloc(&xo_hi_, RC));
   RT_OK(alloc(&xo_lo_, RC));
   RT_OK(alloc(&logits_, (size_t)splitH_ * Rmax_ * Vpad_));
-  RT_OK(alloc(&d_ctrl_, (size_t)S_));
+  // S_ slot control blocks + one block whose first word is the persistent FFN give-up code
+  // (snapshotted with the slots, so a timed-out hand-off fails the unit that ran it)
+  RT_OK(alloc(&d_ctrl_, (size_t)S_ + 1));
+  RT_HIP(hipMemset(d_ctrl_ + S_, 0, sizeof(SlotCtrl)));
   RT_OK(alloc(&d_sem_, (size_t)S_ * RWKVTTS_SEMANTIC_LIMIT));
-  RT_HIP(hipHostMalloc((void**)&h_ctrl_, sizeof(SlotCtrl) * 2 * S_, hipHostMallocDefault));  // 2 snapshots
+  RT_HIP(hipHostMalloc((void**)&h_ctrl_, sizeof(SlotCtrl) * 2 * (S_ + 1), hipHostMallocDefault));  // 2 snapshots
 
   RT_HIP(hipDeviceSynchronize());
   return RWKVTTS_OK;
@@ -580,10 +588,6 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     f.x_lo = xf_lo_;
     f.shift = ffn_sh_;
     f.wt = (wt_mask_ >> 7) & 1;
-    f.tl = tl_next("ln_ffn");
-    prof_begin(&ev);
-    if (!(dbg_exp_ & 0x10000)) launch_ln_mix(f, R, stream_);
-    prof_end("ln_mix_ffn", ev);
     GemmArgs gk{};
     gk.f16 = f16_;
     gk.nseg = 1;
@@ -595,11 +599,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     // key tiles of value K-slice s on the XCD that runs slice s (value xmap: split = xcd + 8 j)
     if ((xalign_mask_ >> 2) & 1) gk.xalign = std::max(1, (F / splitF_) / 64);
     gk.wt = (wt_mask_ >> 2) & 1;
-    prof_begin(&ev);
     gk.exp = dbg_exp_ >> 8;
-    gk.tl = tl_next("gemm_key");
-    if (!(dbg_exp_ & 0x40000)) launch_gemm(gk, stream_);
-    prof_end("gemm_ffn_key", ev);
     GemmArgs gv{};
     gv.f16 = f16_;
     gv.nseg = 1;
@@ -608,10 +608,10 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     gv.xmode = kXRelu2; gv.x_part = partK_; gv.x_nsplit = splitK_; gv.x_ld = F;
     gv.x_part_stride = (int64_t)Rmax_ * F;
     static const bool no_planes = getenv("RWKVTTS_NO_RELU2_PLANES") != nullptr;  // A/B timing switch
-    if (xk_hi_ && R > kPlaneRows && !no_planes) {
+    const bool planes = xk_hi_ && R > kPlaneRows && !no_planes;
+    if (planes) {
       // prefill steps: relu^2 planes once (every value column tile would otherwise re-read the
       // NX f32 key slabs of its K-slice); decode steps keep the fused staging (one launch fewer)
-      launch_relu2_planes(partK_, splitK_, (int64_t)Rmax_ * F, F, F, R, xk_hi_, xk_lo_, stream_);
       gv.seg[0] = {w.ffn_v, xk_hi_, xk_lo_, F, C, 0, 0};
       gv.xmode = kXPlanes;
     }
@@ -619,12 +619,39 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     gv.allow_xmap = (xmap_mask_ >> 3) & 1;
     if (w.quant) { gv.q_fmt = w.quant; gv.qw = w.q_fv; gv.qs = w.s_fv; gv.q_shift = w.qs_fv; }
     gv.wt = (wt_mask_ >> 3) & 1;
-    prof_begin(&ev);
     gv.stamps = (l == 5 && dbg_gstamps_) ? dbg_gstamps_ + 4096 * 4 : nullptr;
     gv.exp = dbg_exp_ >> 8;
-    gv.tl = tl_next("gemm_value");
-    if (!(dbg_exp_ & 0x40000)) launch_gemm(gv, stream_);
-    prof_end("gemm_ffn_value", ev);
+    // decode steps: the whole FFN half as ONE persistent launch (k_ffn_persist, in-launch
+    // hand-offs; bit-identical outputs) where the shapes allow it
+    bool persisted = false;
+    if (ffn_persist_ && inplace && !dbg_exp_ && Lc >= 2) {
+      f.tl = gk.tl = gv.tl = tl_next("ffn_persist");
+      prof_begin(&ev);
+      persisted = launch_ffn_persist(f, gk, gv, ffn_sync_ + (size_t)l * kFfnSyncInts,
+                                     ffn_sync_ + (size_t)((l + Lc - 1) % Lc) * kFfnSyncInts,
+                                     (int*)(d_ctrl_ + S_), R, stream_);
+      if (persisted) {
+        prof_end("ffn_persist", ev);
+      } else if (d_tl_ && tl_n_ > 0) {  // (the timeline slot goes to the three launches below)
+        --tl_n_;
+        if ((int)tl_names_.size() > tl_n_) tl_names_.resize(tl_n_);
+      }
+    }
+    if (!persisted) {
+      f.tl = tl_next("ln_ffn");
+      prof_begin(&ev);
+      if (!(dbg_exp_ & 0x10000)) launch_ln_mix(f, R, stream_);
+      prof_end("ln_mix_ffn", ev);
+      prof_begin(&ev);
+      gk.tl = tl_next("gemm_key");
+      if (!(dbg_exp_ & 0x40000)) launch_gemm(gk, stream_);
+      prof_end("gemm_ffn_key", ev);
+      if (planes) launch_relu2_planes(partK_, splitK_, (int64_t)Rmax_ * F, F, F, R, xk_hi_, xk_lo_, stream_);
+      prof_begin(&ev);
+      gv.tl = tl_next("gemm_value");
+      if (!(dbg_exp_ & 0x40000)) launch_gemm(gv, stream_);
+      prof_end("gemm_ffn_value", ev);
+    }
   }
   if (n_lg > 0) {
     LnMixArgs o{};
@@ -1104,7 +1131,11 @@ int Engine::finish_unit(int b, bool prefill, std::vector<Active>& act, std::vect
   }
   // retire finished slots: every finished slot's tokens copied on the engine's stream (no
   // null-stream sync), one synchronisation, then the jobs are handed back
-  const SlotCtrl* snap = h_ctrl_ + (size_t)b * S_;
+  const SlotCtrl* snap = h_ctrl_ + (size_t)b * (S_ + 1);
+  if (const int code = *(const int*)(snap + S_)) {
+    set_error("persistent FFN launch: a hand-off wait timed out (code " + std::to_string(code) + ")");
+    return RWKVTTS_EHIP;
+  }
   bool copied = false;
   // RWKVTTS_RESULT_COPY_SYNC=1: experiment switch recreating the round-2 result copies
   // (synchronous null-stream hipMemcpy per finished slot; DESIGN §3, the manager hang)
@@ -1358,7 +1389,7 @@ int Engine::serve(JobSource& src) {
       stats.decode_rows += (int64_t)dp.rows.size() * K;
       max_active = std::max<int64_t>(max_active, (int64_t)dp.rows.size());
     }
-    RT_HIP(hipMemcpyAsync(h_ctrl_ + (size_t)b * S_, d_ctrl_, sizeof(SlotCtrl) * S_, hipMemcpyDeviceToHost, stream_));
+    RT_HIP(hipMemcpyAsync(h_ctrl_ + (size_t)b * (S_ + 1), d_ctrl_, sizeof(SlotCtrl) * (S_ + 1), hipMemcpyDeviceToHost, stream_));
     RT_HIP(hipEventRecord(ev1[b], stream_));
     Unit now;
     now.valid = true;

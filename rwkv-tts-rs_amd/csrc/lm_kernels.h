@@ -153,6 +153,11 @@ void launch_embed(const uint32_t* tokens, const int4* rows, const int* ctrl_tok,
 // Launchers return the workgroup count of the launch.
 int launch_ln_mix(const LnMixArgs& a, int n_out_rows, hipStream_t st);
 int launch_gemm(const GemmArgs& a, hipStream_t st);
+// The FFN half of a decode step (LN2 + mix, key GEMM, relu^2, value GEMM) as ONE persistent launch
+// with in-launch hand-offs (k_ffn_persist); false if the shapes are not covered.
+constexpr int kFfnSyncInts = 17 * 64;  // counter block per layer: (1 + 16 K-slices) x 256 B
+bool launch_ffn_persist(const LnMixArgs& ln, const GemmArgs& key, const GemmArgs& val, int* cnt, int* cnt_prev,
+                        int* err, int R, hipStream_t st);
 // Fills a.tw / a.tinfo / a.n_tinfo when the segments' packed weights are contiguous in 64-column
 // tiles and every segment's X is seg[0]'s planes plus a multiple of x_mix_stride; returns whether
 // the table applies (otherwise the kernel looks the segment up).

@@ -287,12 +287,11 @@ __global__ __launch_bounds__(256) void k_ln_mix(LnMixArgs a) {
 // mix vectors) are issued before the row descriptor that addresses the shift state.
 // ------------------------------------------------------------------------------------
 template <bool F16, int MODE, int NMIX, int NP, bool EMB = false>
-__global__ __launch_bounds__(256) void k_ln1024(LnMixArgs a) {
+__device__ __attribute__((always_inline)) void ln1024_body(const LnMixArgs& a, const int out_row) {
   constexpr int C = 1024;
   static_assert(!EMB || (MODE == 1 && NP == 0), "embedding fusion: layer 0's LN + mixes");
   __shared__ float red[16];
   __shared__ __attribute__((aligned(16))) float s_h[EMB ? C : 1];
-  tl_begin(a.tl);
   bf16_t* e_xhi = a.x_hi;
   bf16_t* e_xlo = a.x_lo;
   int64_t e_mix = a.mix_stride;
@@ -305,7 +304,6 @@ __global__ __launch_bounds__(256) void k_ln1024(LnMixArgs a) {
   float* e_shift = a.shift;
   int e_S = a.S, e_L = a.L, e_layer = a.layer, e_inpl = a.inplace;
 
-  const int out_row = blockIdx.x;
   // MODE 1 (LN + mixes) never remaps rows: no dependent row_map load
   const int row = (MODE == 0 && a.row_map) ? a.row_map[out_row] : out_row;
   const int c = 4 * threadIdx.x;
@@ -412,6 +410,12 @@ __global__ __launch_bounds__(256) void k_ln1024(LnMixArgs a) {
       else *(float4_*)(sp + c) = v;
     }
   }
+}
+
+template <bool F16, int MODE, int NMIX, int NP, bool EMB = false>
+__global__ __launch_bounds__(256) void k_ln1024(LnMixArgs a) {
+  tl_begin(a.tl);
+  ln1024_body<F16, MODE, NMIX, NP, EMB>(a, blockIdx.x);
   tl_end(a.tl);
 }
 
@@ -596,8 +600,54 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
 //    latency; in kXRelu2 mode all NX key slabs are in flight at once;
 //  * hi and lo products accumulate in separate MFMA chains (2*MT independent accumulators).
 // ------------------------------------------------------------------------------------
-template <int MT, int KSTEPS, int XMODE, bool F16, int NX, int MS, bool QW = false>
-__global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
+// Inter-workgroup hand-offs of the persistent FFN launch (k_ffn_persist): counters kSyncStride
+// ints (256 B) apart, [0] = LayerNorm rows published, [kSyncStride * (1 + s)] = key workgroups
+// that published their partial slab of value K-slice s.
+constexpr int kSyncStride = 64;
+constexpr int kFfnSlices = 16;  // value K-slices (F / 256 at the 0.4B shape)
+struct FfnSync {
+  int* cnt;          // this layer's counters (zero at launch)
+  int* cnt_prev;     // the counters of the layer launched before this one: zeroed by block 0
+  int* err;          // give-up word: a bounded wait that timed out ORs its code in
+  int n_ln_blocks;   // LayerNorm blocks (rows rounded up to 8: the GEMM blocks keep their XCD order)
+  int ln_rows;       // LayerNorm rows the key workgroups wait for
+  int n_key;         // key workgroups
+  int key_group;     // key column tiles per value K-slice
+  int key_per_slice; // key workgroups per value K-slice (key_group x key splits)
+};
+typedef __attribute__((address_space(1))) int gint_t;
+// one lane polls the counter (relaxed agent-scope load = global_load sc1, s_sleep between polls),
+// bounded by ~50 ms of s_memrealtime; the other waves wait at the barrier. On a timeout the code
+// is ORed into err (the host fails the step) and the workgroup goes on (its output is garbage).
+__device__ inline void sync_wait(const int* c, int target, int* err, int code) {
+  if (threadIdx.x == 0) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load((gint_t*)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 5000000ull) {
+        __hip_atomic_fetch_or((gint_t*)err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+// publish: every wave's write-through (sc1) stores drained, then ONE lane counts the workgroup in
+__device__ inline void sync_arrive(int* c) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add((gint_t*)c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// handed-off bytes are read with sc1 (L1-bypassing) buffer loads only
+__device__ inline u32x4_ ld_sc1_b128(__amdgpu_buffer_rsrc_t r, int off_bytes) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, off_bytes, 0, 16);
+}
+
+// ROLE 0: a plain launch. ROLE 1: key workgroup of k_ffn_persist (weights first, then wait for
+// the LayerNorm rows, X by sc1 loads, publish the partial slab). ROLE 2: value workgroup (weights
+// first, then wait for its K-slice's key slabs, read them by sc1 loads).
+template <int MT, int KSTEPS, int XMODE, bool F16, int NX, int MS, bool QW, int ROLE>
+__device__ __attribute__((always_inline)) void gemm2_body(const GemmArgs& a, const int bx, const FfnSync& sy) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ uint32_t s_rexp[MT * 16];  // f16 relu^2 rows: bits of the row maximum if >= 2^15
   __shared__ float s_qlut[QW ? 16 : 1];  // QW: the NF4 code table
@@ -606,19 +656,18 @@ __global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
   constexpr int ROWS = MT * 16;
   bf16_t* xh = (bf16_t*)smem;
   bf16_t* xl = xh + ROWS * LD;
-  tl_begin(a.tl);
   float* e_out = a.out;
   int64_t e_sstride = a.split_stride;
   int e_ldo = a.ldo, e_M = a.M;
-  int tile = blockIdx.x, split = blockIdx.y;
+  int tile = bx, split = ROLE ? 0 : (int)blockIdx.y;
   if (a.xmap == 2) {  // consumer-aligned 1-D grid (GemmArgs::xalign)
-    const int b = blockIdx.x, xcd = b & 7, j = b >> 3;
+    const int b = bx, xcd = b & 7, j = b >> 3;
     split = j % a.k_split;
     const int lt = j / a.k_split;
     tile = (xcd + 8 * (lt / a.xalign)) * a.xalign + lt % a.xalign;
     if (tile >= a.ntiles) return;  // padding workgroup
   } else if (a.xmap) {  // XCD-aware 1-D grid (GemmArgs::xmap)
-    const int b = blockIdx.x, xcd = b & 7, j = b >> 3;
+    const int b = bx, xcd = b & 7, j = b >> 3;
     if (a.k_split >= 8) {
       split = xcd + 8 * (j / a.ntiles);
       tile = j % a.ntiles;
@@ -696,6 +745,18 @@ __global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
   }
   auto load_x = [&]() {
   if constexpr (XMODE == kXPlanes) {
+    if constexpr (ROLE != 0) {  // handed-off planes: sc1 loads only
+      const auto rh = wt_rsrc(Xhi), rl = wt_rsrc(Xlo);
+#pragma unroll
+      for (int u = 0; u < PERP; ++u) {
+        const int c = threadIdx.x + u * 256;
+        const int r = c / CH, k8 = (c % CH) * 8;
+        const int src = min(xrow0 + r, a.M - 1);
+        const int o = (src * ldx + kbeg + k8) * 2;
+        vh[u] = __builtin_bit_cast(short8, ld_sc1_b128(rh, o));
+        vl[u] = __builtin_bit_cast(short8, ld_sc1_b128(rl, o));
+      }
+    } else {
 #pragma unroll
     for (int u = 0; u < PERP; ++u) {
       const int c = threadIdx.x + u * 256;
@@ -705,7 +766,21 @@ __global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
       vh[u] = *(const short8*)(Xhi + o);
       vl[u] = *(const short8*)(Xlo + o);
     }
+    }
   } else {
+    if constexpr (ROLE != 0) {  // handed-off key slabs: sc1 loads only
+#pragma unroll
+      for (int p = 0; p < NX; ++p) {
+        const auto rp = wt_rsrc(a.x_part + p * a.x_part_stride);
+#pragma unroll
+        for (int u = 0; u < PERR; ++u) {
+          const int c = threadIdx.x + u * 256;
+          const int r = c / (KS / 4), k4 = (c % (KS / 4)) * 4;
+          const int src = min(xrow0 + r, a.M - 1);
+          xr[p][u] = __builtin_bit_cast(float4_, ld_sc1_b128(rp, (src * a.x_ld + kbeg + k4) * 4));
+        }
+      }
+    } else {
 #pragma unroll
     for (int p = 0; p < NX; ++p)
 #pragma unroll
@@ -715,6 +790,7 @@ __global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
         const int src = min(xrow0 + r, a.M - 1);
         xr[p][u] = *(const float4_*)(a.x_part + p * a.x_part_stride + (int64_t)src * a.x_ld + kbeg + k4);
       }
+    }
   }
   };
   auto load_w = [&]() {
@@ -748,8 +824,18 @@ __global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
 #pragma unroll
   for (int t = 0; t < KSTEPS; ++t) b[t] = __builtin_nontemporal_load((const short8*)(wp + t * 512));
   };
-  load_x();
-  load_w();
+  if constexpr (ROLE == 1) {
+    load_w();  // the weight stream does not depend on the LayerNorm: in flight during the wait
+    sync_wait(sy.cnt, sy.ln_rows, sy.err, 1);
+    load_x();
+  } else if constexpr (ROLE == 2) {
+    load_w();
+    sync_wait(sy.cnt + kSyncStride * (1 + split), sy.key_per_slice, sy.err, 2);
+    load_x();
+  } else {
+    load_x();
+    load_w();
+  }
   for (;;) {
   // 3) X -> LDS (rows past M hold a copy of row M-1; their outputs are not stored)
   if constexpr (XMODE == kXPlanes) {
@@ -938,7 +1024,49 @@ __global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
   row0 = rg * ROWS;
   __syncthreads();  // every wave is done with the LDS X image / store staging
   }
+  if constexpr (ROLE == 1) sync_arrive(sy.cnt + kSyncStride * (1 + tile / sy.key_group));
+}
+
+template <int MT, int KSTEPS, int XMODE, bool F16, int NX, int MS, bool QW = false>
+__global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
+  tl_begin(a.tl);
+  gemm2_body<MT, KSTEPS, XMODE, F16, NX, MS, QW, 0>(a, blockIdx.x, FfnSync{});
   tl_end(a.tl);
+}
+
+// ------------------------------------------------------------------------------------
+// ffn_persist: the whole FFN half of a decode step's layer as ONE launch:
+//   blocks [0, n_ln_blocks)            LayerNorm 2 + token-shift mix of row b (k_ln1024's
+//                                      arithmetic), planes / residual / shift stored
+//                                      write-through, then counted into cnt[0];
+//   blocks [+0, +n_key)                key GEMM workgroups (consumer-aligned order): weight
+//                                      fragments requested at dispatch, wait for all LN rows,
+//                                      X planes by sc1 loads, MFMA, partial slab written through,
+//                                      counted into their value K-slice's counter;
+//   blocks [+n_key, +n_key + 256)      value GEMM workgroups (XCD-aware order): weights at
+//                                      dispatch, wait for the K-slice's key slabs, relu^2 staging
+//                                      from sc1 loads, MFMA, partial slab out.
+// Every dependency points to a lower block index, so in-order dispatch keeps every waited-on
+// producer resident or finished (no deadlock with other kernels on the GPU). Every output is the
+// three-launch path's, bit for bit (same bodies, same orders). Block 0 zeroes the counters of
+// the previously launched layer (that launch has finished: stream order).
+// ------------------------------------------------------------------------------------
+template <bool F16>
+__global__ __launch_bounds__(256) void k_ffn_persist(LnMixArgs ln, GemmArgs ka, GemmArgs va, FfnSync sy) {
+  int b = blockIdx.x;
+  tl_begin(ln.tl);
+  if (b < sy.n_ln_blocks) {
+    if (b == 0 && threadIdx.x < 1 + kFfnSlices) sy.cnt_prev[threadIdx.x * kSyncStride] = 0;
+    if (b < sy.ln_rows) {
+      ln1024_body<F16, 1, 1, 8>(ln, b);
+      sync_arrive(sy.cnt);
+    }
+  } else if ((b -= sy.n_ln_blocks) < sy.n_key) {
+    gemm2_body<2, 8, kXPlanes, F16, 1, 0, false, 1>(ka, b, sy);
+  } else {
+    gemm2_body<2, 8, kXRelu2, F16, 4, 0, false, 2>(va, b - sy.n_key, sy);
+  }
+  tl_end(ln.tl);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1278,6 +1406,49 @@ __global__ __launch_bounds__(256) void k_relu2_planes(const float* part, int nx,
 void launch_relu2_planes(const float* part, int nx, int64_t pstride, int ld, int F, int R, bf16_t* hi, bf16_t* lo,
                          hipStream_t st) {
   RT_LAUNCH(k_relu2_planes, dim3((F / 4 + 255) / 256, R), dim3(256), 0, st, part, nx, pstride, ld, F, hi, lo);
+}
+
+// The FFN half of a decode step as one launch (k_ffn_persist); false: a shape it does not cover
+// (the caller runs the three launches). ln / key / val: the three launches' arguments as built by
+// the engine; cnt / cnt_prev: this and the previous layer's counter blocks ((1 + kFfnSlices) x
+// kSyncStride ints, zero before this layer's first use); err: the give-up word.
+bool launch_ffn_persist(const LnMixArgs& ln, const GemmArgs& key, const GemmArgs& val, int* cnt, int* cnt_prev,
+                        int* err, int R, hipStream_t st) {
+  if (ln.C != 1024 || !ln.shift || ln.n_mix != 1 || ln.n_part != 8 || ln.emb || R < 1 || R > 32 ||
+      key.xmode != kXPlanes || val.xmode != kXRelu2 || val.x_nsplit != 4 || key.kslice != 256 ||
+      val.kslice != 256 || key.M != R || val.M != R || key.nseg != 1 || val.nseg != 1 || key.q_fmt || val.q_fmt ||
+      key.stamps || val.stamps || key.exp || val.exp || key.xalign <= 0 || key.f16 != val.f16 || key.f16 != ln.f16 ||
+      cnt == cnt_prev)
+    return false;
+  const int kt = (key.seg[0].N + 63) / 64, vt = (val.seg[0].N + 63) / 64;
+  const int groups = kt / key.xalign;
+  // no padding blocks (every value K-slice gets exactly xalign x k_split producers; key tile t
+  // belongs to K-slice t / xalign), the value grid's XCD order (split = xcd + 8 j) needs
+  // k_split % 8 == 0, and the counters cover kFfnSlices K-slices
+  if (kt % key.xalign || groups % 8 || groups != val.k_split || val.k_split % 8 || val.k_split > kFfnSlices ||
+      key.xalign * 64 != val.kslice)
+    return false;
+  LnMixArgs l = ln;
+  l.n_rows = R;
+  l.wt = 1;
+  GemmArgs ka = key, va = val;
+  ka.xmap = 2; ka.ntiles = kt; ka.wt = 1;
+  va.xmap = 1; va.ntiles = vt;
+  FfnSync sy{};
+  sy.cnt = cnt;
+  sy.cnt_prev = cnt_prev;
+  sy.err = err;
+  sy.n_ln_blocks = 32;  // rows padded to 32 (a multiple of 8: the GEMM blocks keep their XCD order)
+  sy.ln_rows = R;
+  sy.n_key = kt * key.k_split;
+  sy.key_group = key.xalign;
+  sy.key_per_slice = key.xalign * key.k_split;
+  const int nv = vt * val.k_split;
+  const size_t lds = (size_t)2 * 16 * (8 * 32 + 8) * 2 * 2;
+  const dim3 grid(sy.n_ln_blocks + sy.n_key + nv);
+  if (key.f16) RT_LAUNCH((k_ffn_persist<true>), grid, dim3(256), lds, st, l, ka, va, sy);
+  else RT_LAUNCH((k_ffn_persist<false>), grid, dim3(256), lds, st, l, ka, va, sy);
+  return true;
 }
 
 int gemm_ksteps(int kslice) { return kslice / 32; }
