@@ -211,6 +211,8 @@ class Engine {
   bool no_emb_fuse_ = false;  // RWKVTTS_NO_EMB_FUSE at creation: decode steps launch k_embed separately
   uint64_t* dbg_astamps_ = nullptr;  // RWKVTTS_ADV_STAMPS=<file>: k_advance phase stamps, [rows][16]
   std::string dbg_astamp_path_;
+  uint64_t* dbg_fstamps_ = nullptr;  // RWKVTTS_FFN_STAMPS=<file>: layer-5 k_ffn_persist block stamps
+  std::string dbg_fstamp_path_;
   uint64_t* dbg_gstamps_ = nullptr;  // RWKVTTS_GEMM_STAMPS=<file>: layer-5 rkv / ffn_value GEMM stamps
   std::string dbg_gstamp_path_;  // RWKVTTS_DEBUG_EXP: timing experiments (wrong numerics), never in production
   template <typename T>

@@ -103,6 +103,10 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
     dbg_gstamp_path_ = gp;
     RT_OK(alloc(&dbg_gstamps_, 2 * 4096 * 4));
   }
+  if (const char* fs = getenv("RWKVTTS_FFN_STAMPS")) {  // debug: layer-5 k_ffn_persist block stamps
+    dbg_fstamp_path_ = fs;
+    RT_OK(alloc(&dbg_fstamps_, 1024 * 4));
+  }
   if (const char* tp = getenv("RWKVTTS_TIMELINE")) {
     tl_path_ = tp;
     RT_OK(alloc(&d_tl_, (size_t)kTlStride * kTlMax));
@@ -629,7 +633,8 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
       prof_begin(&ev);
       persisted = launch_ffn_persist(f, gk, gv, ffn_sync_ + (size_t)l * kFfnSyncInts,
                                      ffn_sync_ + (size_t)((l + Lc - 1) % Lc) * kFfnSyncInts,
-                                     (int*)(d_ctrl_ + S_), R, stream_);
+                                     (int*)(d_ctrl_ + S_), R, stream_, l == 5 ? dbg_fstamps_ : nullptr,
+                                     ffn_persist_ >> 1);
       if (persisted) {
         prof_end("ffn_persist", ev);
       } else if (d_tl_ && tl_n_ > 0) {  // (the timeline slot goes to the three launches below)
@@ -1446,6 +1451,15 @@ int Engine::dump_stamps() {
     FILE* f = fopen(dbg_astamp_path_.c_str(), "wb");
     if (f) {
       fwrite(ha.data(), 8, ha.size(), f);
+      fclose(f);
+    }
+  }
+  if (dbg_fstamps_) {
+    std::vector<uint64_t> hf(1024 * 4);
+    RT_HIP(hipMemcpy(hf.data(), dbg_fstamps_, hf.size() * 8, hipMemcpyDeviceToHost));
+    FILE* f = fopen(dbg_fstamp_path_.c_str(), "wb");
+    if (f) {
+      fwrite(hf.data(), 8, hf.size(), f);
       fclose(f);
     }
   }

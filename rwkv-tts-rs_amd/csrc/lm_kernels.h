@@ -157,7 +157,7 @@ int launch_gemm(const GemmArgs& a, hipStream_t st);
 // with in-launch hand-offs (k_ffn_persist); false if the shapes are not covered.
 constexpr int kFfnSyncInts = 17 * 64;  // counter block per layer: (1 + 16 K-slices) x 256 B
 bool launch_ffn_persist(const LnMixArgs& ln, const GemmArgs& key, const GemmArgs& val, int* cnt, int* cnt_prev,
-                        int* err, int R, hipStream_t st);
+                        int* err, int R, hipStream_t st, uint64_t* stamps = nullptr, int opts = 0);
 // Fills a.tw / a.tinfo / a.n_tinfo when the segments' packed weights are contiguous in 64-column
 // tiles and every segment's X is seg[0]'s planes plus a multiple of x_mix_stride; returns whether
 // the table applies (otherwise the kernel looks the segment up).

@@ -614,16 +614,25 @@ struct FfnSync {
   int n_key;         // key workgroups
   int key_group;     // key column tiles per value K-slice
   int key_per_slice; // key workgroups per value K-slice (key_group x key splits)
+  int opts;          // bit 0: value workgroups request their weights only once the LN rows are
+                     // published (not at dispatch); bit 1: longer sleep between polls; bit 2: key
+                     // workgroups request their weights after the LN wait (with their X)
+  uint64_t* stamps;  // debug (RWKVTTS_FFN_STAMPS): [block][4] s_memrealtime: start, wait done, work
+                     // done, end (null in production)
 };
+__device__ inline void sync_stamp(const FfnSync& sy, int slot) {
+  if (sy.stamps && threadIdx.x == 0) sy.stamps[blockIdx.x * 4 + slot] = __builtin_amdgcn_s_memrealtime();
+}
 typedef __attribute__((address_space(1))) int gint_t;
 // one lane polls the counter (relaxed agent-scope load = global_load sc1, s_sleep between polls),
 // bounded by ~50 ms of s_memrealtime; the other waves wait at the barrier. On a timeout the code
 // is ORed into err (the host fails the step) and the workgroup goes on (its output is garbage).
-__device__ inline void sync_wait(const int* c, int target, int* err, int code) {
+__device__ inline void sync_wait(const int* c, int target, int* err, int code, int opts = 0) {
   if (threadIdx.x == 0) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while (__hip_atomic_load((gint_t*)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      __builtin_amdgcn_s_sleep(1);
+      if (opts & 2) __builtin_amdgcn_s_sleep(8);
+      else __builtin_amdgcn_s_sleep(1);
       if (__builtin_amdgcn_s_memrealtime() - t0 > 5000000ull) {
         __hip_atomic_fetch_or((gint_t*)err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
@@ -825,12 +834,19 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GemmArgs& a, con
   for (int t = 0; t < KSTEPS; ++t) b[t] = __builtin_nontemporal_load((const short8*)(wp + t * 512));
   };
   if constexpr (ROLE == 1) {
-    load_w();  // the weight stream does not depend on the LayerNorm: in flight during the wait
-    sync_wait(sy.cnt, sy.ln_rows, sy.err, 1);
+    // the weight stream does not depend on the LayerNorm: in flight during the wait (opts bit 2:
+    // requested after it, so the poll is not queued behind the weights and the LN rows' loads do
+    // not compete with them)
+    if (!(sy.opts & 4)) load_w();
+    sync_wait(sy.cnt, sy.ln_rows, sy.err, 1, sy.opts);
+    sync_stamp(sy, 1);
     load_x();
+    if (sy.opts & 4) load_w();
   } else if constexpr (ROLE == 2) {
+    if (sy.opts & 1) sync_wait(sy.cnt, sy.ln_rows, sy.err, 4, sy.opts);  // weights after the LN rows
     load_w();
-    sync_wait(sy.cnt + kSyncStride * (1 + split), sy.key_per_slice, sy.err, 2);
+    sync_wait(sy.cnt + kSyncStride * (1 + split), sy.key_per_slice, sy.err, 2, sy.opts);
+    sync_stamp(sy, 1);
     load_x();
   } else {
     load_x();
@@ -1024,6 +1040,7 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GemmArgs& a, con
   row0 = rg * ROWS;
   __syncthreads();  // every wave is done with the LDS X image / store staging
   }
+  if constexpr (ROLE != 0) sync_stamp(sy, 2);
   if constexpr (ROLE == 1) sync_arrive(sy.cnt + kSyncStride * (1 + tile / sy.key_group));
 }
 
@@ -1055,10 +1072,12 @@ template <bool F16>
 __global__ __launch_bounds__(256) void k_ffn_persist(LnMixArgs ln, GemmArgs ka, GemmArgs va, FfnSync sy) {
   int b = blockIdx.x;
   tl_begin(ln.tl);
+  sync_stamp(sy, 0);
   if (b < sy.n_ln_blocks) {
     if (b == 0 && threadIdx.x < 1 + kFfnSlices) sy.cnt_prev[threadIdx.x * kSyncStride] = 0;
     if (b < sy.ln_rows) {
       ln1024_body<F16, 1, 1, 8>(ln, b);
+      sync_stamp(sy, 2);
       sync_arrive(sy.cnt);
     }
   } else if ((b -= sy.n_ln_blocks) < sy.n_key) {
@@ -1066,6 +1085,7 @@ __global__ __launch_bounds__(256) void k_ffn_persist(LnMixArgs ln, GemmArgs ka, 
   } else {
     gemm2_body<2, 8, kXRelu2, F16, 4, 0, false, 2>(va, b - sy.n_key, sy);
   }
+  sync_stamp(sy, 3);
   tl_end(ln.tl);
 }
 
@@ -1413,7 +1433,7 @@ void launch_relu2_planes(const float* part, int nx, int64_t pstride, int ld, int
 // the engine; cnt / cnt_prev: this and the previous layer's counter blocks ((1 + kFfnSlices) x
 // kSyncStride ints, zero before this layer's first use); err: the give-up word.
 bool launch_ffn_persist(const LnMixArgs& ln, const GemmArgs& key, const GemmArgs& val, int* cnt, int* cnt_prev,
-                        int* err, int R, hipStream_t st) {
+                        int* err, int R, hipStream_t st, uint64_t* stamps, int opts) {
   if (ln.C != 1024 || !ln.shift || ln.n_mix != 1 || ln.n_part != 8 || ln.emb || R < 1 || R > 32 ||
       key.xmode != kXPlanes || val.xmode != kXRelu2 || val.x_nsplit != 4 || key.kslice != 256 ||
       val.kslice != 256 || key.M != R || val.M != R || key.nseg != 1 || val.nseg != 1 || key.q_fmt || val.q_fmt ||
@@ -1443,6 +1463,8 @@ bool launch_ffn_persist(const LnMixArgs& ln, const GemmArgs& key, const GemmArgs
   sy.n_key = kt * key.k_split;
   sy.key_group = key.xalign;
   sy.key_per_slice = key.xalign * key.k_split;
+  sy.stamps = stamps;
+  sy.opts = opts;
   const int nv = vt * val.k_split;
   const size_t lds = (size_t)2 * 16 * (8 * 32 + 8) * 2 * 2;
   const dim3 grid(sy.n_ln_blocks + sy.n_key + nv);

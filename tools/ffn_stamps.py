@@ -1,0 +1,43 @@
+"""k_ffn_persist per-block stamps (RWKVTTS_FFN_STAMPS, layer 5 of the last decode step): per role
+(LayerNorm rows, key workgroups, value workgroups) the min / median / max of each stamp in us
+from the launch's first block start. Usage: ffn_stamps.py [S] (runs 32 requests, S semantic)."""
+import os
+import sys
+import tempfile
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "rwkv-tts-rs_amd"))
+path = os.path.join(tempfile.mkdtemp(), "ffn_stamps.bin")
+os.environ["RWKVTTS_FFN_STAMPS"] = path
+os.environ.setdefault("RWKVTTS_FFN_PERSIST", "1")
+import rwkvtts  # noqa: E402
+from rwkvtts import weights as W  # noqa: E402
+
+S = int(sys.argv[1]) if len(sys.argv) > 1 else 32
+blob = W.synth_blob(W.DIMS_04B, seed=20251205)
+rt = rwkvtts.SharedRwkvRuntime(blob, max_slots=32, token_chunk_size=2048, use_graphs=True)
+reqs = []
+for i in range(32):
+    rs = np.random.RandomState(1000 + i)
+    reqs.append(rwkvtts.TtsBatchRequest(text_tokens=rs.randint(12293, 77822, size=24).tolist(),
+                                        property_tokens=[77823, 77838, 77869, 77845, 77830, 77826],
+                                        args=rwkvtts.SamplerArgs(seed=i), fixed_semantic=S))
+for rep in range(2):
+    rt.generate_batch(reqs)
+    st = rt.stats()
+    print(f"rep {rep}: decode {st['decode_ms'] / max(st['steps'], 1) * 1000:.1f} us/step")
+rt.close()
+a = np.fromfile(path, dtype=np.uint64).reshape(-1, 4).astype(np.float64)
+roles = {"ln": (0, 32), "key": (32, 288), "value": (288, 544)}
+t0 = a[:544, 0][a[:544, 0] > 0].min()
+names = ["start", "wait_done", "work_done", "end"]
+for r, (b, e) in roles.items():
+    x = (a[b:e] - t0) * 0.01  # 100 MHz ticks -> us
+    line = []
+    for k in range(4):
+        v = x[:, k][a[b:e, k] > 0]
+        if v.size:
+            line.append(f"{names[k]} {v.min():6.2f}/{np.median(v):6.2f}/{v.max():6.2f}")
+    print(f"{r:6s} " + "  ".join(line))
