@@ -138,6 +138,8 @@ class Engine {
   int wt_mask_ = 0xFF;
   int ffn_persist_ = 0;     // RWKVTTS_FFN_PERSIST: decode steps' FFN half as one launch (k_ffn_persist)
   int* ffn_sync_ = nullptr; // its hand-off counters: [L][kFfnSyncInts] (give-up code: d_ctrl_[S_])
+  int att_persist_ = 0;     // RWKVTTS_ATT_PERSIST: decode steps' attention half as one launch (k_att_persist)
+  int* att_sync_ = nullptr; // its hand-off counters: [L][kAttSyncInts]
   int xalign_mask_ = 4;     // GemmArgs::xalign per class: bit 0 rkv (-> WKV heads), bit 2 ffn key (-> value K-slices)
   int device_ = 0;
   int f16_ = 0;  // fp16 matrices (else bf16): MFMA f16 and f16 activation planes
@@ -211,6 +213,8 @@ class Engine {
   bool no_emb_fuse_ = false;  // RWKVTTS_NO_EMB_FUSE at creation: decode steps launch k_embed separately
   uint64_t* dbg_astamps_ = nullptr;  // RWKVTTS_ADV_STAMPS=<file>: k_advance phase stamps, [rows][16]
   std::string dbg_astamp_path_;
+  uint64_t* dbg_astamps2_ = nullptr;  // RWKVTTS_ATT_STAMPS=<file>: layer-5 k_att_persist block stamps
+  std::string dbg_astamp2_path_;
   uint64_t* dbg_fstamps_ = nullptr;  // RWKVTTS_FFN_STAMPS=<file>: layer-5 k_ffn_persist block stamps
   std::string dbg_fstamp_path_;
   uint64_t* dbg_gstamps_ = nullptr;  // RWKVTTS_GEMM_STAMPS=<file>: layer-5 rkv / ffn_value GEMM stamps

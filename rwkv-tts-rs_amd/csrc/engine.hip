@@ -99,6 +99,7 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
   if (const char* wm = getenv("RWKVTTS_WT_MASK")) wt_mask_ = (int)strtol(wm, nullptr, 0);
   if (const char* xa = getenv("RWKVTTS_XALIGN_MASK")) xalign_mask_ = (int)strtol(xa, nullptr, 0);
   if (const char* fp = getenv("RWKVTTS_FFN_PERSIST")) ffn_persist_ = atoi(fp);
+  if (const char* ap = getenv("RWKVTTS_ATT_PERSIST")) att_persist_ = atoi(ap);
   if (const char* gp = getenv("RWKVTTS_GEMM_STAMPS")) {
     dbg_gstamp_path_ = gp;
     RT_OK(alloc(&dbg_gstamps_, 2 * 4096 * 4));
@@ -106,6 +107,10 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
   if (const char* fs = getenv("RWKVTTS_FFN_STAMPS")) {  // debug: layer-5 k_ffn_persist block stamps
     dbg_fstamp_path_ = fs;
     RT_OK(alloc(&dbg_fstamps_, 1024 * 4));
+  }
+  if (const char* as = getenv("RWKVTTS_ATT_STAMPS")) {  // debug: layer-5 k_att_persist block stamps
+    dbg_astamp2_path_ = as;
+    RT_OK(alloc(&dbg_astamps2_, 1024 * 4));
   }
   if (const char* tp = getenv("RWKVTTS_TIMELINE")) {
     tl_path_ = tp;
@@ -281,6 +286,8 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
   // previous layer's block)
   RT_OK(alloc(&ffn_sync_, (size_t)Lc * kFfnSyncInts));
   RT_HIP(hipMemset(ffn_sync_, 0, (size_t)Lc * kFfnSyncInts * sizeof(int)));
+  RT_OK(alloc(&att_sync_, (size_t)Lc * kAttSyncInts));  // k_att_persist's, the same scheme
+  RT_HIP(hipMemset(att_sync_, 0, (size_t)Lc * kAttSyncInts * sizeof(int)));
   RT_OK(alloc(&vfirst_, RC));
   RT_OK(alloc(&xo_hi_, RC));
   RT_OK(alloc(&xo_lo_, RC));
@@ -503,11 +510,6 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
       m.ln0_b = ln0_b_;
       m.n_vocab = dims.n_vocab;
     }
-    m.tl = tl_next("ln_att");
-    prof_begin(&ev);
-    if (!(dbg_exp_ & 0x10000))
-      RT_CHECK(launch_ln_mix(m, R, stream_) >= 0, RWKVTTS_EUNSUPPORTED, "layer-0 embedding fusion: unsupported shape");
-    prof_end("ln_mix_att", ev);
     // ---- r, k, v and the LoRA-down projections (w, a, v, g) in one launch (7 segments)
     GemmArgs g{};
     g.f16 = f16_;
@@ -535,12 +537,8 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     g.allow_xmap = xmap_mask_ & 1;
     g.xalign = (xalign_mask_ & 1) ? 1 : 0;  // r / k / v tile h (head h) on the XCD of WKV head h
     g.wt = wt_mask_ & 1;
-    prof_begin(&ev);
     g.stamps = (l == 5 && dbg_gstamps_) ? dbg_gstamps_ : nullptr;
     g.exp = dbg_exp_ >> 8;
-    g.tl = tl_next("gemm_rkv");
-    if (!(dbg_exp_ & 0x40000)) launch_gemm(g, stream_);
-    prof_end("gemm_rkv_lora", ev);
     // ---- WKV + LoRA-up + GroupNorm + bonus + gate
     WkvArgs k{};
     k.f16 = f16_;
@@ -558,10 +556,6 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     k.Dw = dims.d_decay; k.Da = dims.d_aaa; k.Dv = dims.d_mv; k.Dg = dims.d_gate;
     k.stamps = (l == 5) ? dbg_stamps_ : nullptr;
     k.exp = dbg_exp_;
-    k.tl = tl_next("wkv");
-    prof_begin(&ev);
-    if (!(dbg_exp_ & 0x20000)) launch_wkv(k, n_seg, H_, stream_);
-    prof_end("wkv", ev);
     // ---- output projection (split-K partials)
     GemmArgs go{};
     go.f16 = f16_;
@@ -572,11 +566,43 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     go.allow_xmap = (xmap_mask_ >> 1) & 1;
     if (w.quant) { go.q_fmt = w.quant; go.qw = w.q_o; go.qs = w.s_o; go.q_shift = w.qs_o; }
     go.wt = (wt_mask_ >> 1) & 1;
-    prof_begin(&ev);
     go.exp = dbg_exp_ >> 8;
-    go.tl = tl_next("gemm_wo");
-    if (!(dbg_exp_ & 0x40000)) launch_gemm(go, stream_);
-    prof_end("gemm_wo", ev);
+    // decode steps: the attention half as ONE persistent launch (k_att_persist: LN1 + mixes, rkv +
+    // LoRA-down, WKV, Wo with in-launch hand-offs; bit-identical outputs) where the shapes allow it
+    bool att_persisted = false;
+    if (att_persist_ && inplace && !dbg_exp_ && Lc >= 2 && !dbg_stamps_ && !g.stamps) {
+      m.tl = g.tl = k.tl = go.tl = tl_next("att_persist");
+      prof_begin(&ev);
+      att_persisted = launch_att_persist(m, g, k, go, att_sync_ + (size_t)l * kAttSyncInts,
+                                         att_sync_ + (size_t)((l + Lc - 1) % Lc) * kAttSyncInts,
+                                         (int*)(d_ctrl_ + S_), R, H_, stream_, l == 5 ? dbg_astamps2_ : nullptr,
+                                         att_persist_ >> 1);
+      if (att_persisted) {
+        prof_end("att_persist", ev);
+      } else if (d_tl_ && tl_n_ > 0) {
+        --tl_n_;
+        if ((int)tl_names_.size() > tl_n_) tl_names_.resize(tl_n_);
+      }
+    }
+    if (!att_persisted) {
+      m.tl = tl_next("ln_att");
+      prof_begin(&ev);
+      if (!(dbg_exp_ & 0x10000))
+        RT_CHECK(launch_ln_mix(m, R, stream_) >= 0, RWKVTTS_EUNSUPPORTED, "layer-0 embedding fusion: unsupported shape");
+      prof_end("ln_mix_att", ev);
+      g.tl = tl_next("gemm_rkv");
+      prof_begin(&ev);
+      if (!(dbg_exp_ & 0x40000)) launch_gemm(g, stream_);
+      prof_end("gemm_rkv_lora", ev);
+      k.tl = tl_next("wkv");
+      prof_begin(&ev);
+      if (!(dbg_exp_ & 0x20000)) launch_wkv(k, n_seg, H_, stream_);
+      prof_end("wkv", ev);
+      go.tl = tl_next("gemm_wo");
+      prof_begin(&ev);
+      if (!(dbg_exp_ & 0x40000)) launch_gemm(go, stream_);
+      prof_end("gemm_wo", ev);
+    }
     // ---- ffn: residual + Wo partials -> LN2 -> mix
     LnMixArgs f = m;
     f.emb = nullptr;  // (layer 0's embedding fusion belongs to the attention LayerNorm only)
@@ -1451,6 +1477,15 @@ int Engine::dump_stamps() {
     FILE* f = fopen(dbg_astamp_path_.c_str(), "wb");
     if (f) {
       fwrite(ha.data(), 8, ha.size(), f);
+      fclose(f);
+    }
+  }
+  if (dbg_astamps2_) {
+    std::vector<uint64_t> hf(1024 * 4);
+    RT_HIP(hipMemcpy(hf.data(), dbg_astamps2_, hf.size() * 8, hipMemcpyDeviceToHost));
+    FILE* f = fopen(dbg_astamp2_path_.c_str(), "wb");
+    if (f) {
+      fwrite(hf.data(), 8, hf.size(), f);
       fclose(f);
     }
   }

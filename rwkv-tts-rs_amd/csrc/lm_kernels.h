@@ -155,7 +155,12 @@ int launch_ln_mix(const LnMixArgs& a, int n_out_rows, hipStream_t st);
 int launch_gemm(const GemmArgs& a, hipStream_t st);
 // The FFN half of a decode step (LN2 + mix, key GEMM, relu^2, value GEMM) as ONE persistent launch
 // with in-launch hand-offs (k_ffn_persist); false if the shapes are not covered.
-constexpr int kFfnSyncInts = 17 * 64;  // counter block per layer: (1 + 16 K-slices) x 256 B
+constexpr int kFfnSyncInts = 24 * 64;  // counter block per layer: (8 LN replicas + 16 K-slices) x 256 B
+// The attention half of a decode step (LN1 + mixes, rkv + LoRA-down, WKV, Wo) as ONE persistent
+// launch (k_att_persist); false if the shapes are not covered.
+constexpr int kAttSyncInts = 48 * 64;  // counter block per layer (lm_kernels.hip kAtt*)
+bool launch_att_persist(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs& wkv, const GemmArgs& wo, int* cnt,
+                        int* cnt_prev, int* err, int R, int H, hipStream_t st, uint64_t* stamps, int opts);
 bool launch_ffn_persist(const LnMixArgs& ln, const GemmArgs& key, const GemmArgs& val, int* cnt, int* cnt_prev,
                         int* err, int R, hipStream_t st, uint64_t* stamps = nullptr, int opts = 0);
 // Fills a.tw / a.tinfo / a.n_tinfo when the segments' packed weights are contiguous in 64-column

@@ -601,19 +601,34 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
 //  * hi and lo products accumulate in separate MFMA chains (2*MT independent accumulators).
 // ------------------------------------------------------------------------------------
 // Inter-workgroup hand-offs of the persistent FFN launch (k_ffn_persist): counters kSyncStride
-// ints (256 B) apart, [0] = LayerNorm rows published, [kSyncStride * (1 + s)] = key workgroups
-// that published their partial slab of value K-slice s.
+// ints (256 B) apart, [kSyncStride * r] (r < kLnReplicas) = LayerNorm rows published (one replica
+// per XCD: every LN workgroup adds to all of them, a key workgroup polls replica blockIdx % 8, so
+// 512 pollers do not share one line), [kSyncStride * (kLnReplicas + s)] = key workgroups that
+// published their partial slab of value K-slice s.
 constexpr int kSyncStride = 64;
+constexpr int kLnReplicas = 8;
 constexpr int kFfnSlices = 16;  // value K-slices (F / 256 at the 0.4B shape)
-struct FfnSync {
+// counter blocks (kSyncStride-int units) of the persistent attention launch (k_att_persist)
+constexpr int kAttLn = 0;      // kLnReplicas: LayerNorm rows published
+constexpr int kAttHead = 8;    // 16: head h's r / k / v tiles published (3 tiles x the K-splits)
+constexpr int kAttLora = 24;   // kLnReplicas: the LoRA-down tiles published
+constexpr int kAttWkv = 32;    // 16: WKV workgroups of head h done (one per row)
+constexpr int kAttCounters = 48;
+struct FfnSync {     // (both persistent launches)
   int* cnt;          // this layer's counters (zero at launch)
   int* cnt_prev;     // the counters of the layer launched before this one: zeroed by block 0
+  int n_prev;        // counters to zero there
   int* err;          // give-up word: a bounded wait that timed out ORs its code in
   int n_ln_blocks;   // LayerNorm blocks (rows rounded up to 8: the GEMM blocks keep their XCD order)
-  int ln_rows;       // LayerNorm rows the key workgroups wait for
-  int n_key;         // key workgroups
-  int key_group;     // key column tiles per value K-slice
-  int key_per_slice; // key workgroups per value K-slice (key_group x key splits)
+  int ln_rows;       // LayerNorm rows the GEMM workgroups wait for
+  int n_key;         // FFN: key workgroups; attention: rkv workgroups
+  int key_group;     // FFN: key column tiles per value K-slice
+  int key_per_slice; // FFN: key workgroups per value K-slice (key_group x key splits)
+  int n_wkv;         // attention: WKV workgroups
+  int rkv_tiles;     // attention: column tiles of the rkv launch (its grid is tiles x splits)
+  int head_target;   // attention: rkv workgroups per head (3 tiles x splits)
+  int lora_target;   // attention: LoRA-down workgroups (tiles x splits)
+  int C;             // attention: channels (r / k / v columns [0, 3C), LoRA-down beyond)
   int opts;          // bit 0: value workgroups request their weights only once the LN rows are
                      // published (not at dispatch); bit 1: longer sleep between polls; bit 2: key
                      // workgroups request their weights after the LN wait (with their X)
@@ -642,10 +657,12 @@ __device__ inline void sync_wait(const int* c, int target, int* err, int code, i
   __syncthreads();
 }
 // publish: every wave's write-through (sc1) stores drained, then ONE lane counts the workgroup in
-__device__ inline void sync_arrive(int* c) {
+// (replicas > 1: lanes 0..replicas-1 of wave 0 add to one replica each, kSyncStride ints apart)
+__device__ inline void sync_arrive(int* c, int replicas = 1) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_fetch_add((gint_t*)c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x < replicas)
+    __hip_atomic_fetch_add((gint_t*)(c + threadIdx.x * kSyncStride), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // handed-off bytes are read with sc1 (L1-bypassing) buffer loads only
 __device__ inline u32x4_ ld_sc1_b128(__amdgpu_buffer_rsrc_t r, int off_bytes) {
@@ -654,9 +671,13 @@ __device__ inline u32x4_ ld_sc1_b128(__amdgpu_buffer_rsrc_t r, int off_bytes) {
 
 // ROLE 0: a plain launch. ROLE 1: key workgroup of k_ffn_persist (weights first, then wait for
 // the LayerNorm rows, X by sc1 loads, publish the partial slab). ROLE 2: value workgroup (weights
-// first, then wait for its K-slice's key slabs, read them by sc1 loads).
+// first, then wait for its K-slice's key slabs, read them by sc1 loads). ROLE 3: rkv workgroup of
+// k_att_persist (as ROLE 1; publishes to its head's counter, or the LoRA-down counter). ROLE 4:
+// Wo workgroup (weights first, then wait for the WKV workgroups of its K-slice's two heads).
+// by: the split index of an xmap-0 grid (blockIdx.y for a plain launch).
 template <int MT, int KSTEPS, int XMODE, bool F16, int NX, int MS, bool QW, int ROLE>
-__device__ __attribute__((always_inline)) void gemm2_body(const GemmArgs& a, const int bx, const FfnSync& sy) {
+__device__ __attribute__((always_inline)) void gemm2_body(const GemmArgs& a, const int bx, const int by,
+                                                          const FfnSync& sy) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ uint32_t s_rexp[MT * 16];  // f16 relu^2 rows: bits of the row maximum if >= 2^15
   __shared__ float s_qlut[QW ? 16 : 1];  // QW: the NF4 code table
@@ -668,7 +689,7 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GemmArgs& a, con
   float* e_out = a.out;
   int64_t e_sstride = a.split_stride;
   int e_ldo = a.ldo, e_M = a.M;
-  int tile = bx, split = ROLE ? 0 : (int)blockIdx.y;
+  int tile = bx, split = by;
   if (a.xmap == 2) {  // consumer-aligned 1-D grid (GemmArgs::xalign)
     const int b = bx, xcd = b & 7, j = b >> 3;
     split = j % a.k_split;
@@ -833,19 +854,26 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GemmArgs& a, con
 #pragma unroll
   for (int t = 0; t < KSTEPS; ++t) b[t] = __builtin_nontemporal_load((const short8*)(wp + t * 512));
   };
-  if constexpr (ROLE == 1) {
+  if constexpr (ROLE == 1 || ROLE == 3) {
     // the weight stream does not depend on the LayerNorm: in flight during the wait (opts bit 2:
     // requested after it, so the poll is not queued behind the weights and the LN rows' loads do
     // not compete with them)
     if (!(sy.opts & 4)) load_w();
-    sync_wait(sy.cnt, sy.ln_rows, sy.err, 1, sy.opts);
+    sync_wait(sy.cnt + kSyncStride * (blockIdx.x & (kLnReplicas - 1)), sy.ln_rows, sy.err, 1, sy.opts);
     sync_stamp(sy, 1);
     load_x();
     if (sy.opts & 4) load_w();
-  } else if constexpr (ROLE == 2) {
-    if (sy.opts & 1) sync_wait(sy.cnt, sy.ln_rows, sy.err, 4, sy.opts);  // weights after the LN rows
+  } else if constexpr (ROLE == 4) {
     load_w();
-    sync_wait(sy.cnt + kSyncStride * (1 + split), sy.key_per_slice, sy.err, 2, sy.opts);
+    const int h0 = kbeg >> 6;  // the K-slice's first head (64 channels per head)
+    for (int hh = h0; hh < h0 + (KS >> 6); ++hh) sync_wait(sy.cnt + kSyncStride * (kAttWkv + hh), sy.ln_rows, sy.err, 8, sy.opts);
+    sync_stamp(sy, 1);
+    load_x();
+  } else if constexpr (ROLE == 2) {
+    if (sy.opts & 1)  // weights after the LN rows
+      sync_wait(sy.cnt + kSyncStride * (blockIdx.x & (kLnReplicas - 1)), sy.ln_rows, sy.err, 4, sy.opts);
+    load_w();
+    sync_wait(sy.cnt + kSyncStride * (kLnReplicas + split), sy.key_per_slice, sy.err, 2, sy.opts);
     sync_stamp(sy, 1);
     load_x();
   } else {
@@ -1041,13 +1069,18 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GemmArgs& a, con
   __syncthreads();  // every wave is done with the LDS X image / store staging
   }
   if constexpr (ROLE != 0) sync_stamp(sy, 2);
-  if constexpr (ROLE == 1) sync_arrive(sy.cnt + kSyncStride * (1 + tile / sy.key_group));
+  if constexpr (ROLE == 1) sync_arrive(sy.cnt + kSyncStride * (kLnReplicas + tile / sy.key_group));
+  if constexpr (ROLE == 3) {
+    const int c0 = col_off + (tile - tstart) * 64;  // this tile's first output column
+    if (c0 < 3 * sy.C) sync_arrive(sy.cnt + kSyncStride * (kAttHead + ((c0 % sy.C) >> 6)));
+    else sync_arrive(sy.cnt + kSyncStride * kAttLora, kLnReplicas);
+  }
 }
 
 template <int MT, int KSTEPS, int XMODE, bool F16, int NX, int MS, bool QW = false>
 __global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
   tl_begin(a.tl);
-  gemm2_body<MT, KSTEPS, XMODE, F16, NX, MS, QW, 0>(a, blockIdx.x, FfnSync{});
+  gemm2_body<MT, KSTEPS, XMODE, F16, NX, MS, QW, 0>(a, blockIdx.x, blockIdx.y, FfnSync{});
   tl_end(a.tl);
 }
 
@@ -1069,21 +1102,21 @@ __global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
 // the previously launched layer (that launch has finished: stream order).
 // ------------------------------------------------------------------------------------
 template <bool F16>
-__global__ __launch_bounds__(256) void k_ffn_persist(LnMixArgs ln, GemmArgs ka, GemmArgs va, FfnSync sy) {
+__global__ __launch_bounds__(256, 2) void k_ffn_persist(LnMixArgs ln, GemmArgs ka, GemmArgs va, FfnSync sy) {
   int b = blockIdx.x;
   tl_begin(ln.tl);
   sync_stamp(sy, 0);
   if (b < sy.n_ln_blocks) {
-    if (b == 0 && threadIdx.x < 1 + kFfnSlices) sy.cnt_prev[threadIdx.x * kSyncStride] = 0;
+    if (b == 0 && threadIdx.x < sy.n_prev) sy.cnt_prev[threadIdx.x * kSyncStride] = 0;
     if (b < sy.ln_rows) {
       ln1024_body<F16, 1, 1, 8>(ln, b);
       sync_stamp(sy, 2);
-      sync_arrive(sy.cnt);
+      sync_arrive(sy.cnt, kLnReplicas);
     }
   } else if ((b -= sy.n_ln_blocks) < sy.n_key) {
-    gemm2_body<2, 8, kXPlanes, F16, 1, 0, false, 1>(ka, b, sy);
+    gemm2_body<2, 8, kXPlanes, F16, 1, 0, false, 1>(ka, b, 0, sy);
   } else {
-    gemm2_body<2, 8, kXRelu2, F16, 4, 0, false, 2>(va, b - sy.n_key, sy);
+    gemm2_body<2, 8, kXRelu2, F16, 4, 0, false, 2>(va, b - sy.n_key, 0, sy);
   }
   sync_stamp(sy, 3);
   tl_end(ln.tl);
@@ -1465,6 +1498,7 @@ bool launch_ffn_persist(const LnMixArgs& ln, const GemmArgs& key, const GemmArgs
   sy.key_per_slice = key.xalign * key.k_split;
   sy.stamps = stamps;
   sy.opts = opts;
+  sy.n_prev = kLnReplicas + kFfnSlices;
   const int nv = vt * val.k_split;
   const size_t lds = (size_t)2 * 16 * (8 * 32 + 8) * 2 * 2;
   const dim3 grid(sy.n_ln_blocks + sy.n_key + nv);
@@ -2100,21 +2134,27 @@ __global__ __launch_bounds__(128) void k_wkv4(WkvArgs a) {
 // State blocks: thread t's q-th float4 at float4 index q * 256 + t (engine.hip perm_index,
 // layout 2); LoRA-up rows: entry u of thread t at uint4 index u * 256 + t (launch_pack_lora6).
 // ------------------------------------------------------------------------------------
-template <bool F16, bool MULTI_ROW = false>  // MULTI_ROW: the same code, a distinct symbol for prefill steps
-__global__ __launch_bounds__(256) void k_wkv6(WkvArgs a) {
+// ROLE 0: a plain launch. ROLE 1: WKV workgroup of k_att_persist (decode rows only): the LoRA-up
+// rows and the state (independent of this layer's rkv launch) are requested at dispatch, then
+// the workgroup waits for its head's r / k / v tiles and the LoRA-down tiles, reads the partials
+// by sc1 loads, and publishes its z row (staged in LDS, stored write-through by one wave) to
+// its head's counter.
+template <bool F16, int ROLE>
+__device__ __attribute__((always_inline)) void wkv6_body(const WkvArgs& a, const int bx, const int by,
+                                                         const FfnSync& sy) {
   constexpr int N = 64, DW = 64, DA = 64, DV = 32, DG = 128, DALL = DW + DA + DV + DG, NP = 4;
+  __shared__ __attribute__((aligned(16))) float s_z[ROLE ? N : 1];
   __shared__ __attribute__((aligned(16))) float s_hid[DALL];
   __shared__ __attribute__((aligned(16))) float s_vec[5][N];  // w, kk (unnormalised), a, k, r
   __shared__ float s_red[4][4];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, i = t >> 2, qq = t & 3;
-  int seg_i = blockIdx.x, h = blockIdx.y;
+  int seg_i = bx, h = by;
   if (a.xmap) {  // 1-D grid: head h's workgroups share one XCD (its LoRA-up rows stay in one L2)
-    const int b = blockIdx.x, xcd = b & 7, j = b >> 3;
+    const int b = bx, xcd = b & 7, j = b >> 3;
     h = xcd + 8 * (j / a.n_seg);
     seg_i = j % a.n_seg;
   }
   const int C = a.C, c = h * N + i;
-  tl_begin(a.tl);
   // debug phase stamps (as k_wkv4: RWKVTTS_WKV_STAMPS, layer 5 only; null in production)
   uint64_t* stp = (a.stamps && t == 0) ? a.stamps + ((int64_t)h * a.n_seg + seg_i) * 8 : nullptr;
   if (stp) { stp[0] = __builtin_amdgcn_s_memrealtime(); stp[1] = __builtin_amdgcn_s_memtime(); }
@@ -2134,6 +2174,16 @@ __global__ __launch_bounds__(256) void k_wkv6(WkvArgs a) {
   float rp[NP], kp[NP], vp[NP], vf = 0.f;
   auto load_parts = [&](int row) {
     const float* prow = a.part + (int64_t)row * a.ldp;
+    if constexpr (ROLE == 1) {  // handed-off partial slabs: sc1 loads only
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+        const auto rs = wt_rsrc(prow + p * a.part_stride);
+        hp[p] = __builtin_bit_cast(float4_, ld_sc1_b128(rs, (3 * C + (hid_thread ? 4 * t : 0)) * 4));
+        rp[p] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, c * 4, 0, 16));
+        kp[p] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, (C + c) * 4, 0, 16));
+        vp[p] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, (2 * C + c) * 4, 0, 16));
+      }
+    } else {
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
       const float* pp = prow + p * a.part_stride;
@@ -2142,19 +2192,35 @@ __global__ __launch_bounds__(256) void k_wkv6(WkvArgs a) {
       kp[p] = pp[C + c];
       vp[p] = pp[2 * C + c];
     }
+    }
     vf = a.layer > 0 ? a.v_first[(int64_t)row * a.ldv + c] : 0.f;
   };
   // issue order = need order (vmcnt retires in order): partials (hidden nonlinearity), then the
   // LoRA-up rows (LoRA / mixing phase), then the state (update phase)
   uint4 lw[9];  // 8 bf16 per entry: w 0..1 | a 2..3 | v 4 | g 5..8
   const uint4* pl = (const uint4*)(a.lup + (int64_t)h * 9 * 256 * 8);
+  int slot, r_begin, n_rows;
+  if constexpr (ROLE == 1) {
+    // LoRA-up rows and the state first (they do not depend on this layer's rkv workgroups), then
+    // wait for the head's r / k / v tiles and the LoRA-down tiles, then their partials
+    slot = sg.x; r_begin = sg.y; n_rows = sg.z;
+#pragma unroll
+    for (int u = 0; u < 9; ++u) lw[u] = pl[u * 256 + t];
+    load_state(slot);
+    sync_wait(sy.cnt + kSyncStride * (kAttHead + h), sy.head_target, sy.err, 16, sy.opts);
+    sync_wait(sy.cnt + kSyncStride * (kAttLora + (blockIdx.x & (kLnReplicas - 1))), sy.lora_target, sy.err, 32,
+              sy.opts);
+    sync_stamp(sy, 1);
+    load_parts(r_begin);
+  } else {
   load_parts(spec);
 #pragma unroll
   for (int u = 0; u < 9; ++u) lw[u] = pl[u * 256 + t];
   load_state(spec);
-  const int slot = sg.x, r_begin = sg.y, n_rows = sg.z;
+  slot = sg.x; r_begin = sg.y; n_rows = sg.z;
   if (r_begin != spec) load_parts(r_begin);
   if (slot != spec) load_state(slot);
+  }
   float4_* Srow = (float4_*)(a.state + (int64_t)slot * a.slot_stride + soff);
   auto quad_sum = [](float x) {
     x += dpp_mov<0xB1>(x);
@@ -2281,14 +2347,138 @@ __global__ __launch_bounds__(256) void k_wkv6(WkvArgs a) {
     const float mean = ((s_red[2][0] + s_red[2][1]) + (s_red[2][2] + s_red[2][3])) * (1.0f / N);
     const float var =
         fmaxf(((s_red[3][0] + s_red[3][1]) + (s_red[3][2] + s_red[3][3])) * (1.0f / N) - mean * mean, 0.f);
+    if constexpr (ROLE == 1) {
+      // the row's 64 z values through LDS; wave 0's lanes 0..15 store 4 channels each as one 8-byte
+      // write-through store per plane (split as split_store does: the same bits)
+      if (qq == 0) {
+        const float gn = (y - mean) * __builtin_amdgcn_rsqf(var + 64e-5f) * lnw + lnb;
+        s_z[i] = (gn + bonus * v) * lo3;
+      }
+      __syncthreads();
+      if (t < 16) {
+        const float4_ z4 = *(const float4_*)(s_z + 4 * t);
+        uint16_t hh[4], ll[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          hh[e] = f32_to_w16(z4[e], F16);
+          ll[e] = f32_to_w16(z4[e] - w16_to_f32(hh[e], F16), F16);
+        }
+        const int64_t zo = ((int64_t)row * a.ldz + h * N + 4 * t) * 2;
+        store_wt(wt_rsrc(a.z_hi), (int)zo, make_uint2(hh[0] | ((uint32_t)hh[1] << 16), hh[2] | ((uint32_t)hh[3] << 16)));
+        store_wt(wt_rsrc(a.z_lo), (int)zo, make_uint2(ll[0] | ((uint32_t)ll[1] << 16), ll[2] | ((uint32_t)ll[3] << 16)));
+      }
+    } else {
     if (qq == 0) {
       const float gn = (y - mean) * __builtin_amdgcn_rsqf(var + 64e-5f) * lnw + lnb;
       split_store((gn + bonus * v) * lo3, a.z_hi, a.z_lo, (int64_t)row * a.ldz + c, F16);
     }
+    }
     if (rr + 1 < n_rows) __syncthreads();
   }
   if (stp) { stp[6] = __builtin_amdgcn_s_memtime(); stp[7] = __builtin_amdgcn_s_memrealtime(); }
+  if constexpr (ROLE == 1) {
+    sync_stamp(sy, 2);
+    sync_arrive(sy.cnt + kSyncStride * (kAttWkv + h));
+  }
+}
+
+template <bool F16, bool MULTI_ROW = false>  // MULTI_ROW: the same code, a distinct symbol for prefill steps
+__global__ __launch_bounds__(256) void k_wkv6(WkvArgs a) {
+  tl_begin(a.tl);
+  wkv6_body<F16, 0>(a, blockIdx.x, blockIdx.y, FfnSync{});
   tl_end(a.tl);
+}
+
+// ------------------------------------------------------------------------------------
+// att_persist: the attention half of a decode step's layer as ONE launch:
+//   blocks [0, n_ln_blocks)        LayerNorm 1 + six token-shift mixes of row b (k_ln1024's
+//                                  arithmetic; layer 0 with the embedding folded in), planes /
+//                                  residual / shift written through, counted into the LN replicas;
+//   blocks [+0, +n_key)            rkv + LoRA-down workgroups (tile = b % tiles, split = b / tiles):
+//                                  weights at dispatch, wait for the LN rows, X planes by sc1
+//                                  loads, MFMA, partial slab written through, counted into their
+//                                  head's counter (r / k / v tiles) or the LoRA-down replicas;
+//   blocks [+n_key, +n_wkv)        WKV workgroups (slot, head; head h on one XCD): LoRA-up rows and
+//                                  state at dispatch, wait for the head's tiles and the LoRA-down
+//                                  tiles, partials by sc1 loads, z row written through, counted
+//                                  into the head's WKV counter;
+//   blocks [+n_wkv, +n_wo)         Wo workgroups (XCD-aware): weights at dispatch, wait for the
+//                                  WKV workgroups of their K-slice's two heads, z by sc1 loads.
+// Dependencies point to lower block indices only (see k_ffn_persist); outputs are the four
+// launches', bit for bit. Block 0 zeroes the previous layer's counters.
+// ------------------------------------------------------------------------------------
+template <bool F16, bool EMB>
+__global__ __launch_bounds__(256, 2) void k_att_persist(LnMixArgs ln, GemmArgs ga, WkvArgs wa, GemmArgs go, FfnSync sy) {
+  int b = blockIdx.x;
+  tl_begin(ln.tl);
+  sync_stamp(sy, 0);
+  if (b < sy.n_ln_blocks) {
+    if (b == 0 && threadIdx.x < sy.n_prev) sy.cnt_prev[threadIdx.x * kSyncStride] = 0;
+    if (b < sy.ln_rows) {
+      if constexpr (EMB) ln1024_body<F16, 1, 6, 0, true>(ln, b);
+      else ln1024_body<F16, 1, 6, 16>(ln, b);
+      sync_stamp(sy, 2);
+      sync_arrive(sy.cnt + kSyncStride * kAttLn, kLnReplicas);
+    }
+  } else if ((b -= sy.n_ln_blocks) < sy.n_key) {
+    gemm2_body<2, 8, kXPlanes, F16, 1, 2, false, 3>(ga, b % sy.rkv_tiles, b / sy.rkv_tiles, sy);
+  } else if ((b -= sy.n_key) < sy.n_wkv) {
+    wkv6_body<F16, 1>(wa, b, 0, sy);
+  } else {
+    gemm2_body<2, 4, kXPlanes, F16, 1, 0, false, 4>(go, b - sy.n_wkv, 0, sy);
+  }
+  sync_stamp(sy, 3);
+  tl_end(ln.tl);
+}
+
+bool launch_att_persist(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs& wkv, const GemmArgs& wo, int* cnt,
+                        int* cnt_prev, int* err, int R, int H, hipStream_t st, uint64_t* stamps, int opts) {
+  const bool emb = ln.emb != nullptr;
+  const int rkv_tiles = rkv.seg[rkv.nseg - 1].tile_start + (rkv.seg[rkv.nseg - 1].N + 63) / 64;
+  const int lora_tiles = rkv_tiles - 3 * ln.C / 64;
+  if (ln.C != 1024 || H != 16 || !ln.shift || ln.n_mix != 6 || ln.n_part != (emb ? 0 : 16) || R < 1 || R > 32 ||
+      rkv.xmode != kXPlanes || rkv.n_tinfo != rkv_tiles || rkv.kslice != 256 || rkv.k_split != 4 || rkv.M != R ||
+      rkv.q_fmt || rkv.stamps || rkv.exp || rkv.xalign || lora_tiles < 1 || rkv.ldo != wkv.ldp ||
+      wkv.perm != 2 || wkv.n_part != 4 || wkv.multi_row || !wkv.allow_xmap || wkv.n_seg != R || wkv.stamps ||
+      wkv.exp || wkv.Dw != 64 || wkv.Da != 64 || wkv.Dv != 32 || wkv.Dg != 128 ||
+      wo.xmode != kXPlanes || wo.kslice != 128 || wo.k_split != 8 || wo.nseg != 1 || wo.M != R || wo.q_fmt ||
+      wo.stamps || wo.exp || (wo.seg[0].N + 63) / 64 != 16 ||
+      rkv.f16 != ln.f16 || wo.f16 != ln.f16 || wkv.f16 != ln.f16 || cnt == cnt_prev)
+    return false;
+  LnMixArgs l = ln;
+  l.n_rows = R;
+  l.wt = 1;
+  GemmArgs ga = rkv, gw = wo;
+  ga.xmap = 0; ga.ntiles = rkv_tiles; ga.wt = 1;
+  gw.xmap = 1; gw.ntiles = 16;
+  WkvArgs wa = wkv;
+  wa.xmap = 1; wa.wt = 1;
+  FfnSync sy{};
+  sy.cnt = cnt;
+  sy.cnt_prev = cnt_prev;
+  sy.n_prev = kAttCounters;
+  sy.err = err;
+  sy.n_ln_blocks = 32;
+  sy.ln_rows = R;
+  sy.n_key = rkv_tiles * rkv.k_split;
+  sy.rkv_tiles = rkv_tiles;
+  sy.n_wkv = R * H;
+  sy.head_target = 3 * rkv.k_split;
+  sy.lora_target = lora_tiles * rkv.k_split;
+  sy.C = ln.C;
+  sy.opts = opts;
+  sy.stamps = stamps;
+  const int n_wo = 16 * wo.k_split;
+  const size_t lds = (size_t)2 * 16 * (8 * 32 + 8) * 2 * 2;  // the rkv body's X image (the largest)
+  const dim3 grid(sy.n_ln_blocks + sy.n_key + sy.n_wkv + n_wo);
+  if (ln.f16) {
+    if (emb) RT_LAUNCH((k_att_persist<true, true>), grid, dim3(256), lds, st, l, ga, wa, gw, sy);
+    else RT_LAUNCH((k_att_persist<true, false>), grid, dim3(256), lds, st, l, ga, wa, gw, sy);
+  } else {
+    if (emb) RT_LAUNCH((k_att_persist<false, true>), grid, dim3(256), lds, st, l, ga, wa, gw, sy);
+    else RT_LAUNCH((k_att_persist<false, false>), grid, dim3(256), lds, st, l, ga, wa, gw, sy);
+  }
+  return true;
 }
 
 int wkv_perm_layout(int Dw, int Da, int Dv, int Dg, int n_part, int max_slots, int variant) {

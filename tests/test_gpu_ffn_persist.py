@@ -1,9 +1,11 @@
-"""The decode step's FFN half as ONE persistent launch (csrc/lm_kernels.hip k_ffn_persist:
-LayerNorm 2 + mix, key GEMM, relu^2, value GEMM with in-launch write-through hand-offs) against
-the three-launch path it replaces: the same bodies and reduction orders, so token streams must be
+"""The decode step's two halves as persistent launches (csrc/lm_kernels.hip k_ffn_persist: LayerNorm
+2 + mix, key GEMM, relu^2, value GEMM; k_att_persist: LayerNorm 1 + six mixes (layer 0 with the
+embedding folded in), rkv + LoRA-down, WKV, Wo -- with in-launch write-through hand-offs) against
+the launches they replace: the same bodies and reduction orders, so token streams must be
 identical bit for bit -- at the bench shape (32 slots, 0.4B bf16, graph replay), with fewer rows
-than slots (R < 32: padded LayerNorm blocks), eager launches, the fp16 model, and against the
-oracle. RWKVTTS_FFN_PERSIST is read when an engine is created."""
+than slots (R < 32: padded LayerNorm blocks), eager launches, the fp16 model, two engines on one
+GPU, and against the oracle. RWKVTTS_FFN_PERSIST / RWKVTTS_ATT_PERSIST are read when an engine
+is created (0 = the separate launches)."""
 import os
 
 import numpy as np
@@ -16,21 +18,40 @@ from helpers import make_request, synth_text, to_struct
 pytestmark = pytest.mark.gpu
 
 
-def _runtime(blob, persist, **kw):
-    old = os.environ.get("RWKVTTS_FFN_PERSIST")
-    os.environ["RWKVTTS_FFN_PERSIST"] = "1" if persist else "0"
-    try:
+MODES = {"off": {"RWKVTTS_FFN_PERSIST": "0", "RWKVTTS_ATT_PERSIST": "0"},
+         "ffn": {"RWKVTTS_FFN_PERSIST": "5", "RWKVTTS_ATT_PERSIST": "0"},
+         "att": {"RWKVTTS_FFN_PERSIST": "0", "RWKVTTS_ATT_PERSIST": "5"},
+         "both": {"RWKVTTS_FFN_PERSIST": "5", "RWKVTTS_ATT_PERSIST": "5"}}
+
+
+class _env:
+    def __init__(self, kv):
+        self.kv = kv
+
+    def __enter__(self):
+        self.old = {k: os.environ.get(k) for k in self.kv}
+        os.environ.update(self.kv)
+
+    def __exit__(self, *a):
+        for k, v in self.old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def _runtime(blob, mode, **kw):
+    if mode is True:
+        mode = "both"
+    elif mode is False:
+        mode = "off"
+    with _env(MODES[mode]):
         return rwkvtts.SharedRwkvRuntime(blob, **kw)
-    finally:
-        if old is None:
-            os.environ.pop("RWKVTTS_FFN_PERSIST", None)
-        else:
-            os.environ["RWKVTTS_FFN_PERSIST"] = old
 
 
-def _both(blob, reqs, **kw):
+def _both(blob, reqs, modes=("off", "ffn", "att", "both"), **kw):
     outs, profs = [], []
-    for persist in (False, True):
+    for persist in modes:
         rt = _runtime(blob, persist, **kw)
         try:
             outs.append(rt.generate_batch(reqs))
@@ -51,17 +72,20 @@ def blob04():
 
 def test_persist_bench_shape_bitwise(blob04):
     reqs = [make_request(synth_text(100 + i), seed=i, fixed=40) for i in range(32)]
-    (a, b), _ = _both(blob04, reqs, max_slots=32, token_chunk_size=2048, use_graphs=True)
-    assert a == b
+    outs, _ = _both(blob04, reqs, max_slots=32, token_chunk_size=2048, use_graphs=True)
+    assert all(o == outs[0] for o in outs[1:])
 
 
 def test_persist_fewer_rows_and_eager(blob04):
     import oracle
     reqs = [make_request(synth_text(200 + i), seed=50 + i, fixed=12 + i) for i in range(5)]
-    (a, b), profs = _both(blob04, reqs, max_slots=8, token_chunk_size=512, use_graphs=False)
-    assert a == b
-    # the persistent launch ran (and the three launches did not) in the decode steps
+    outs, profs = _both(blob04, reqs, max_slots=8, token_chunk_size=512, use_graphs=False)
+    assert all(o == outs[0] for o in outs[1:])
+    b = outs[3]
+    # the persistent launches ran (and the separate ones did not) in the decode steps
     assert "ffn_persist" in profs[1] and "ffn_persist" not in profs[0], profs[1].keys()
+    assert "att_persist" in profs[2] and "wkv" in profs[0], profs[2].keys()
+    assert "att_persist" in profs[3] and "ffn_persist" in profs[3], profs[3].keys()
     om = oracle.Model(blob04)
     q, keep = to_struct(reqs[2])
     g, s, _ = om.generate(q)
@@ -71,23 +95,16 @@ def test_persist_fewer_rows_and_eager(blob04):
 def test_persist_f16_bitwise():
     blob = W.synth_blob(W.DIMS_04B, seed=7, dtype=rwkvtts._ffi.DTYPE_F16)
     reqs = [make_request(synth_text(300 + i), seed=70 + i, fixed=16) for i in range(8)]
-    (a, b), _ = _both(blob, reqs, max_slots=8, token_chunk_size=512, use_graphs=True)
-    assert a == b
+    outs, _ = _both(blob, reqs, modes=("off", "both"), max_slots=8, token_chunk_size=512, use_graphs=True)
+    assert outs[0] == outs[1]
 
 
 def test_persist_under_the_manager_two_engines_one_device(blob04):
     """Two engines on one device decoding at the same time: two persistent launches in flight on
     the GPU together (dependencies only point to lower block indices: no deadlock)."""
-    old = os.environ.get("RWKVTTS_FFN_PERSIST")
-    os.environ["RWKVTTS_FFN_PERSIST"] = "1"
-    try:
+    with _env(MODES["both"]):
         m = rwkvtts.DynamicBatchManager(blob04, rwkvtts.DynamicBatchConfig(max_batch_size=64, collect_timeout_ms=5),
                                         devices=[0, 0], max_slots=32, token_chunk_size=512)
-    finally:
-        if old is None:
-            os.environ.pop("RWKVTTS_FFN_PERSIST", None)
-        else:
-            os.environ["RWKVTTS_FFN_PERSIST"] = old
     try:
         reqs = [make_request(synth_text(400 + i), seed=90 + i, fixed=20) for i in range(48)]
         got = m.generate_tts_batch(reqs)

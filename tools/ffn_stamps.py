@@ -1,6 +1,7 @@
-"""k_ffn_persist per-block stamps (RWKVTTS_FFN_STAMPS, layer 5 of the last decode step): per role
-(LayerNorm rows, key workgroups, value workgroups) the min / median / max of each stamp in us
-from the launch's first block start. Usage: ffn_stamps.py [S] (runs 32 requests, S semantic)."""
+"""Persistent-launch per-block stamps (layer 5 of the last decode step): k_ffn_persist
+(RWKVTTS_FFN_STAMPS; roles LayerNorm rows, key, value) or k_att_persist (RWKVTTS_ATT_STAMPS; roles
+LayerNorm rows, rkv, WKV, Wo): per role the min / median / max of each stamp in us from the
+launch's first block start. Usage: ffn_stamps.py [S] [ffn|att] (32 requests, S semantic)."""
 import os
 import sys
 import tempfile
@@ -9,9 +10,10 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "rwkv-tts-rs_amd"))
-path = os.path.join(tempfile.mkdtemp(), "ffn_stamps.bin")
-os.environ["RWKVTTS_FFN_STAMPS"] = path
-os.environ.setdefault("RWKVTTS_FFN_PERSIST", "1")
+which = sys.argv[2] if len(sys.argv) > 2 else "ffn"
+path = os.path.join(tempfile.mkdtemp(), "stamps.bin")
+os.environ["RWKVTTS_FFN_STAMPS" if which == "ffn" else "RWKVTTS_ATT_STAMPS"] = path
+os.environ.setdefault("RWKVTTS_FFN_PERSIST" if which == "ffn" else "RWKVTTS_ATT_PERSIST", "5")
 import rwkvtts  # noqa: E402
 from rwkvtts import weights as W  # noqa: E402
 
@@ -30,8 +32,10 @@ for rep in range(2):
     print(f"rep {rep}: decode {st['decode_ms'] / max(st['steps'], 1) * 1000:.1f} us/step")
 rt.close()
 a = np.fromfile(path, dtype=np.uint64).reshape(-1, 4).astype(np.float64)
-roles = {"ln": (0, 32), "key": (32, 288), "value": (288, 544)}
-t0 = a[:544, 0][a[:544, 0] > 0].min()
+roles = ({"ln": (0, 32), "key": (32, 288), "value": (288, 544)} if which == "ffn" else
+         {"ln": (0, 32), "rkv": (32, 244), "wkv": (244, 756), "wo": (756, 884)})
+nb = max(e for _, e in roles.values())
+t0 = a[:nb, 0][a[:nb, 0] > 0].min()
 names = ["start", "wait_done", "work_done", "end"]
 for r, (b, e) in roles.items():
     x = (a[b:e] - t0) * 0.01  # 100 MHz ticks -> us
