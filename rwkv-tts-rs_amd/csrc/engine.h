@@ -136,9 +136,11 @@ class Engine {
   // write-through (sc1) output stores per launch class, same bit order as xmap_mask_, plus
   // bit 6 ln_att, bit 7 ln_ffn
   int wt_mask_ = 0xFF;
-  int ffn_persist_ = 0;     // RWKVTTS_FFN_PERSIST: decode steps' FFN half as one launch (k_ffn_persist)
+  int ffn_persist_ = 5;     // RWKVTTS_FFN_PERSIST: decode steps' FFN half as one launch (k_ffn_persist);
+                            // 0 off, else 1 + 2 x launch options (5: long poll sleep, the measured best)
   int* ffn_sync_ = nullptr; // its hand-off counters: [L][kFfnSyncInts] (give-up code: d_ctrl_[S_])
-  int att_persist_ = 0;     // RWKVTTS_ATT_PERSIST: decode steps' attention half as one launch (k_att_persist)
+  int att_persist_ = 5;     // RWKVTTS_ATT_PERSIST: decode steps' attention half as one launch (k_att_persist),
+                            // same encoding
   int* att_sync_ = nullptr; // its hand-off counters: [L][kAttSyncInts]
   int xalign_mask_ = 4;     // GemmArgs::xalign per class: bit 0 rkv (-> WKV heads), bit 2 ffn key (-> value K-slices)
   int device_ = 0;

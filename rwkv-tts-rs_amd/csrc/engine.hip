@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <chrono>
 #include <deque>
+#include <map>
 #include <mutex>
 #include <random>
 
@@ -23,7 +24,33 @@ int Engine::alloc(T** p, size_t count) {
   return RWKVTTS_OK;
 }
 
+// At most ONE engine per device (in this process) runs the persistent launches. Two persistent
+// launches in flight on one GPU can deadlock: workgroups are dealt to the 8 XCDs round-robin and
+// each XCD dispatches its share in order, so when another launch fills one XCD, a launch's
+// consumers may be resident on other XCDs while producers they wait for are not -- and the other
+// launch's consumers may wait the same way. Separate launches never wait on one another, so one
+// persistent engine beside any number of others (and the vocoder) always makes progress. The
+// first engine created on a device takes the slot; it is released when that engine is destroyed.
+namespace {
+std::mutex g_persist_mu;
+std::map<int, const void*> g_persist_owner;  // device -> the engine holding the persistent slot
+}  // namespace
+
+static bool claim_persistent(int device, const void* who) {
+  std::lock_guard<std::mutex> lk(g_persist_mu);
+  auto it = g_persist_owner.find(device);
+  if (it != g_persist_owner.end() && it->second != who) return false;
+  g_persist_owner[device] = who;
+  return true;
+}
+static void release_persistent(int device, const void* who) {
+  std::lock_guard<std::mutex> lk(g_persist_mu);
+  auto it = g_persist_owner.find(device);
+  if (it != g_persist_owner.end() && it->second == who) g_persist_owner.erase(it);
+}
+
 Engine::~Engine() {
+  release_persistent(device_, this);
   hipSetDevice(device_);
   if (stream_) hipStreamSynchronize(stream_);
   for (auto& g : graphs_) hipGraphExecDestroy(g.second);
@@ -100,6 +127,7 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
   if (const char* xa = getenv("RWKVTTS_XALIGN_MASK")) xalign_mask_ = (int)strtol(xa, nullptr, 0);
   if (const char* fp = getenv("RWKVTTS_FFN_PERSIST")) ffn_persist_ = atoi(fp);
   if (const char* ap = getenv("RWKVTTS_ATT_PERSIST")) att_persist_ = atoi(ap);
+  if ((ffn_persist_ || att_persist_) && !claim_persistent(desc.device, this)) ffn_persist_ = att_persist_ = 0;
   if (const char* gp = getenv("RWKVTTS_GEMM_STAMPS")) {
     dbg_gstamp_path_ = gp;
     RT_OK(alloc(&dbg_gstamps_, 2 * 4096 * 4));
@@ -466,6 +494,17 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
   // launch and one boundary fewer per step; k_embed's arithmetic, bit for bit). Prefill steps keep
   // k_embed (their token-shift rows need the previous token's embedding as well).
   const bool emb_fused = inplace && C == 1024 && !no_emb_fuse_;
+  // persistent launches (k_att_persist / k_ffn_persist) run for EVERY layer of a decode forward or
+  // for none: each launch zeroes the previous layer's hand-off counters, so a layer that fell back
+  // to the separate launches would leave its successor's counters dirty. Quantised layers and the
+  // debug paths take the separate launches; the attention form needs layer 0's embedding fusion
+  // (its LayerNorm reads no slabs otherwise). Layer 0 tries; if its shapes are not covered, the
+  // whole forward falls back.
+  bool any_quant = false;
+  for (const LayerW& lw : L_) any_quant = any_quant || lw.quant != 0;
+  bool use_att = att_persist_ && inplace && !dbg_exp_ && Lc >= 2 && !dbg_stamps_ && !dbg_gstamps_ && !any_quant &&
+                 emb_fused;
+  bool use_ffn = ffn_persist_ && inplace && !dbg_exp_ && Lc >= 2 && !dbg_gstamps_ && !any_quant;
   if (!emb_fused) {
     prof_begin(&ev);
     launch_embed(d_tok_, d_rows_, &d_ctrl_[0].next_token, (int)(sizeof(SlotCtrl) / 4), emb_,
@@ -570,7 +609,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     // decode steps: the attention half as ONE persistent launch (k_att_persist: LN1 + mixes, rkv +
     // LoRA-down, WKV, Wo with in-launch hand-offs; bit-identical outputs) where the shapes allow it
     bool att_persisted = false;
-    if (att_persist_ && inplace && !dbg_exp_ && Lc >= 2 && !dbg_stamps_ && !g.stamps) {
+    if (use_att) {
       m.tl = g.tl = k.tl = go.tl = tl_next("att_persist");
       prof_begin(&ev);
       att_persisted = launch_att_persist(m, g, k, go, att_sync_ + (size_t)l * kAttSyncInts,
@@ -579,9 +618,13 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
                                          att_persist_ >> 1);
       if (att_persisted) {
         prof_end("att_persist", ev);
-      } else if (d_tl_ && tl_n_ > 0) {
-        --tl_n_;
-        if ((int)tl_names_.size() > tl_n_) tl_names_.resize(tl_n_);
+      } else {
+        RT_CHECK(l == 0, RWKVTTS_EHIP, "persistent attention launch: a layer after layer 0 fell back");
+        use_att = false;  // not covered: the separate launches for this whole forward
+        if (d_tl_ && tl_n_ > 0) {
+          --tl_n_;
+          if ((int)tl_names_.size() > tl_n_) tl_names_.resize(tl_n_);
+        }
       }
     }
     if (!att_persisted) {
@@ -654,7 +697,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     // decode steps: the whole FFN half as ONE persistent launch (k_ffn_persist, in-launch
     // hand-offs; bit-identical outputs) where the shapes allow it
     bool persisted = false;
-    if (ffn_persist_ && inplace && !dbg_exp_ && Lc >= 2) {
+    if (use_ffn) {
       f.tl = gk.tl = gv.tl = tl_next("ffn_persist");
       prof_begin(&ev);
       persisted = launch_ffn_persist(f, gk, gv, ffn_sync_ + (size_t)l * kFfnSyncInts,
@@ -663,9 +706,13 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
                                      ffn_persist_ >> 1);
       if (persisted) {
         prof_end("ffn_persist", ev);
-      } else if (d_tl_ && tl_n_ > 0) {  // (the timeline slot goes to the three launches below)
-        --tl_n_;
-        if ((int)tl_names_.size() > tl_n_) tl_names_.resize(tl_n_);
+      } else {
+        RT_CHECK(l == 0, RWKVTTS_EHIP, "persistent FFN launch: a layer after layer 0 fell back");
+        use_ffn = false;
+        if (d_tl_ && tl_n_ > 0) {  // (the timeline slot goes to the three launches below)
+          --tl_n_;
+          if ((int)tl_names_.size() > tl_n_) tl_names_.resize(tl_n_);
+        }
       }
     }
     if (!persisted) {

@@ -858,11 +858,12 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GemmArgs& a, con
     // the weight stream does not depend on the LayerNorm: in flight during the wait (opts bit 2:
     // requested after it, so the poll is not queued behind the weights and the LN rows' loads do
     // not compete with them)
-    if (!(sy.opts & 4)) load_w();
+    const bool late_w = ROLE == 1 ? (sy.opts & 4) != 0 : (sy.opts & 16) != 0;
+    if (!late_w) load_w();
     sync_wait(sy.cnt + kSyncStride * (blockIdx.x & (kLnReplicas - 1)), sy.ln_rows, sy.err, 1, sy.opts);
     sync_stamp(sy, 1);
     load_x();
-    if (sy.opts & 4) load_w();
+    if (late_w) load_w();
   } else if constexpr (ROLE == 4) {
     load_w();
     const int h0 = kbeg >> 6;  // the K-slice's first head (64 channels per head)
@@ -2143,7 +2144,7 @@ template <bool F16, int ROLE>
 __device__ __attribute__((always_inline)) void wkv6_body(const WkvArgs& a, const int bx, const int by,
                                                          const FfnSync& sy) {
   constexpr int N = 64, DW = 64, DA = 64, DV = 32, DG = 128, DALL = DW + DA + DV + DG, NP = 4;
-  __shared__ __attribute__((aligned(16))) float s_z[ROLE ? N : 1];
+  __shared__ __attribute__((aligned(16))) uint16_t s_zh[ROLE ? N : 4], s_zl[ROLE ? N : 4];
   __shared__ __attribute__((aligned(16))) float s_hid[DALL];
   __shared__ __attribute__((aligned(16))) float s_vec[5][N];  // w, kk (unnormalised), a, k, r
   __shared__ float s_red[4][4];
@@ -2204,6 +2205,9 @@ __device__ __attribute__((always_inline)) void wkv6_body(const WkvArgs& a, const
     // LoRA-up rows and the state first (they do not depend on this layer's rkv workgroups), then
     // wait for the head's r / k / v tiles and the LoRA-down tiles, then their partials
     slot = sg.x; r_begin = sg.y; n_rows = sg.z;
+    // (opts bit 3: only once the LN rows are published -- the LN phase then runs without this
+    // prefetch beside it; the rkv phase still hides it)
+    if (sy.opts & 8) sync_wait(sy.cnt + kSyncStride * (kAttLn + (blockIdx.x & (kLnReplicas - 1))), sy.ln_rows, sy.err, 64, sy.opts);
 #pragma unroll
     for (int u = 0; u < 9; ++u) lw[u] = pl[u * 256 + t];
     load_state(slot);
@@ -2325,7 +2329,7 @@ __device__ __attribute__((always_inline)) void wkv6_body(const WkvArgs& a, const
         y2 += sv * (float2_){rq[e], rq[e + 1]};
       }
     }
-    if (rr + 1 == n_rows) {
+    if (rr + 1 == n_rows && ROLE == 0) {  // (ROLE 1 stores the state after its hand-off)
       if (a.wt) {
         const auto rs = wt_rsrc(a.state + (int64_t)slot * a.slot_stride + a.layer_off + (int64_t)h * N * N);
 #pragma unroll
@@ -2348,24 +2352,23 @@ __device__ __attribute__((always_inline)) void wkv6_body(const WkvArgs& a, const
     const float var =
         fmaxf(((s_red[3][0] + s_red[3][1]) + (s_red[3][2] + s_red[3][3])) * (1.0f / N) - mean * mean, 0.f);
     if constexpr (ROLE == 1) {
-      // the row's 64 z values through LDS; wave 0's lanes 0..15 store 4 channels each as one 8-byte
-      // write-through store per plane (split as split_store does: the same bits)
+      // the row's 64 z values split by the same threads and expression as split_store (the
+      // compiler fuses the product into the 16-bit conversion, so the split must stay here to
+      // keep the bits), the planes through LDS; wave 0's lanes 0..15 store 4 channels each as one
+      // 8-byte write-through store per plane
       if (qq == 0) {
         const float gn = (y - mean) * __builtin_amdgcn_rsqf(var + 64e-5f) * lnw + lnb;
-        s_z[i] = (gn + bonus * v) * lo3;
+        const float zx = (gn + bonus * v) * lo3;
+        const uint16_t hb = f32_to_w16(zx, F16);
+        s_zh[i] = hb;
+        s_zl[i] = f32_to_w16(zx - w16_to_f32(hb, F16), F16);
       }
       __syncthreads();
       if (t < 16) {
-        const float4_ z4 = *(const float4_*)(s_z + 4 * t);
-        uint16_t hh[4], ll[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          hh[e] = f32_to_w16(z4[e], F16);
-          ll[e] = f32_to_w16(z4[e] - w16_to_f32(hh[e], F16), F16);
-        }
+        const uint2 hv = *(const uint2*)(s_zh + 4 * t), lv = *(const uint2*)(s_zl + 4 * t);
         const int64_t zo = ((int64_t)row * a.ldz + h * N + 4 * t) * 2;
-        store_wt(wt_rsrc(a.z_hi), (int)zo, make_uint2(hh[0] | ((uint32_t)hh[1] << 16), hh[2] | ((uint32_t)hh[3] << 16)));
-        store_wt(wt_rsrc(a.z_lo), (int)zo, make_uint2(ll[0] | ((uint32_t)ll[1] << 16), ll[2] | ((uint32_t)ll[3] << 16)));
+        store_wt(wt_rsrc(a.z_hi), (int)zo, hv);
+        store_wt(wt_rsrc(a.z_lo), (int)zo, lv);
       }
     } else {
     if (qq == 0) {
@@ -2379,6 +2382,11 @@ __device__ __attribute__((always_inline)) void wkv6_body(const WkvArgs& a, const
   if constexpr (ROLE == 1) {
     sync_stamp(sy, 2);
     sync_arrive(sy.cnt + kSyncStride * (kAttWkv + h));
+    // the final state (read by the next step's launch only) goes out after the hand-off, so its
+    // write-through drain is not on the Wo workgroups' path
+    const auto rs = wt_rsrc(a.state + (int64_t)slot * a.slot_stride + a.layer_off + (int64_t)h * N * N);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) store_wt(rs, (q * 256 + t) * 16, S4[q]);
   }
 }
 

@@ -14,6 +14,7 @@
 // has one owner thread running Engine::serve, which admits queued requests into free state slots
 // between forward steps (continuous batching). One engine per GPU = request-level data
 // parallelism over the node; no collective is needed on this path.
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -539,6 +540,9 @@ void Worker::run(rwkvtts_engine_desc desc, const void* w, size_t bytes) {
     rc = eng.serve(*this);
     progress(eng);
     if (rc != RWKVTTS_OK) {
+      // the error text lives in this (engine) thread: log it, callers only see the status code
+      fprintf(stderr, "rwkvtts manager: engine %d (device %d) failed (%d): %s\n", idx_, desc.device, rc,
+              rwkvtts_last_error());
       dead = true;  // an engine failure fails its in-flight jobs (serve) and everything queued here
       std::vector<Job*> rest;
       bool open = true;
