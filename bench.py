@@ -103,6 +103,10 @@ def algorithmic_bytes(d, R, head_rows):
         "ln_mix_ffn": R * C * 4 * 2,
     }
     per_step = {k: v * L for k, v in per.items()}
+    # the persistent launches of a decode step (k_att_persist / k_ffn_persist) move the bytes of
+    # the launches they replace (per launch; not added to per_step again)
+    per["att_persist"] = per["ln_mix_att"] + per["gemm_rkv_lora"] + per["wkv"] + per["gemm_wo"]
+    per["ffn_persist"] = per["ln_mix_ffn"] + per["gemm_ffn_key"] + per["gemm_ffn_value"]
     per_step["gemm_head"] = head_rows * C * 2 + R * head_rows * 4
     per_step["embed"] = R * C * 2
     return per, per_step
@@ -310,8 +314,10 @@ def main():
         per_launch, per_step = algorithmic_bytes(dims, R, 8193)
         for name, (launches, ms) in prof.items():
             kernels[name] = {"launches": launches, "avg_us": 1000.0 * ms / max(launches, 1), "total_ms": ms}
-        # dominant kernel by total time among the decode-step kernels with a byte model
-        cand = [(v["total_ms"], k) for k, v in kernels.items() if k in per_launch]
+        # dominant kernel by total time among the decode-step kernels with a byte model (launched
+        # at least once per decode step: prefill-only launches are not the decode loop's)
+        n_dec = max((v["launches"] for v in kernels.values()), default=0)
+        cand = [(v["total_ms"], k) for k, v in kernels.items() if k in per_launch and v["launches"] * 4 >= n_dec]
         if cand:
             _, dom = max(cand)
             avg_s = kernels[dom]["avg_us"] * 1e-6

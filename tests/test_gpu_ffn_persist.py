@@ -18,10 +18,12 @@ from helpers import make_request, synth_text, to_struct
 pytestmark = pytest.mark.gpu
 
 
-MODES = {"off": {"RWKVTTS_FFN_PERSIST": "0", "RWKVTTS_ATT_PERSIST": "0"},
-         "ffn": {"RWKVTTS_FFN_PERSIST": "5", "RWKVTTS_ATT_PERSIST": "0"},
-         "att": {"RWKVTTS_FFN_PERSIST": "0", "RWKVTTS_ATT_PERSIST": "5"},
-         "both": {"RWKVTTS_FFN_PERSIST": "5", "RWKVTTS_ATT_PERSIST": "5"}}
+# (RWKVTTS_PERSIST_MIN_ROWS=1: the persistent forms also for the small row counts tested here;
+# by default decode steps below 16 rows take the separate launches)
+MODES = {"off": {"RWKVTTS_FFN_PERSIST": "0", "RWKVTTS_ATT_PERSIST": "0", "RWKVTTS_PERSIST_MIN_ROWS": "1"},
+         "ffn": {"RWKVTTS_FFN_PERSIST": "5", "RWKVTTS_ATT_PERSIST": "0", "RWKVTTS_PERSIST_MIN_ROWS": "1"},
+         "att": {"RWKVTTS_FFN_PERSIST": "0", "RWKVTTS_ATT_PERSIST": "5", "RWKVTTS_PERSIST_MIN_ROWS": "1"},
+         "both": {"RWKVTTS_FFN_PERSIST": "5", "RWKVTTS_ATT_PERSIST": "5", "RWKVTTS_PERSIST_MIN_ROWS": "1"}}
 
 
 class _env:

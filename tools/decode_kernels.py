@@ -13,6 +13,10 @@ DECODE = {
     "wkv": (("k_wkv6<false, false>", "k_wkv6<false>"), 131072),
     "ln_mix_att": (("k_ln1024<false, 1, 6, 16",), 8192),
     "ln_mix_ffn": (("k_ln1024<false, 1, 1, 8",), 8192),
+    # the persistent decode launches (round 4): 32 LN + 212 rkv + 512 WKV + 128 Wo blocks and
+    # 32 LN + 256 key + 256 value blocks of 256 threads
+    "att_persist": (("k_att_persist<false, true>", "k_att_persist<false, false>"), 884 * 256),
+    "ffn_persist": (("k_ffn_persist<false>",), 544 * 256),
 }
 
 
