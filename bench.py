@@ -177,6 +177,8 @@ def main():
                     help="prompt rows per engine step (all admitted prompts share it; outputs are chunk-invariant, bitwise)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-batch1", action="store_true", help="skip the config-2 (one request) leg")
+    ap.add_argument("--no-graph-timing", dest="graph_timing", action="store_false",
+                    help="per-kernel times from an eager HIP-event pass instead of in-graph stamps")
     ap.add_argument("--profile", action="store_true", help="per-kernel HIP-event pass (default on)")
     ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
                     help="run the vocoder of each batch after its LM decode instead of overlapped")
@@ -245,8 +247,15 @@ def main():
         assert sum(p.size for p in pcm) == 320 * n, "vocoder output length mismatch"
         return n
 
+    # in-graph kernel timing (rwkvtts_set_profiling mode 2): the decode graphs captured during the
+    # warmup carry launch-timeline slots; the last step of every decode window of the timed region
+    # is sampled (per launch: first workgroup start -> last workgroup end)
+    if args.graph_timing:
+        rt.set_profiling(2)
     for w in range(args.warmup):
         run(-1 - w)
+    if args.graph_timing:
+        rt.set_profiling(2)  # (clears what the warmup accumulated)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -286,6 +295,9 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    gprof = rt.profile() if args.graph_timing else {}
+    if args.graph_timing:
+        rt.set_profiling(0)
     elapsed, total_tokens = D.reduce_run(elapsed, sem_tokens, device="cuda")
     samples = total_tokens * 320
     value = samples / elapsed
@@ -298,13 +310,17 @@ def main():
     step_roof = None
     codec_roof = None
     if rank == 0:
-        # the LM pass and the vocoder pass run alone (the kernels' own speed; in the timed loop
-        # the vocoder overlaps only the first ~12 % of a batch's decode steps, so the rocprof
-        # median over the timed region's decode launches measures the same thing)
-        rt.set_profiling(True)
-        prof_out = rt.generate_batch(requests(10**6))
-        prof = rt.profile()
-        rt.set_profiling(False)
+        # decode-step kernels: the in-graph samples of the timed region (the same launches rocprof
+        # traces); without them (--no-graph-timing) an eager HIP-event pass of one batch. The
+        # vocoder's own pass runs alone.
+        if gprof:
+            prof = gprof
+            prof_out = out
+        else:
+            rt.set_profiling(True)
+            prof_out = rt.generate_batch(requests(10**6))
+            prof = rt.profile()
+            rt.set_profiling(False)
         voc.set_profiling(True)
         vocode(prof_out)
         vprof = voc.profile()
@@ -327,7 +343,9 @@ def main():
                         "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
                         "traffic_source": tsrc, "bytes_per_launch": per_launch[dom],
                         "avg_us": round(kernels[dom]["avg_us"], 2),
-                        "avg_us_source": "HIP events on the engine stream, eager decode launches (one batch)",
+                        "avg_us_source": ("in-graph launch stamps of the timed region's decode steps (last step "
+                                          "of every decode window: first workgroup start -> last workgroup end)"
+                                          if gprof else "HIP events on the engine stream, eager launches (one batch)"),
                         "rocprof": rocprof_decode(dom)}
         # vocoder: MFMA-bound conv stack, achieved TFLOP/s per class and for the whole decoder
         cfl = codec_flops(cdims, B_PER_GPU * SEMANTIC)

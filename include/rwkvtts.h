@@ -346,8 +346,11 @@ typedef struct {
 } rwkvtts_stats;
 int rwkvtts_get_stats(rwkvtts_engine* e, rwkvtts_stats* out);
 
-/* Per-kernel HIP-event timing over the last generate call (enabled by
- * rwkvtts_set_profiling(e, 1)): name, launches, total ms. */
+/* Per-kernel timing: rwkvtts_set_profiling(e, 1) = HIP events on eager launches (graphs off);
+ * (e, 2) = in-graph timing: the decode graphs are recaptured with launch-timeline slots and the
+ * last step of every graph-replayed decode window is sampled (first workgroup start to last
+ * workgroup end per launch, the interval rocprofv3 --kernel-trace reports); 0 = off. Calling
+ * it again with the same mode clears the accumulated entries. Entries: name, launches, total ms. */
 int rwkvtts_set_profiling(rwkvtts_engine* e, int on);
 int rwkvtts_profile_entry(rwkvtts_engine* e, int idx, char* name, int name_cap, int64_t* launches,
                           double* total_ms);

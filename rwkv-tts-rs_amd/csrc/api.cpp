@@ -150,10 +150,12 @@ int rwkvtts_get_stats(rwkvtts_engine* e, rwkvtts_stats* out) {
 
 int rwkvtts_set_profiling(rwkvtts_engine* e, int on) {
   RT_CHECK(e, RWKVTTS_EINVAL, "null engine");
+  RT_CHECK(on >= 0 && on <= 2, RWKVTTS_EINVAL, "set_profiling: 0, 1 or 2");
   LOCK(e);
-  e->eng.profiling = on != 0;
-  e->eng.prof.clear();
-  return RWKVTTS_OK;
+  GUARD({
+    e->eng.profiling = on == 1;
+    return e->eng.set_graph_timing(on == 2);
+  })
 }
 
 int rwkvtts_profile_entry(rwkvtts_engine* e, int idx, char* name, int name_cap, int64_t* launches,

@@ -112,22 +112,19 @@ __device__ inline void store_wt(__amdgpu_buffer_rsrc_t r, int off_bytes, float v
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, off_bytes, 0, 16);
 }
 
-// Debug timeline (RWKVTTS_TIMELINE): start of the launch's first workgroup and end of its last
-// one in s_memrealtime ticks (100 MHz, one clock for every CU); ends are max-reduced over 64
-// slots to keep the atomics off one address. Slot layout per launch: [0] start, [2..65] ends.
-// Null in production.
+// Launch timeline: start of the launch's first workgroup and end of its last one in
+// s_memrealtime ticks (100 MHz, one clock for every CU); ends are max-reduced over 64 slots to keep
+// the atomics off one address. Slot layout per launch: [0] start, [2..65] ends. The slot pointer
+// is null unless the engine records launch times: the debug timeline (RWKVTTS_TIMELINE, make TL=1)
+// or the in-graph kernel timing the bench samples (rwkvtts_set_profiling(e, 2)); with a null slot
+// a hook is one uniform branch.
 constexpr int kTlStride = 66;
 __device__ inline int tl_block() { return (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x; }
-// The hooks compile to nothing unless the library is built with -DRWKVTTS_TL (make TL=1).
 __device__ inline void tl_begin(unsigned long long* tl) {
-#ifdef RWKVTTS_TL
   if (tl && threadIdx.x == 0 && tl_block() == 0) tl[0] = (unsigned long long)__builtin_amdgcn_s_memrealtime();
-#endif
 }
 __device__ inline void tl_end(unsigned long long* tl) {
-#ifdef RWKVTTS_TL
   if (tl && threadIdx.x == 0) atomicMax(&tl[2 + (tl_block() & 63)], (unsigned long long)__builtin_amdgcn_s_memrealtime());
-#endif
 }
 
 // Kernel launches of the LM / sampler path go through RT_LAUNCH. While the engine has a

@@ -116,6 +116,13 @@ class Engine {
   rwkvtts_stats stats{};
   bool profiling = false;
   std::vector<ProfEntry> prof;
+  // In-graph kernel timing (rwkvtts_set_profiling(e, 2)): the decode graphs are (re)captured with
+  // launch-timeline slots; after every graph-replayed decode window the last step's per-launch
+  // (first workgroup start, last workgroup end) stamps are copied back with the control snapshot
+  // and accumulated into `prof` by launch name -- the kernels' own durations inside the graphs,
+  // as rocprofv3 --kernel-trace reports them, without eager launches or per-step syncs.
+  int set_graph_timing(bool on);
+  bool graph_timing() const { return d_gt_ != nullptr && gtime_; }
 
  private:
   int run_step(const StepPlan& p, bool upload);
@@ -154,15 +161,23 @@ class Engine {
   // debug timeline (RWKVTTS_TIMELINE=path): per launch of a decode step, earliest WG start and
   // latest WG end (s_memrealtime); accumulated over steps and written at the end of generate()
   unsigned long long* d_tl_ = nullptr;  // [kTlMax][kTlStride]
+  unsigned long long* d_gt_ = nullptr;  // in-graph timing slots [kTlMax][kTlStride]
+  unsigned long long* h_gt_ = nullptr;  // pinned: 2 snapshots of them (one per unit buffer)
+  bool gtime_ = false;
+  std::map<std::pair<int, int>, std::vector<std::string>> graph_names_;  // launch names per graph
+  std::pair<int, int> last_graph_ = {-1, -1};  // key of the graph the last run_step replayed
+  std::pair<int, int> unit_graph_[2] = {{-1, -1}, {-1, -1}};  // per unit buffer (decode windows)
+  unsigned long long* tl_base() const { return d_tl_ ? d_tl_ : (gtime_ ? d_gt_ : nullptr); }
   std::string tl_path_;
   std::vector<std::string> tl_names_;
   std::vector<double> tl_start_, tl_dur_;
   int tl_steps_ = 0;
   int tl_n_ = 0;
   unsigned long long* tl_next(const char* name) {
-    if (!d_tl_ || tl_n_ >= kTlMax) return nullptr;
+    unsigned long long* base = tl_base();
+    if (!base || tl_n_ >= kTlMax) return nullptr;
     if ((int)tl_names_.size() <= tl_n_) tl_names_.push_back(name);
-    unsigned long long* p = d_tl_ + (size_t)kTlStride * tl_n_;
+    unsigned long long* p = base + (size_t)kTlStride * tl_n_;
     ++tl_n_;
     return p;
   }

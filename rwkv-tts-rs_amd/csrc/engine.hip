@@ -59,6 +59,7 @@ Engine::~Engine() {
   for (void* p : {(void*)d_samp_logits_, (void*)d_keys_, (void*)d_draws_, (void*)d_out_, d_wide_})
     if (p) hipFree(p);
   if (h_ctrl_) hipHostFree(h_ctrl_);
+  if (h_gt_) hipHostFree(h_gt_);
   if (stream_) hipStreamDestroy(stream_);
 }
 
@@ -490,7 +491,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
   const bool inplace = tok_from_ctrl;
   if (!inplace) hipLaunchKernelGGL(k_rows_parity, dim3(nb), dim3(256), 0, stream_, d_rows_, slot_par_, R);
   tl_n_ = 0;
-  if (d_tl_) tl_names_.clear();  // the names of this forward's launches (decode steps have one fewer)
+  if (tl_base()) tl_names_.clear();  // the names of this forward's launches (decode steps have one fewer)
   // decode steps: the embedding (token -> row -> LN0) runs inside layer 0's LayerNorm launch (one
   // launch and one boundary fewer per step; k_embed's arithmetic, bit for bit). Prefill steps keep
   // k_embed (their token-shift rows need the previous token's embedding as well).
@@ -625,7 +626,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
       } else {
         RT_CHECK(l == 0, RWKVTTS_EHIP, "persistent attention launch: a layer after layer 0 fell back");
         use_att = false;  // not covered: the separate launches for this whole forward
-        if (d_tl_ && tl_n_ > 0) {
+        if (tl_base() && tl_n_ > 0) {
           --tl_n_;
           if ((int)tl_names_.size() > tl_n_) tl_names_.resize(tl_n_);
         }
@@ -713,7 +714,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
       } else {
         RT_CHECK(l == 0, RWKVTTS_EHIP, "persistent FFN launch: a layer after layer 0 fell back");
         use_ffn = false;
-        if (d_tl_ && tl_n_ > 0) {  // (the timeline slot goes to the three launches below)
+        if (tl_base() && tl_n_ > 0) {  // (the timeline slot goes to the three launches below)
           --tl_n_;
           if ((int)tl_names_.size() > tl_n_) tl_names_.resize(tl_n_);
         }
@@ -809,6 +810,23 @@ int Engine::upload_plan(const StepPlan& p) {
 }
 
 // Runs one forward step. Decode steps (tok_from_ctrl) replay a cached hipGraph.
+int Engine::set_graph_timing(bool on) {
+  RT_HIP(hipSetDevice(device_));
+  if (on && !d_gt_) {
+    RT_OK(alloc(&d_gt_, (size_t)kTlStride * kTlMax));
+    RT_HIP(hipHostMalloc((void**)&h_gt_, sizeof(unsigned long long) * 2 * kTlStride * kTlMax, hipHostMallocDefault));
+  }
+  if (on != gtime_) {  // the decode graphs carry (or drop) the timeline slots: recapture
+    RT_HIP(hipStreamSynchronize(stream_));
+    for (auto& g : graphs_) hipGraphExecDestroy(g.second);
+    graphs_.clear();
+    graph_names_.clear();
+    gtime_ = on;
+  }
+  prof.clear();
+  return RWKVTTS_OK;
+}
+
 int Engine::run_step(const StepPlan& p, bool upload) {
   const int R = (int)p.rows.size();
   RT_CHECK(R > 0 && R <= Rmax_, RWKVTTS_EINVAL, "step rows out of range");
@@ -836,10 +854,13 @@ int Engine::run_step(const StepPlan& p, bool upload) {
       RT_HIP(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
       RT_HIP(hipGraphDestroy(graph));
       it = graphs_.emplace(key, exec).first;
+      if (tl_base()) graph_names_[key] = tl_names_;
     }
     RT_HIP(hipGraphLaunch(it->second, stream_));
+    last_graph_ = key;
     return RWKVTTS_OK;
   }
+  last_graph_ = {-1, -1};
   RT_OK(launch_forward(R, n_seg, n_lg, p.head_rows, p.tok_from_ctrl, p.advance));
   return RWKVTTS_OK;
 }
@@ -1196,6 +1217,23 @@ int Engine::finish_unit(int b, bool prefill, std::vector<Active>& act, std::vect
   hipEventElapsedTime(&ms, ev0[b], ev1[b]);
   (prefill ? stats.prefill_ms : stats.decode_ms) += ms;
   RT_OK(flush_prof());
+  if (graph_timing() && unit_graph_[b].first >= 0) {
+    const std::vector<std::string>& names = graph_names_[unit_graph_[b]];
+    const unsigned long long* h = h_gt_ + (size_t)b * kTlStride * kTlMax;
+    for (size_t i = 0; i < names.size(); ++i) {
+      const unsigned long long* q = h + (size_t)kTlStride * i;
+      unsigned long long e = 0;
+      for (int j = 2; j < kTlStride; ++j) e = std::max(e, q[j]);
+      if (e <= q[0]) continue;
+      auto it = std::find_if(prof.begin(), prof.end(), [&](const ProfEntry& x) { return x.name == names[i]; });
+      if (it == prof.end()) {
+        prof.push_back({names[i], 0, 0.0});
+        it = prof.end() - 1;
+      }
+      it->launches++;
+      it->ms += (double)(e - q[0]) * 1e-5;  // 100 MHz ticks -> ms
+    }
+  }
   if (d_tl_ && !prefill && stats.steps > 40) {  // semantic-phase steps only
     std::vector<unsigned long long> h((size_t)kTlStride * kTlMax);
     RT_HIP(hipMemcpy(h.data(), d_tl_, h.size() * 8, hipMemcpyDeviceToHost));
@@ -1472,6 +1510,13 @@ int Engine::serve(JobSource& src) {
       max_active = std::max<int64_t>(max_active, (int64_t)dp.rows.size());
     }
     RT_HIP(hipMemcpyAsync(h_ctrl_ + (size_t)b * (S_ + 1), d_ctrl_, sizeof(SlotCtrl) * (S_ + 1), hipMemcpyDeviceToHost, stream_));
+    unit_graph_[b] = {-1, -1};
+    if (graph_timing() && !any_prefill && last_graph_.first >= 0) {  // the window's last step's stamps
+      const size_t n = graph_names_[last_graph_].size();
+      RT_HIP(hipMemcpyAsync(h_gt_ + (size_t)b * kTlStride * kTlMax, d_gt_, n * kTlStride * 8, hipMemcpyDeviceToHost,
+                            stream_));
+      unit_graph_[b] = last_graph_;
+    }
     RT_HIP(hipEventRecord(ev1[b], stream_));
     Unit now;
     now.valid = true;

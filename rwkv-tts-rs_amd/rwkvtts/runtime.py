@@ -289,8 +289,11 @@ class SharedRwkvRuntime:
         return {f: getattr(s, f) for f, _ in _ffi.Stats._fields_}
 
     @_locked
-    def set_profiling(self, on: bool):
-        check(lib().rwkvtts_set_profiling(self._h, 1 if on else 0), "set_profiling")
+    def set_profiling(self, on):
+        """False / True (1): HIP events on eager launches; 2: in-graph sampled timing of the
+        graph-replayed decode steps (rwkvtts.h rwkvtts_set_profiling)."""
+        mode = on if isinstance(on, int) and not isinstance(on, bool) else (1 if on else 0)
+        check(lib().rwkvtts_set_profiling(self._h, mode), "set_profiling")
 
     @_locked
     def profile(self):

@@ -22,7 +22,8 @@ dur = {n: [] for n in DECODE}
 syms = {n: set() for n in DECODE}
 for r in rows:
     name = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("rwkvtts::", "")
-    g = int(r.get("Grid_Size", 0) or 0)
+    g = int(r.get("Grid_Size", 0) or 0) or (int(r.get("Grid_Size_X", 1) or 1) * int(r.get("Grid_Size_Y", 1) or 1) *
+                                            int(r.get("Grid_Size_Z", 1) or 1))
     for n, (prefixes, grid) in DECODE.items():
         if g == grid and any(name.startswith(p) for p in prefixes):
             dur[n].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)

@@ -11,7 +11,8 @@ skip = float(sys.argv[2]) if len(sys.argv) > 2 else 0.5
 rows = rows[int(len(rows) * skip):]
 tot, cnt = defaultdict(float), defaultdict(int)
 for r in rows:
-    k = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("rwkvtts::", "")[:60] + " g" + r.get("Grid_Size", "")
+    g = r.get("Grid_Size") or str(int(r.get("Grid_Size_X", 1) or 1) * int(r.get("Grid_Size_Y", 1) or 1) * int(r.get("Grid_Size_Z", 1) or 1))
+    k = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("rwkvtts::", "")[:60] + " g" + g
     tot[k] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
     cnt[k] += 1
 span = (int(rows[-1]["End_Timestamp"]) - int(rows[0]["Start_Timestamp"])) / 1e3
