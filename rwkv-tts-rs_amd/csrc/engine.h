@@ -150,6 +150,8 @@ class Engine {
   int att_persist_ = 5;     // RWKVTTS_ATT_PERSIST: decode steps' attention half as one launch (k_att_persist),
                             // same encoding
   int* att_sync_ = nullptr; // its hand-off counters: [L][kAttSyncInts]
+  int layer_persist_ = 1;   // RWKVTTS_LAYER_PERSIST: both halves persistent -> ONE launch per layer (k_layer_persist)
+  int* layer_sync_ = nullptr; // its counters: [L][kLayerSyncInts]
   int xalign_mask_ = 4;     // GemmArgs::xalign per class: bit 0 rkv (-> WKV heads), bit 2 ffn key (-> value K-slices)
   int device_ = 0;
   int f16_ = 0;  // fp16 matrices (else bf16): MFMA f16 and f16 activation planes

@@ -128,6 +128,7 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
   if (const char* xa = getenv("RWKVTTS_XALIGN_MASK")) xalign_mask_ = (int)strtol(xa, nullptr, 0);
   if (const char* fp = getenv("RWKVTTS_FFN_PERSIST")) ffn_persist_ = atoi(fp);
   if (const char* ap = getenv("RWKVTTS_ATT_PERSIST")) att_persist_ = atoi(ap);
+  if (const char* lp = getenv("RWKVTTS_LAYER_PERSIST")) layer_persist_ = atoi(lp);
   if (const char* pm = getenv("RWKVTTS_PERSIST_MIN_ROWS")) persist_min_rows_ = atoi(pm);
   if ((ffn_persist_ || att_persist_) && !claim_persistent(desc.device, this)) ffn_persist_ = att_persist_ = 0;
   if (const char* gp = getenv("RWKVTTS_GEMM_STAMPS")) {
@@ -140,7 +141,7 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
   }
   if (const char* as = getenv("RWKVTTS_ATT_STAMPS")) {  // debug: layer-5 k_att_persist block stamps
     dbg_astamp2_path_ = as;
-    RT_OK(alloc(&dbg_astamps2_, 1024 * 4));
+    RT_OK(alloc(&dbg_astamps2_, 2048 * 4));
   }
   if (const char* tp = getenv("RWKVTTS_TIMELINE")) {
     tl_path_ = tp;
@@ -316,6 +317,8 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
   // previous layer's block)
   RT_OK(alloc(&ffn_sync_, (size_t)Lc * kFfnSyncInts));
   RT_HIP(hipMemset(ffn_sync_, 0, (size_t)Lc * kFfnSyncInts * sizeof(int)));
+  RT_OK(alloc(&layer_sync_, (size_t)Lc * kLayerSyncInts));  // k_layer_persist's
+  RT_HIP(hipMemset(layer_sync_, 0, (size_t)Lc * kLayerSyncInts * sizeof(int)));
   RT_OK(alloc(&att_sync_, (size_t)Lc * kAttSyncInts));  // k_att_persist's, the same scheme
   RT_HIP(hipMemset(att_sync_, 0, (size_t)Lc * kAttSyncInts * sizeof(int)));
   RT_OK(alloc(&vfirst_, RC));
@@ -510,6 +513,8 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
   bool use_att = att_persist_ && inplace && big && !dbg_exp_ && Lc >= 2 && !dbg_stamps_ && !dbg_gstamps_ &&
                  !any_quant && emb_fused;
   bool use_ffn = ffn_persist_ && inplace && big && !dbg_exp_ && Lc >= 2 && !dbg_gstamps_ && !any_quant;
+  // both halves persistent: one launch per layer (k_layer_persist) unless RWKVTTS_LAYER_PERSIST=0
+  bool use_layer = use_att && use_ffn && layer_persist_;
   if (!emb_fused) {
     prof_begin(&ev);
     launch_embed(d_tok_, d_rows_, &d_ctrl_[0].next_token, (int)(sizeof(SlotCtrl) / 4), emb_,
@@ -614,7 +619,9 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     // decode steps: the attention half as ONE persistent launch (k_att_persist: LN1 + mixes, rkv +
     // LoRA-down, WKV, Wo with in-launch hand-offs; bit-identical outputs) where the shapes allow it
     bool att_persisted = false;
-    if (use_att) {
+    if (use_layer) {
+      att_persisted = true;  // launched with the FFN half below (k_layer_persist)
+    } else if (use_att) {
       m.tl = g.tl = k.tl = go.tl = tl_next("att_persist");
       prof_begin(&ev);
       att_persisted = launch_att_persist(m, g, k, go, att_sync_ + (size_t)l * kAttSyncInts,
@@ -702,7 +709,42 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     // decode steps: the whole FFN half as ONE persistent launch (k_ffn_persist, in-launch
     // hand-offs; bit-identical outputs) where the shapes allow it
     bool persisted = false;
-    if (use_ffn) {
+    if (use_layer) {
+      f.tl = gk.tl = gv.tl = m.tl = g.tl = k.tl = go.tl = tl_next("layer_persist");
+      prof_begin(&ev);
+      persisted = launch_layer_persist(m, g, k, go, f, gk, gv, layer_sync_ + (size_t)l * kLayerSyncInts,
+                                       layer_sync_ + (size_t)((l + Lc - 1) % Lc) * kLayerSyncInts,
+                                       (int*)(d_ctrl_ + S_), R, H_, stream_, l == 5 ? dbg_astamps2_ : nullptr,
+                                       att_persist_ >> 1);
+      if (persisted) {
+        prof_end("layer_persist", ev);
+      } else {
+        // layer 0 not covered: no launch was made for this layer yet -- the separate launches of
+        // both halves, and for the rest of this forward
+        RT_CHECK(l == 0, RWKVTTS_EHIP, "persistent layer launch: a layer after layer 0 fell back");
+        use_layer = use_att = use_ffn = false;
+        if (tl_base() && tl_n_ > 0) {
+          --tl_n_;
+          if ((int)tl_names_.size() > tl_n_) tl_names_.resize(tl_n_);
+        }
+        m.tl = tl_next("ln_att");
+        prof_begin(&ev);
+        RT_CHECK(launch_ln_mix(m, R, stream_) >= 0, RWKVTTS_EUNSUPPORTED, "layer-0 embedding fusion: unsupported shape");
+        prof_end("ln_mix_att", ev);
+        g.tl = tl_next("gemm_rkv");
+        prof_begin(&ev);
+        launch_gemm(g, stream_);
+        prof_end("gemm_rkv_lora", ev);
+        k.tl = tl_next("wkv");
+        prof_begin(&ev);
+        launch_wkv(k, n_seg, H_, stream_);
+        prof_end("wkv", ev);
+        go.tl = tl_next("gemm_wo");
+        prof_begin(&ev);
+        launch_gemm(go, stream_);
+        prof_end("gemm_wo", ev);
+      }
+    } else if (use_ffn) {
       f.tl = gk.tl = gv.tl = tl_next("ffn_persist");
       prof_begin(&ev);
       persisted = launch_ffn_persist(f, gk, gv, ffn_sync_ + (size_t)l * kFfnSyncInts,
@@ -1577,7 +1619,7 @@ int Engine::dump_stamps() {
     }
   }
   if (dbg_astamps2_) {
-    std::vector<uint64_t> hf(1024 * 4);
+    std::vector<uint64_t> hf(2048 * 4);
     RT_HIP(hipMemcpy(hf.data(), dbg_astamps2_, hf.size() * 8, hipMemcpyDeviceToHost));
     FILE* f = fopen(dbg_astamp2_path_.c_str(), "wb");
     if (f) {

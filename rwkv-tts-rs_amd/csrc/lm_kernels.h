@@ -161,6 +161,12 @@ constexpr int kFfnSyncInts = 24 * 64;  // counter block per layer: (8 LN replica
 constexpr int kAttSyncInts = 48 * 64;  // counter block per layer (lm_kernels.hip kAtt*)
 bool launch_att_persist(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs& wkv, const GemmArgs& wo, int* cnt,
                         int* cnt_prev, int* err, int R, int H, hipStream_t st, uint64_t* stamps, int opts);
+// A decode step's whole layer (both halves) as ONE persistent launch (k_layer_persist); the
+// counter block is kLayerSyncInts.
+constexpr int kLayerSyncInts = (48 + 8 + 8 + 16) * 64;
+bool launch_layer_persist(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs& wkv, const GemmArgs& wo,
+                          const LnMixArgs& lf, const GemmArgs& key, const GemmArgs& val, int* cnt, int* cnt_prev,
+                          int* err, int R, int H, hipStream_t st, uint64_t* stamps, int opts);
 bool launch_ffn_persist(const LnMixArgs& ln, const GemmArgs& key, const GemmArgs& val, int* cnt, int* cnt_prev,
                         int* err, int R, hipStream_t st, uint64_t* stamps = nullptr, int opts = 0);
 // Fills a.tw / a.tinfo / a.n_tinfo when the segments' packed weights are contiguous in 64-column

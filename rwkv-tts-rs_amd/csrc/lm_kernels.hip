@@ -286,7 +286,9 @@ __global__ __launch_bounds__(256) void k_ln_mix(LnMixArgs a) {
 // MODE 0: ln_out (x = LN(h) planes only). Loads that need only the row (residual, slabs, LN and
 // mix vectors) are issued before the row descriptor that addresses the shift state.
 // ------------------------------------------------------------------------------------
-template <bool F16, int MODE, int NMIX, int NP, bool EMB = false>
+// SC1: the residual and the partial slabs were written earlier in the same (persistent) launch:
+// read with sc1 (L1-bypassing) buffer loads from wave-uniform bases
+template <bool F16, int MODE, int NMIX, int NP, bool EMB = false, bool SC1 = false>
 __device__ __attribute__((always_inline)) void ln1024_body(const LnMixArgs& a, const int out_row) {
   constexpr int C = 1024;
   static_assert(!EMB || (MODE == 1 && NP == 0), "embedding fusion: layer 0's LN + mixes");
@@ -348,11 +350,20 @@ __device__ __attribute__((always_inline)) void ln1024_body(const LnMixArgs& a, c
     __syncthreads();
     v = *(const float4_*)(s_h + c);
   } else {
-    v = ld4(e_hin + (int64_t)row * C + c);
+    if constexpr (SC1)
+      v = __builtin_bit_cast(float4_, __builtin_amdgcn_raw_buffer_load_b128(wt_rsrc(e_hin + (int64_t)row * C), c * 4, 0, 16));
+    else
+      v = ld4(e_hin + (int64_t)row * C + c);
   }
   float4_ t[NP > 0 ? NP : 1];
 #pragma unroll
-  for (int p = 0; p < NP; ++p) t[p] = ld4(e_part + p * e_pstride + (int64_t)row * e_ldp + c);
+  for (int p = 0; p < NP; ++p) {
+    if constexpr (SC1)
+      t[p] = __builtin_bit_cast(float4_, __builtin_amdgcn_raw_buffer_load_b128(
+                                             wt_rsrc(e_part + p * e_pstride + (int64_t)row * e_ldp), c * 4, 0, 16));
+    else
+      t[p] = ld4(e_part + p * e_pstride + (int64_t)row * e_ldp + c);
+  }
   int slot = 0, flags = 0, prev_row = -1, par = 0;
   float4_ pv = {0.f, 0.f, 0.f, 0.f};
   if constexpr (MODE == 1) {
@@ -629,6 +640,8 @@ struct FfnSync {     // (both persistent launches)
   int head_target;   // attention: rkv workgroups per head (3 tiles x splits)
   int lora_target;   // attention: LoRA-down workgroups (tiles x splits)
   int C;             // attention: channels (r / k / v columns [0, 3C), LoRA-down beyond)
+  int* wo_done;      // one-launch layer: Wo workgroups count in here (kLnReplicas replicas) ...
+  int wo_target;     // ... and the FFN LayerNorm rows wait for all of them
   int opts;          // bit 0: value workgroups request their weights only once the LN rows are
                      // published (not at dispatch); bit 1: longer sleep between polls; bit 2: key
                      // workgroups request their weights after the LN wait (with their X)
@@ -1071,6 +1084,9 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GemmArgs& a, con
   }
   if constexpr (ROLE != 0) sync_stamp(sy, 2);
   if constexpr (ROLE == 1) sync_arrive(sy.cnt + kSyncStride * (kLnReplicas + tile / sy.key_group));
+  if constexpr (ROLE == 4) {
+    if (sy.wo_done) sync_arrive(sy.wo_done, kLnReplicas);
+  }
   if constexpr (ROLE == 3) {
     const int c0 = col_off + (tile - tstart) * 64;  // this tile's first output column
     if (c0 < 3 * sy.C) sync_arrive(sy.cnt + kSyncStride * (kAttHead + ((c0 % sy.C) >> 6)));
@@ -1466,8 +1482,14 @@ void launch_relu2_planes(const float* part, int nx, int64_t pstride, int ld, int
 // (the caller runs the three launches). ln / key / val: the three launches' arguments as built by
 // the engine; cnt / cnt_prev: this and the previous layer's counter blocks ((1 + kFfnSlices) x
 // kSyncStride ints, zero before this layer's first use); err: the give-up word.
-bool launch_ffn_persist(const LnMixArgs& ln, const GemmArgs& key, const GemmArgs& val, int* cnt, int* cnt_prev,
-                        int* err, int R, hipStream_t st, uint64_t* stamps, int opts) {
+struct FfnPrep {
+  LnMixArgs l;
+  GemmArgs ka, va;
+  FfnSync sy;
+  int nv;
+};
+static bool prep_ffn_persist(const LnMixArgs& ln, const GemmArgs& key, const GemmArgs& val, int* cnt, int* cnt_prev,
+                             int* err, int R, uint64_t* stamps, int opts, FfnPrep& P) {
   if (ln.C != 1024 || !ln.shift || ln.n_mix != 1 || ln.n_part != 8 || ln.emb || R < 1 || R > 32 ||
       key.xmode != kXPlanes || val.xmode != kXRelu2 || val.x_nsplit != 4 || key.kslice != 256 ||
       val.kslice != 256 || key.M != R || val.M != R || key.nseg != 1 || val.nseg != 1 || key.q_fmt || val.q_fmt ||
@@ -1482,13 +1504,18 @@ bool launch_ffn_persist(const LnMixArgs& ln, const GemmArgs& key, const GemmArgs
   if (kt % key.xalign || groups % 8 || groups != val.k_split || val.k_split % 8 || val.k_split > kFfnSlices ||
       key.xalign * 64 != val.kslice)
     return false;
-  LnMixArgs l = ln;
+  LnMixArgs& l = P.l;
+  l = ln;
   l.n_rows = R;
   l.wt = 1;
-  GemmArgs ka = key, va = val;
+  GemmArgs& ka = P.ka;
+  GemmArgs& va = P.va;
+  ka = key;
+  va = val;
   ka.xmap = 2; ka.ntiles = kt; ka.wt = 1;
   va.xmap = 1; va.ntiles = vt;
-  FfnSync sy{};
+  FfnSync& sy = P.sy;
+  sy = FfnSync{};
   sy.cnt = cnt;
   sy.cnt_prev = cnt_prev;
   sy.err = err;
@@ -1500,9 +1527,20 @@ bool launch_ffn_persist(const LnMixArgs& ln, const GemmArgs& key, const GemmArgs
   sy.stamps = stamps;
   sy.opts = opts;
   sy.n_prev = kLnReplicas + kFfnSlices;
-  const int nv = vt * val.k_split;
+  P.nv = vt * val.k_split;
+  return true;
+}
+
+bool launch_ffn_persist(const LnMixArgs& ln, const GemmArgs& key, const GemmArgs& val, int* cnt, int* cnt_prev,
+                        int* err, int R, hipStream_t st, uint64_t* stamps, int opts) {
+  FfnPrep P;
+  if (!prep_ffn_persist(ln, key, val, cnt, cnt_prev, err, R, stamps, opts, P)) return false;
+  LnMixArgs& l = P.l;
+  GemmArgs& ka = P.ka;
+  GemmArgs& va = P.va;
+  FfnSync& sy = P.sy;
   const size_t lds = (size_t)2 * 16 * (8 * 32 + 8) * 2 * 2;
-  const dim3 grid(sy.n_ln_blocks + sy.n_key + nv);
+  const dim3 grid(sy.n_ln_blocks + sy.n_key + P.nv);
   if (key.f16) RT_LAUNCH((k_ffn_persist<true>), grid, dim3(256), lds, st, l, ka, va, sy);
   else RT_LAUNCH((k_ffn_persist<false>), grid, dim3(256), lds, st, l, ka, va, sy);
   return true;
@@ -2439,8 +2477,57 @@ __global__ __launch_bounds__(256, 2) void k_att_persist(LnMixArgs ln, GemmArgs g
   tl_end(ln.tl);
 }
 
-bool launch_att_persist(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs& wkv, const GemmArgs& wo, int* cnt,
-                        int* cnt_prev, int* err, int R, int H, hipStream_t st, uint64_t* stamps, int opts) {
+// ------------------------------------------------------------------------------------
+// layer_persist: a decode step's WHOLE layer as one launch: k_att_persist's blocks, then
+// k_ffn_persist's, whose LayerNorm rows wait for every Wo workgroup (wo_done replicas) and read
+// the residual and the Wo slabs by sc1 loads. One launch boundary per layer instead of two.
+// ------------------------------------------------------------------------------------
+template <bool F16, bool EMB>
+__global__ __launch_bounds__(256, 2) void k_layer_persist(LnMixArgs ln, GemmArgs ga, WkvArgs wa, GemmArgs go,
+                                                          LnMixArgs lf, GemmArgs ka, GemmArgs va, FfnSync sy,
+                                                          FfnSync sf) {
+  int b = blockIdx.x;
+  tl_begin(ln.tl);
+  sync_stamp(sy, 0);
+  const int n_att = sy.n_ln_blocks + sy.n_key + sy.n_wkv + 16 * go.k_split;
+  if (b < n_att) {
+    if (b < sy.n_ln_blocks) {
+      if (b == 0 && threadIdx.x < sy.n_prev) sy.cnt_prev[threadIdx.x * kSyncStride] = 0;
+      if (b < sy.ln_rows) {
+        if constexpr (EMB) ln1024_body<F16, 1, 6, 0, true>(ln, b);
+        else ln1024_body<F16, 1, 6, 16>(ln, b);
+        sync_arrive(sy.cnt + kSyncStride * kAttLn, kLnReplicas);
+      }
+    } else if ((b -= sy.n_ln_blocks) < sy.n_key) {
+      gemm2_body<2, 8, kXPlanes, F16, 1, 2, false, 3>(ga, b % sy.rkv_tiles, b / sy.rkv_tiles, sy);
+    } else if ((b -= sy.n_key) < sy.n_wkv) {
+      wkv6_body<F16, 1>(wa, b, 0, sy);
+    } else {
+      gemm2_body<2, 4, kXPlanes, F16, 1, 0, false, 4>(go, b - sy.n_wkv, 0, sy);
+    }
+  } else if ((b -= n_att) < sf.n_ln_blocks) {
+    if (b < sf.ln_rows) {
+      sync_wait(sy.wo_done + kSyncStride * (blockIdx.x & (kLnReplicas - 1)), sy.wo_target, sf.err, 128, sf.opts);
+      ln1024_body<F16, 1, 1, 8, false, true>(lf, b);
+      sync_arrive(sf.cnt, kLnReplicas);
+    }
+  } else if ((b -= sf.n_ln_blocks) < sf.n_key) {
+    gemm2_body<2, 8, kXPlanes, F16, 1, 0, false, 1>(ka, b, 0, sf);
+  } else {
+    gemm2_body<2, 8, kXRelu2, F16, 4, 0, false, 2>(va, b - sf.n_key, 0, sf);
+  }
+  sync_stamp(sy, 3);
+  tl_end(ln.tl);
+}
+
+struct AttPrep {
+  LnMixArgs l;
+  GemmArgs ga, gw;
+  WkvArgs wa;
+  FfnSync sy;
+};
+static bool prep_att_persist(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs& wkv, const GemmArgs& wo, int* cnt,
+                             int* cnt_prev, int* err, int R, int H, uint64_t* stamps, int opts, AttPrep& P) {
   const bool emb = ln.emb != nullptr;
   const int rkv_tiles = rkv.seg[rkv.nseg - 1].tile_start + (rkv.seg[rkv.nseg - 1].N + 63) / 64;
   const int lora_tiles = rkv_tiles - 3 * ln.C / 64;
@@ -2453,15 +2540,22 @@ bool launch_att_persist(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs&
       wo.stamps || wo.exp || (wo.seg[0].N + 63) / 64 != 16 ||
       rkv.f16 != ln.f16 || wo.f16 != ln.f16 || wkv.f16 != ln.f16 || cnt == cnt_prev)
     return false;
-  LnMixArgs l = ln;
+  LnMixArgs& l = P.l;
+  l = ln;
   l.n_rows = R;
   l.wt = 1;
-  GemmArgs ga = rkv, gw = wo;
+  GemmArgs& ga = P.ga;
+  GemmArgs& gw = P.gw;
+  ga = rkv;
+  gw = wo;
   ga.xmap = 0; ga.ntiles = rkv_tiles; ga.wt = 1;
   gw.xmap = 1; gw.ntiles = 16;
-  WkvArgs wa = wkv;
+  gw.wt = 1;
+  WkvArgs& wa = P.wa;
+  wa = wkv;
   wa.xmap = 1; wa.wt = 1;
-  FfnSync sy{};
+  FfnSync& sy = P.sy;
+  sy = FfnSync{};
   sy.cnt = cnt;
   sy.cnt_prev = cnt_prev;
   sy.n_prev = kAttCounters;
@@ -2476,6 +2570,19 @@ bool launch_att_persist(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs&
   sy.C = ln.C;
   sy.opts = opts;
   sy.stamps = stamps;
+  return true;
+}
+
+bool launch_att_persist(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs& wkv, const GemmArgs& wo, int* cnt,
+                        int* cnt_prev, int* err, int R, int H, hipStream_t st, uint64_t* stamps, int opts) {
+  AttPrep P;
+  if (!prep_att_persist(ln, rkv, wkv, wo, cnt, cnt_prev, err, R, H, stamps, opts, P)) return false;
+  const bool emb = ln.emb != nullptr;
+  LnMixArgs& l = P.l;
+  GemmArgs& ga = P.ga;
+  GemmArgs& gw = P.gw;
+  WkvArgs& wa = P.wa;
+  FfnSync& sy = P.sy;
   const int n_wo = 16 * wo.k_split;
   const size_t lds = (size_t)2 * 16 * (8 * 32 + 8) * 2 * 2;  // the rkv body's X image (the largest)
   const dim3 grid(sy.n_ln_blocks + sy.n_key + sy.n_wkv + n_wo);
@@ -2486,6 +2593,40 @@ bool launch_att_persist(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs&
     if (emb) RT_LAUNCH((k_att_persist<false, true>), grid, dim3(256), lds, st, l, ga, wa, gw, sy);
     else RT_LAUNCH((k_att_persist<false, false>), grid, dim3(256), lds, st, l, ga, wa, gw, sy);
   }
+  return true;
+}
+
+bool launch_layer_persist(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs& wkv, const GemmArgs& wo,
+                          const LnMixArgs& lf, const GemmArgs& key, const GemmArgs& val, int* cnt, int* cnt_prev,
+                          int* err, int R, int H, hipStream_t st, uint64_t* stamps, int opts) {
+  // counter block: [0, kAttCounters) attention, [kAttCounters, +kLnReplicas) Wo done,
+  // [kLayerFfn, +kLnReplicas + kFfnSlices) FFN (FfnSync's own layout from there)
+  constexpr int kWoDone = kAttCounters, kFfn = kAttCounters + kLnReplicas;
+  AttPrep A;
+  FfnPrep F;
+  if (!prep_att_persist(ln, rkv, wkv, wo, cnt, cnt_prev, err, R, H, stamps, opts, A)) return false;
+  if (!prep_ffn_persist(lf, key, val, cnt + kSyncStride * kFfn, cnt_prev + kSyncStride * kFfn, err, R, nullptr, opts,
+                        F))
+    return false;
+  A.sy.n_prev = kFfn + kLnReplicas + kFfnSlices;  // block 0 zeroes the previous layer's whole block
+  A.sy.wo_done = cnt + kSyncStride * kWoDone;
+  A.sy.wo_target = 16 * wo.k_split;
+  F.sy.n_prev = 0;
+  const int n_att = A.sy.n_ln_blocks + A.sy.n_key + A.sy.n_wkv + 16 * wo.k_split;
+  const size_t lds = (size_t)2 * 16 * (8 * 32 + 8) * 2 * 2;
+  const dim3 grid(n_att + F.sy.n_ln_blocks + F.sy.n_key + F.nv);
+  const bool emb = ln.emb != nullptr;
+#define LP(F16_, EMB_)                                                                                       \
+  RT_LAUNCH((k_layer_persist<F16_, EMB_>), grid, dim3(256), lds, st, A.l, A.ga, A.wa, A.gw, F.l, F.ka, F.va, \
+            A.sy, F.sy)
+  if (ln.f16) {
+    if (emb) LP(true, true);
+    else LP(true, false);
+  } else {
+    if (emb) LP(false, true);
+    else LP(false, false);
+  }
+#undef LP
   return true;
 }
 

@@ -20,10 +20,14 @@ pytestmark = pytest.mark.gpu
 
 # (RWKVTTS_PERSIST_MIN_ROWS=1: the persistent forms also for the small row counts tested here;
 # by default decode steps below 16 rows take the separate launches)
-MODES = {"off": {"RWKVTTS_FFN_PERSIST": "0", "RWKVTTS_ATT_PERSIST": "0", "RWKVTTS_PERSIST_MIN_ROWS": "1"},
-         "ffn": {"RWKVTTS_FFN_PERSIST": "5", "RWKVTTS_ATT_PERSIST": "0", "RWKVTTS_PERSIST_MIN_ROWS": "1"},
-         "att": {"RWKVTTS_FFN_PERSIST": "0", "RWKVTTS_ATT_PERSIST": "5", "RWKVTTS_PERSIST_MIN_ROWS": "1"},
-         "both": {"RWKVTTS_FFN_PERSIST": "5", "RWKVTTS_ATT_PERSIST": "5", "RWKVTTS_PERSIST_MIN_ROWS": "1"}}
+# "halves": both halves persistent as two launches per layer; "both": one launch per layer
+# (k_layer_persist, the default when both halves are on)
+_M = {"RWKVTTS_PERSIST_MIN_ROWS": "1"}
+MODES = {"off": dict(_M, RWKVTTS_FFN_PERSIST="0", RWKVTTS_ATT_PERSIST="0"),
+         "ffn": dict(_M, RWKVTTS_FFN_PERSIST="5", RWKVTTS_ATT_PERSIST="0"),
+         "att": dict(_M, RWKVTTS_FFN_PERSIST="0", RWKVTTS_ATT_PERSIST="5"),
+         "halves": dict(_M, RWKVTTS_FFN_PERSIST="5", RWKVTTS_ATT_PERSIST="5", RWKVTTS_LAYER_PERSIST="0"),
+         "both": dict(_M, RWKVTTS_FFN_PERSIST="5", RWKVTTS_ATT_PERSIST="5", RWKVTTS_LAYER_PERSIST="1")}
 
 
 class _env:
@@ -51,7 +55,7 @@ def _runtime(blob, mode, **kw):
         return rwkvtts.SharedRwkvRuntime(blob, **kw)
 
 
-def _both(blob, reqs, modes=("off", "ffn", "att", "both"), **kw):
+def _both(blob, reqs, modes=("off", "ffn", "att", "halves", "both"), **kw):
     """Token streams of every mode; the recurrent state after generation must be bitwise the
     first mode's as well (a 1-ulp difference that does not flip a token is still a difference)."""
     outs, profs, ref_states = [], [], None
@@ -91,11 +95,12 @@ def test_persist_fewer_rows_and_eager(blob04):
     reqs = [make_request(synth_text(200 + i), seed=50 + i, fixed=12 + i) for i in range(5)]
     outs, profs = _both(blob04, reqs, max_slots=8, token_chunk_size=512, use_graphs=False)
     assert all(o == outs[0] for o in outs[1:])
-    b = outs[3]
+    b = outs[4]
     # the persistent launches ran (and the separate ones did not) in the decode steps
     assert "ffn_persist" in profs[1] and "ffn_persist" not in profs[0], profs[1].keys()
     assert "att_persist" in profs[2] and "wkv" in profs[0], profs[2].keys()
     assert "att_persist" in profs[3] and "ffn_persist" in profs[3], profs[3].keys()
+    assert "layer_persist" in profs[4] and "att_persist" not in profs[4], profs[4].keys()
     om = oracle.Model(blob04)
     q, keep = to_struct(reqs[2])
     g, s, _ = om.generate(q)

@@ -13,7 +13,8 @@ sys.path.insert(0, os.path.join(ROOT, "rwkv-tts-rs_amd"))
 which = sys.argv[2] if len(sys.argv) > 2 else "ffn"
 path = os.path.join(tempfile.mkdtemp(), "stamps.bin")
 os.environ["RWKVTTS_FFN_STAMPS" if which == "ffn" else "RWKVTTS_ATT_STAMPS"] = path
-os.environ.setdefault("RWKVTTS_FFN_PERSIST" if which == "ffn" else "RWKVTTS_ATT_PERSIST", "5")
+if which == "att":  # the attention launch alone (two launches per layer)
+    os.environ.setdefault("RWKVTTS_LAYER_PERSIST", "0")
 import rwkvtts  # noqa: E402
 from rwkvtts import weights as W  # noqa: E402
 
@@ -34,6 +35,8 @@ rt.close()
 a = np.fromfile(path, dtype=np.uint64).reshape(-1, 4).astype(np.float64)
 roles = ({"ln": (0, 32), "key": (32, 288), "value": (288, 544)} if which == "ffn" else
          {"ln": (0, 32), "rkv": (32, 244), "wkv": (244, 756), "wo": (756, 884)})
+if which == "layer":  # k_layer_persist: the attention blocks, then the FFN blocks
+    roles.update({"ffn_ln": (884, 916), "key": (916, 1172), "value": (1172, 1428)})
 nb = max(e for _, e in roles.values())
 t0 = a[:nb, 0][a[:nb, 0] > 0].min()
 names = ["start", "wait_done", "work_done", "end"]
