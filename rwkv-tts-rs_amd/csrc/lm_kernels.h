@@ -1,5 +1,8 @@
 // lm_kernels.h -- argument blocks and launchers of the RWKV-7 forward kernels.
 #pragma once
+#include <stddef.h>
+#include <string.h>
+
 #include "common.h"
 
 namespace rwkvtts {
@@ -60,8 +63,11 @@ struct GemmSeg {
   int tile_start;      // first 64-column tile index of this segment
 };
 
-struct GemmArgs {
-  GemmSeg seg[8];
+// NSEG_ segments and NTINFO_ tile descriptors (the arrays last, so every instantiation shares the
+// scalar fields' layout): GemmArgs (8, 128) everywhere; GemmArgs1 (1, 1) for single-segment
+// launches inside the persistent layer launch, whose kernel arguments must stay under 4 KB.
+template <int NSEG_, int NTINFO_>
+struct GemmArgsT {
   int nseg;
   int K;
   int M;               // valid rows
@@ -111,8 +117,20 @@ struct GemmArgs {
   // matrix's largest |w|) so that the lo half stays a normal f16 number; the product is scaled
   // back by 2^-q_shift in the epilogue (powers of two: exact)
   int q_shift;
-  uint32_t tinfo[128];
+  GemmSeg seg[NSEG_];
+  uint32_t tinfo[NTINFO_];
 };
+using GemmArgs = GemmArgsT<8, 128>;
+using GemmArgs1 = GemmArgsT<1, 1>;
+// a single-segment launch's arguments without the segment / descriptor tables
+inline GemmArgs1 gemm_args1(const GemmArgs& a) {
+  GemmArgs1 b;
+  static_assert(offsetof(GemmArgs, seg) == offsetof(GemmArgs1, seg), "shared scalar layout");
+  memcpy((void*)&b, (const void*)&a, offsetof(GemmArgs, seg));
+  b.seg[0] = a.seg[0];
+  b.tinfo[0] = 0;
+  return b;
+}
 
 struct WkvArgs {
   const float* part;   // [n_part][R][ldp]

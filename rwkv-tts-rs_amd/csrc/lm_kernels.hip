@@ -688,8 +688,8 @@ __device__ inline u32x4_ ld_sc1_b128(__amdgpu_buffer_rsrc_t r, int off_bytes) {
 // k_att_persist (as ROLE 1; publishes to its head's counter, or the LoRA-down counter). ROLE 4:
 // Wo workgroup (weights first, then wait for the WKV workgroups of its K-slice's two heads).
 // by: the split index of an xmap-0 grid (blockIdx.y for a plain launch).
-template <int MT, int KSTEPS, int XMODE, bool F16, int NX, int MS, bool QW, int ROLE>
-__device__ __attribute__((always_inline)) void gemm2_body(const GemmArgs& a, const int bx, const int by,
+template <int MT, int KSTEPS, int XMODE, bool F16, int NX, int MS, bool QW, int ROLE, class GA>
+__device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int bx, const int by,
                                                           const FfnSync& sy) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ uint32_t s_rexp[MT * 16];  // f16 relu^2 rows: bits of the row maximum if >= 2^15
@@ -2483,8 +2483,8 @@ __global__ __launch_bounds__(256, 2) void k_att_persist(LnMixArgs ln, GemmArgs g
 // the residual and the Wo slabs by sc1 loads. One launch boundary per layer instead of two.
 // ------------------------------------------------------------------------------------
 template <bool F16, bool EMB>
-__global__ __launch_bounds__(256, 2) void k_layer_persist(LnMixArgs ln, GemmArgs ga, WkvArgs wa, GemmArgs go,
-                                                          LnMixArgs lf, GemmArgs ka, GemmArgs va, FfnSync sy,
+__global__ __launch_bounds__(256, 2) void k_layer_persist(LnMixArgs ln, GemmArgs ga, WkvArgs wa, GemmArgs1 go,
+                                                          LnMixArgs lf, GemmArgs1 ka, GemmArgs1 va, FfnSync sy,
                                                           FfnSync sf) {
   int b = blockIdx.x;
   tl_begin(ln.tl);
@@ -2616,9 +2616,11 @@ bool launch_layer_persist(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArg
   const size_t lds = (size_t)2 * 16 * (8 * 32 + 8) * 2 * 2;
   const dim3 grid(n_att + F.sy.n_ln_blocks + F.sy.n_key + F.nv);
   const bool emb = ln.emb != nullptr;
+  const GemmArgs1 gw1 = gemm_args1(A.gw), ka1 = gemm_args1(F.ka), va1 = gemm_args1(F.va);
+  static_assert(sizeof(LnMixArgs) * 2 + sizeof(GemmArgs) + sizeof(WkvArgs) + 3 * sizeof(GemmArgs1) +
+                        2 * sizeof(FfnSync) <= 4096, "k_layer_persist's arguments must fit 4 KB");
 #define LP(F16_, EMB_)                                                                                       \
-  RT_LAUNCH((k_layer_persist<F16_, EMB_>), grid, dim3(256), lds, st, A.l, A.ga, A.wa, A.gw, F.l, F.ka, F.va, \
-            A.sy, F.sy)
+  RT_LAUNCH((k_layer_persist<F16_, EMB_>), grid, dim3(256), lds, st, A.l, A.ga, A.wa, gw1, F.l, ka1, va1, A.sy, F.sy)
   if (ln.f16) {
     if (emb) LP(true, true);
     else LP(true, false);
