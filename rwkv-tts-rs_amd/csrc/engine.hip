@@ -129,6 +129,7 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
   if (const char* fp = getenv("RWKVTTS_FFN_PERSIST")) ffn_persist_ = atoi(fp);
   if (const char* ap = getenv("RWKVTTS_ATT_PERSIST")) att_persist_ = atoi(ap);
   if (const char* lp = getenv("RWKVTTS_LAYER_PERSIST")) layer_persist_ = atoi(lp);
+  if (const char* sp = getenv("RWKVTTS_STEP_PERSIST")) step_persist_ = atoi(sp);
   if (const char* pm = getenv("RWKVTTS_PERSIST_MIN_ROWS")) persist_min_rows_ = atoi(pm);
   if ((ffn_persist_ || att_persist_) && !claim_persistent(desc.device, this)) ffn_persist_ = att_persist_ = 0;
   if (const char* gp = getenv("RWKVTTS_GEMM_STAMPS")) {
@@ -317,6 +318,8 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
   // previous layer's block)
   RT_OK(alloc(&ffn_sync_, (size_t)Lc * kFfnSyncInts));
   RT_HIP(hipMemset(ffn_sync_, 0, (size_t)Lc * kFfnSyncInts * sizeof(int)));
+  RT_OK(alloc(&step_sync_, (size_t)Lc * kStepSyncInts));  // k_step_persist's (ln_out re-zeroes them)
+  RT_HIP(hipMemset(step_sync_, 0, (size_t)Lc * kStepSyncInts * sizeof(int)));
   RT_OK(alloc(&layer_sync_, (size_t)Lc * kLayerSyncInts));  // k_layer_persist's
   RT_HIP(hipMemset(layer_sync_, 0, (size_t)Lc * kLayerSyncInts * sizeof(int)));
   RT_OK(alloc(&att_sync_, (size_t)Lc * kAttSyncInts));  // k_att_persist's, the same scheme
@@ -515,6 +518,25 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
   bool use_ffn = ffn_persist_ && inplace && big && !dbg_exp_ && Lc >= 2 && !dbg_gstamps_ && !any_quant;
   // both halves persistent: one launch per layer (k_layer_persist) unless RWKVTTS_LAYER_PERSIST=0
   bool use_layer = use_att && use_ffn && layer_persist_;
+  // ... and all layers in ONE launch (k_step_persist) with RWKVTTS_STEP_PERSIST: its argument
+  // table for R rows is built once (run_step, before a capture) by a collect pass of this function
+  bool use_step = use_layer && step_persist_;
+  if (collect_) {
+    if (!use_step) return RWKVTTS_OK;  // (no table: nothing to collect, nothing launched)
+  } else if (use_step) {
+    auto it = step_tables_.find(R);
+    if (it == step_tables_.end()) {
+      RT_OK(build_step_table(R));
+      it = step_tables_.find(R);
+    }
+    if (!it->second) {
+      use_step = false;  // shapes not covered: the per-layer launches (which fall back themselves)
+    } else {
+      prof_begin(&ev);
+      launch_step_persist(it->second, Lc, step_nb_[R], f16_ != 0, tl_next("step_persist"), stream_);
+      prof_end("step_persist", ev);
+    }
+  }
   if (!emb_fused) {
     prof_begin(&ev);
     launch_embed(d_tok_, d_rows_, &d_ctrl_[0].next_token, (int)(sizeof(SlotCtrl) / 4), emb_,
@@ -522,7 +544,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     prof_end("embed", ev);
   }
   const int64_t RC = (int64_t)Rmax_ * C;
-  for (int l = 0; l < Lc; ++l) {
+  for (int l = 0; l < Lc && !(use_step && !collect_); ++l) {
     const LayerW& w = L_[l];
     // ---- att: residual (+ previous layer's ffn partials) -> LN1 -> 6 mixes
     LnMixArgs m{};
@@ -709,6 +731,18 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     // decode steps: the whole FFN half as ONE persistent launch (k_ffn_persist, in-launch
     // hand-offs; bit-identical outputs) where the shapes allow it
     bool persisted = false;
+    if (collect_) {  // building the one-launch step's argument table (no launches)
+      LayerArgs la;
+      if (!prep_layer_args(m, g, k, go, f, gk, gv, step_sync_ + (size_t)l * kStepSyncInts,
+                           l == 0 ? nullptr : step_sync_ + (size_t)(l - 1) * kStepSyncInts, (int*)(d_ctrl_ + S_), R,
+                           H_, att_persist_ >> 1, la)) {
+        RT_CHECK(l == 0, RWKVTTS_EHIP, "one-launch step: a layer after layer 0 is not covered");
+        collect_->clear();  // layer 0 not covered: no table
+        return RWKVTTS_OK;
+      }
+      collect_->push_back(la);
+      continue;
+    }
     if (use_layer) {
       f.tl = gk.tl = gv.tl = m.tl = g.tl = k.tl = go.tl = tl_next("layer_persist");
       prof_begin(&ev);
@@ -778,6 +812,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
       prof_end("gemm_ffn_value", ev);
     }
   }
+  if (collect_) return RWKVTTS_OK;
   if (n_lg > 0) {
     LnMixArgs o{};
     o.f16 = f16_;
@@ -797,6 +832,10 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     o.shift = nullptr;
     o.C = C;
     o.row_map = d_lg_rows_;
+    if (use_step) {  // the step launch's hand-off counters, zero again for the next step
+      o.zero = step_sync_;
+      o.zero_n = Lc * (kStepSyncInts / kSyncStride);
+    }
     o.tl = tl_next("ln_out");
     prof_begin(&ev);
     launch_ln_mix(o, n_lg, stream_);
@@ -852,6 +891,25 @@ int Engine::upload_plan(const StepPlan& p) {
 }
 
 // Runs one forward step. Decode steps (tok_from_ctrl) replay a cached hipGraph.
+int Engine::build_step_table(int R) {
+  std::vector<LayerArgs> v;
+  collect_ = &v;
+  const int rc = launch_forward(R, R, R, std::min(8193, dims.n_vocab), true, true);
+  collect_ = nullptr;
+  RT_OK(rc);
+  if (v.empty()) {  // the one-launch form does not apply to R rows: remembered, no step launch
+    step_tables_[R] = nullptr;
+    return RWKVTTS_OK;
+  }
+  RT_CHECK((int)v.size() == dims.n_layer, RWKVTTS_EHIP, "one-launch step: a layer fell back");
+  LayerArgs* d = nullptr;
+  RT_OK(alloc(&d, v.size()));
+  RT_HIP(hipMemcpy(d, v.data(), sizeof(LayerArgs) * v.size(), hipMemcpyHostToDevice));
+  step_tables_[R] = d;
+  step_nb_[R] = step_blocks_per_layer(v[0]);
+  return RWKVTTS_OK;
+}
+
 int Engine::set_graph_timing(bool on) {
   RT_HIP(hipSetDevice(device_));
   if (on && !d_gt_) {
@@ -879,6 +937,9 @@ int Engine::run_step(const StepPlan& p, bool upload) {
     auto key = std::make_pair(R, p.head_rows * 2 + (p.advance ? 1 : 0));
     auto it = graphs_.find(key);
     if (it == graphs_.end()) {
+      // the one-launch step's argument table is uploaded before the capture (no synchronous copy
+      // may happen inside it)
+      if (step_persist_ && !step_tables_.count(R)) RT_OK(build_step_table(R));
       // one capture at a time per process: engines owned by different threads (the manager's
       // workers) never capture / instantiate concurrently
       static std::mutex capture_mu;

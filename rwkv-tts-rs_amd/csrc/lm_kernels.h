@@ -51,6 +51,10 @@ struct LnMixArgs {
   const float* ln0_w;
   const float* ln0_b;
   int n_vocab;
+  // ln_out after a one-launch decode step (k_step_persist): block 0 zeroes zero_n hand-off counters
+  // (64 ints apart) from zero, for the next step's launch
+  int* zero;
+  int zero_n;
 };
 
 struct GemmSeg {
@@ -174,6 +178,61 @@ int launch_gemm(const GemmArgs& a, hipStream_t st);
 // The FFN half of a decode step (LN2 + mix, key GEMM, relu^2, value GEMM) as ONE persistent launch
 // with in-launch hand-offs (k_ffn_persist); false if the shapes are not covered.
 constexpr int kFfnSyncInts = 24 * 64;  // counter block per layer: (8 LN replicas + 16 K-slices) x 256 B
+// ---- persistent launches: hand-off counters and their arguments (lm_kernels.hip) ----------
+// Inter-workgroup hand-offs of the persistent FFN launch (k_ffn_persist): counters kSyncStride
+// ints (256 B) apart (see lm_kernels.hip for each launch's layout).
+constexpr int kSyncStride = 64;
+constexpr int kLnReplicas = 8;
+constexpr int kFfnSlices = 16;  // value K-slices (F / 256 at the 0.4B shape)
+// counter blocks (kSyncStride-int units) of the persistent attention launch (k_att_persist)
+constexpr int kAttLn = 0;      // kLnReplicas: LayerNorm rows published
+constexpr int kAttHead = 8;    // 16: head h's r / k / v tiles published (3 tiles x the K-splits)
+constexpr int kAttLora = 24;   // kLnReplicas: the LoRA-down tiles published
+constexpr int kAttWkv = 32;    // 16: WKV workgroups of head h done (one per row)
+constexpr int kAttCounters = 48;
+struct FfnSync {     // (both persistent launches)
+  int* cnt;          // this layer's counters (zero at launch)
+  int* cnt_prev;     // the counters of the layer launched before this one: zeroed by block 0
+  int n_prev;        // counters to zero there
+  int* err;          // give-up word: a bounded wait that timed out ORs its code in
+  int n_ln_blocks;   // LayerNorm blocks (rows rounded up to 8: the GEMM blocks keep their XCD order)
+  int ln_rows;       // LayerNorm rows the GEMM workgroups wait for
+  int n_key;         // FFN: key workgroups; attention: rkv workgroups
+  int key_group;     // FFN: key column tiles per value K-slice
+  int key_per_slice; // FFN: key workgroups per value K-slice (key_group x key splits)
+  int n_wkv;         // attention: WKV workgroups
+  int rkv_tiles;     // attention: column tiles of the rkv launch (its grid is tiles x splits)
+  int head_target;   // attention: rkv workgroups per head (3 tiles x splits)
+  int lora_target;   // attention: LoRA-down workgroups (tiles x splits)
+  int C;             // attention: channels (r / k / v columns [0, 3C), LoRA-down beyond)
+  int* val_done;     // one-launch step: FFN value workgroups count into shard blockIdx % 8 ...
+  const int* prev_val_done;  // ... and the next layer's LN1 rows wait for the sum of the 8 shards
+  int val_target;    //     of the previous layer (= its value workgroups)
+  int* wo_done;      // one-launch layer: Wo workgroups count in here (kLnReplicas replicas) ...
+  int wo_target;     // ... and the FFN LayerNorm rows wait for all of them
+  int opts;          // bit 0: value workgroups request their weights only once the LN rows are
+                     // published (not at dispatch); bit 1: longer sleep between polls; bit 2: key
+                     // workgroups request their weights after the LN wait (with their X)
+  uint64_t* stamps;  // debug (RWKVTTS_FFN_STAMPS): [block][4] s_memrealtime: start, wait done, work
+                     // done, end (null in production)
+};
+
+// one layer's arguments of the one-launch decode step (k_step_persist reads them from a device table)
+struct LayerArgs {
+  LnMixArgs ln;      // LN1 + mixes (layer 0: the embedding form)
+  GemmArgs ga;       // rkv + LoRA-down
+  WkvArgs wa;
+  GemmArgs1 go;      // Wo
+  LnMixArgs lf;      // LN2 + mix
+  GemmArgs1 ka, va;  // FFN key / value
+  FfnSync sy, sf;
+};
+constexpr int kStepSyncInts = (48 + 8 + 8 + 16 + 8) * 64;  // layer block + value-done shards
+bool prep_layer_args(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs& wkv, const GemmArgs& wo,
+                     const LnMixArgs& lf, const GemmArgs& key, const GemmArgs& val, int* cnt, const int* prev_cnt,
+                     int* err, int R, int H, int opts, LayerArgs& out);
+void launch_step_persist(const LayerArgs* dT, int n_layers, int nb, bool f16, unsigned long long* tl, hipStream_t st);
+int step_blocks_per_layer(const LayerArgs& a);
 // The attention half of a decode step (LN1 + mixes, rkv + LoRA-down, WKV, Wo) as ONE persistent
 // launch (k_att_persist); false if the shapes are not covered.
 constexpr int kAttSyncInts = 48 * 64;  // counter block per layer (lm_kernels.hip kAtt*)

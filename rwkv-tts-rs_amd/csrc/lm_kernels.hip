@@ -426,6 +426,8 @@ __device__ __attribute__((always_inline)) void ln1024_body(const LnMixArgs& a, c
 template <bool F16, int MODE, int NMIX, int NP, bool EMB = false>
 __global__ __launch_bounds__(256) void k_ln1024(LnMixArgs a) {
   tl_begin(a.tl);
+  if (a.zero && blockIdx.x == 0)
+    for (int i = threadIdx.x; i < a.zero_n; i += 256) a.zero[i * 64] = 0;
   ln1024_body<F16, MODE, NMIX, NP, EMB>(a, blockIdx.x);
   tl_end(a.tl);
 }
@@ -616,38 +618,6 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
 // per XCD: every LN workgroup adds to all of them, a key workgroup polls replica blockIdx % 8, so
 // 512 pollers do not share one line), [kSyncStride * (kLnReplicas + s)] = key workgroups that
 // published their partial slab of value K-slice s.
-constexpr int kSyncStride = 64;
-constexpr int kLnReplicas = 8;
-constexpr int kFfnSlices = 16;  // value K-slices (F / 256 at the 0.4B shape)
-// counter blocks (kSyncStride-int units) of the persistent attention launch (k_att_persist)
-constexpr int kAttLn = 0;      // kLnReplicas: LayerNorm rows published
-constexpr int kAttHead = 8;    // 16: head h's r / k / v tiles published (3 tiles x the K-splits)
-constexpr int kAttLora = 24;   // kLnReplicas: the LoRA-down tiles published
-constexpr int kAttWkv = 32;    // 16: WKV workgroups of head h done (one per row)
-constexpr int kAttCounters = 48;
-struct FfnSync {     // (both persistent launches)
-  int* cnt;          // this layer's counters (zero at launch)
-  int* cnt_prev;     // the counters of the layer launched before this one: zeroed by block 0
-  int n_prev;        // counters to zero there
-  int* err;          // give-up word: a bounded wait that timed out ORs its code in
-  int n_ln_blocks;   // LayerNorm blocks (rows rounded up to 8: the GEMM blocks keep their XCD order)
-  int ln_rows;       // LayerNorm rows the GEMM workgroups wait for
-  int n_key;         // FFN: key workgroups; attention: rkv workgroups
-  int key_group;     // FFN: key column tiles per value K-slice
-  int key_per_slice; // FFN: key workgroups per value K-slice (key_group x key splits)
-  int n_wkv;         // attention: WKV workgroups
-  int rkv_tiles;     // attention: column tiles of the rkv launch (its grid is tiles x splits)
-  int head_target;   // attention: rkv workgroups per head (3 tiles x splits)
-  int lora_target;   // attention: LoRA-down workgroups (tiles x splits)
-  int C;             // attention: channels (r / k / v columns [0, 3C), LoRA-down beyond)
-  int* wo_done;      // one-launch layer: Wo workgroups count in here (kLnReplicas replicas) ...
-  int wo_target;     // ... and the FFN LayerNorm rows wait for all of them
-  int opts;          // bit 0: value workgroups request their weights only once the LN rows are
-                     // published (not at dispatch); bit 1: longer sleep between polls; bit 2: key
-                     // workgroups request their weights after the LN wait (with their X)
-  uint64_t* stamps;  // debug (RWKVTTS_FFN_STAMPS): [block][4] s_memrealtime: start, wait done, work
-                     // done, end (null in production)
-};
 __device__ inline void sync_stamp(const FfnSync& sy, int slot) {
   if (sy.stamps && threadIdx.x == 0) sy.stamps[blockIdx.x * 4 + slot] = __builtin_amdgcn_s_memrealtime();
 }
@@ -661,6 +631,24 @@ __device__ inline void sync_wait(const int* c, int target, int* err, int code, i
     while (__hip_atomic_load((gint_t*)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
       if (opts & 2) __builtin_amdgcn_s_sleep(8);
       else __builtin_amdgcn_s_sleep(1);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 5000000ull) {
+        __hip_atomic_fetch_or((gint_t*)err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+// wait until the sum of `shards` counters (kSyncStride ints apart) reaches target (one lane polls)
+__device__ inline void sync_wait_sum(const int* c, int shards, int target, int* err, int code) {
+  if (threadIdx.x == 0) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+      int sum = 0;
+      for (int i = 0; i < shards; ++i)
+        sum += __hip_atomic_load((gint_t*)(c + i * kSyncStride), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (sum >= target) break;
+      __builtin_amdgcn_s_sleep(8);
       if (__builtin_amdgcn_s_memrealtime() - t0 > 5000000ull) {
         __hip_atomic_fetch_or((gint_t*)err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
@@ -1084,6 +1072,9 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
   }
   if constexpr (ROLE != 0) sync_stamp(sy, 2);
   if constexpr (ROLE == 1) sync_arrive(sy.cnt + kSyncStride * (kLnReplicas + tile / sy.key_group));
+  if constexpr (ROLE == 2) {
+    if (sy.val_done) sync_arrive(sy.val_done + kSyncStride * (blockIdx.x & (kLnReplicas - 1)));
+  }
   if constexpr (ROLE == 4) {
     if (sy.wo_done) sync_arrive(sy.wo_done, kLnReplicas);
   }
@@ -2232,7 +2223,12 @@ __device__ __attribute__((always_inline)) void wkv6_body(const WkvArgs& a, const
       vp[p] = pp[2 * C + c];
     }
     }
-    vf = a.layer > 0 ? a.v_first[(int64_t)row * a.ldv + c] : 0.f;
+    if constexpr (ROLE == 1)  // (layer 0's WKV may have written it in this same launch: k_step_persist)
+      vf = a.layer > 0 ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                     wt_rsrc(a.v_first + (int64_t)row * a.ldv), c * 4, 0, 16))
+                       : 0.f;
+    else
+      vf = a.layer > 0 ? a.v_first[(int64_t)row * a.ldv + c] : 0.f;
   };
   // issue order = need order (vmcnt retires in order): partials (hidden nonlinearity), then the
   // LoRA-up rows (LoRA / mixing phase), then the state (update phase)
@@ -2322,7 +2318,10 @@ __device__ __attribute__((always_inline)) void wkv6_body(const WkvArgs& a, const
     const float kk = k * kkc;
     k = k * (1.0f + (av - 1.0f) * kac);
     if (a.layer == 0) {
-      if (qq == 0) a.v_first[(int64_t)row * a.ldv + c] = v;
+      if (qq == 0) {
+        if constexpr (ROLE == 1) store_wt(wt_rsrc(a.v_first + (int64_t)row * a.ldv), c * 4, v);
+        else a.v_first[(int64_t)row * a.ldv + c] = v;
+      }
     } else {
       v = v + (vf_row - v) * fsigm(v0 + lo2);
     }
@@ -2573,6 +2572,54 @@ static bool prep_att_persist(const LnMixArgs& ln, const GemmArgs& rkv, const Wkv
   return true;
 }
 
+// ------------------------------------------------------------------------------------
+// step_persist: a decode step's 24 layers as ONE launch: layer l's k_layer_persist blocks at
+// [l * nb, (l + 1) * nb), their arguments read from a device table (LayerArgs[L]); layer l's LN1
+// rows wait for the previous layer's FFN value workgroups (8 shards) and read its residual and
+// slabs by sc1 loads. Counters are zeroed by the ln_out launch that follows (LnMixArgs::zero).
+// ------------------------------------------------------------------------------------
+template <bool F16>
+__global__ __launch_bounds__(256, 2) void k_step_persist(const LayerArgs* __restrict__ T, int nb,
+                                                         unsigned long long* tl) {
+  const int layer = blockIdx.x / nb;
+  int b = blockIdx.x - layer * nb;
+  const LayerArgs& A = T[layer];
+  const FfnSync& sy = A.sy;
+  const FfnSync& sf = A.sf;
+  tl_begin(tl);
+  const int n_att = sy.n_ln_blocks + sy.n_key + sy.n_wkv + 16 * A.go.k_split;
+  if (b < n_att) {
+    if (b < sy.n_ln_blocks) {
+      if (b < sy.ln_rows) {
+        if (layer == 0) {
+          ln1024_body<F16, 1, 6, 0, true>(A.ln, b);
+        } else {
+          sync_wait_sum(sy.prev_val_done, kLnReplicas, sy.val_target, sy.err, 256);
+          ln1024_body<F16, 1, 6, 16, false, true>(A.ln, b);
+        }
+        sync_arrive(sy.cnt + kSyncStride * kAttLn, kLnReplicas);
+      }
+    } else if ((b -= sy.n_ln_blocks) < sy.n_key) {
+      gemm2_body<2, 8, kXPlanes, F16, 1, 2, false, 3>(A.ga, b % sy.rkv_tiles, b / sy.rkv_tiles, sy);
+    } else if ((b -= sy.n_key) < sy.n_wkv) {
+      wkv6_body<F16, 1>(A.wa, b, 0, sy);
+    } else {
+      gemm2_body<2, 4, kXPlanes, F16, 1, 0, false, 4>(A.go, b - sy.n_wkv, 0, sy);
+    }
+  } else if ((b -= n_att) < sf.n_ln_blocks) {
+    if (b < sf.ln_rows) {
+      sync_wait(sy.wo_done + kSyncStride * (blockIdx.x & (kLnReplicas - 1)), sy.wo_target, sf.err, 128, sf.opts);
+      ln1024_body<F16, 1, 1, 8, false, true>(A.lf, b);
+      sync_arrive(sf.cnt, kLnReplicas);
+    }
+  } else if ((b -= sf.n_ln_blocks) < sf.n_key) {
+    gemm2_body<2, 8, kXPlanes, F16, 1, 0, false, 1>(A.ka, b, 0, sf);
+  } else {
+    gemm2_body<2, 8, kXRelu2, F16, 4, 0, false, 2>(A.va, b - sf.n_key, 0, sf);
+  }
+  tl_end(tl);
+}
+
 bool launch_att_persist(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs& wkv, const GemmArgs& wo, int* cnt,
                         int* cnt_prev, int* err, int R, int H, hipStream_t st, uint64_t* stamps, int opts) {
   AttPrep P;
@@ -2630,6 +2677,52 @@ bool launch_layer_persist(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArg
   }
 #undef LP
   return true;
+}
+
+// One layer of the one-launch step: its k_layer_persist arguments plus the layer-to-layer hand-off
+// (this layer's value-done shards, the previous layer's to wait for). cnt: this layer's
+// kStepSyncInts block; prev_cnt: the previous layer's (null for layer 0). No zeroing in-launch.
+bool prep_layer_args(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs& wkv, const GemmArgs& wo,
+                     const LnMixArgs& lf, const GemmArgs& key, const GemmArgs& val, int* cnt, const int* prev_cnt,
+                     int* err, int R, int H, int opts, LayerArgs& out) {
+  constexpr int kWoDone = kAttCounters, kFfn = kAttCounters + kLnReplicas, kValDone = kFfn + kLnReplicas + kFfnSlices;
+  AttPrep A;
+  FfnPrep F;
+  int* dummy_prev = cnt + kSyncStride * 1;  // (prep requires cnt != cnt_prev; n_prev = 0 below)
+  if (!prep_att_persist(ln, rkv, wkv, wo, cnt, dummy_prev, err, R, H, nullptr, opts, A)) return false;
+  if (!prep_ffn_persist(lf, key, val, cnt + kSyncStride * kFfn, dummy_prev, err, R, nullptr, opts, F)) return false;
+  if ((prev_cnt == nullptr) != (ln.emb != nullptr)) return false;  // layer 0 (embedding form) has no predecessor
+  A.sy.n_prev = 0;
+  A.sy.cnt_prev = nullptr;
+  A.sy.wo_done = cnt + kSyncStride * kWoDone;
+  A.sy.wo_target = 16 * wo.k_split;
+  A.sy.prev_val_done = prev_cnt ? prev_cnt + kSyncStride * kValDone : nullptr;
+  A.sy.val_target = F.nv;
+  F.sy.n_prev = 0;
+  F.sy.cnt_prev = nullptr;
+  F.sy.val_done = cnt + kSyncStride * kValDone;
+  out.ln = A.l;
+  out.ga = A.ga;
+  out.wa = A.wa;
+  out.go = gemm_args1(A.gw);
+  out.lf = F.l;
+  out.ka = gemm_args1(F.ka);
+  out.va = gemm_args1(F.va);
+  out.sy = A.sy;
+  out.sf = F.sy;
+  return true;
+}
+
+int step_blocks_per_layer(const LayerArgs& a) {
+  return a.sy.n_ln_blocks + a.sy.n_key + a.sy.n_wkv + 16 * a.go.k_split + a.sf.n_ln_blocks + a.sf.n_key +
+         (a.va.seg[0].N + 63) / 64 * a.va.k_split;
+}
+
+void launch_step_persist(const LayerArgs* dT, int n_layers, int nb, bool f16, unsigned long long* tl, hipStream_t st) {
+  const size_t lds = (size_t)2 * 16 * (8 * 32 + 8) * 2 * 2;
+  const dim3 grid(n_layers * nb);
+  if (f16) RT_LAUNCH((k_step_persist<true>), grid, dim3(256), lds, st, dT, nb, tl);
+  else RT_LAUNCH((k_step_persist<false>), grid, dim3(256), lds, st, dT, nb, tl);
 }
 
 int wkv_perm_layout(int Dw, int Da, int Dv, int Dg, int n_part, int max_slots, int variant) {

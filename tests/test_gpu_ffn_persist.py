@@ -21,13 +21,16 @@ pytestmark = pytest.mark.gpu
 # (RWKVTTS_PERSIST_MIN_ROWS=1: the persistent forms also for the small row counts tested here;
 # by default decode steps below 16 rows take the separate launches)
 # "halves": both halves persistent as two launches per layer; "both": one launch per layer
-# (k_layer_persist, the default when both halves are on)
+# (k_layer_persist); "step": one launch per decode step (k_step_persist)
 _M = {"RWKVTTS_PERSIST_MIN_ROWS": "1"}
 MODES = {"off": dict(_M, RWKVTTS_FFN_PERSIST="0", RWKVTTS_ATT_PERSIST="0"),
          "ffn": dict(_M, RWKVTTS_FFN_PERSIST="5", RWKVTTS_ATT_PERSIST="0"),
          "att": dict(_M, RWKVTTS_FFN_PERSIST="0", RWKVTTS_ATT_PERSIST="5"),
          "halves": dict(_M, RWKVTTS_FFN_PERSIST="5", RWKVTTS_ATT_PERSIST="5", RWKVTTS_LAYER_PERSIST="0"),
-         "both": dict(_M, RWKVTTS_FFN_PERSIST="5", RWKVTTS_ATT_PERSIST="5", RWKVTTS_LAYER_PERSIST="1")}
+         "both": dict(_M, RWKVTTS_FFN_PERSIST="5", RWKVTTS_ATT_PERSIST="5", RWKVTTS_LAYER_PERSIST="1",
+                      RWKVTTS_STEP_PERSIST="0"),
+         "step": dict(_M, RWKVTTS_FFN_PERSIST="5", RWKVTTS_ATT_PERSIST="5", RWKVTTS_LAYER_PERSIST="1",
+                      RWKVTTS_STEP_PERSIST="1")}
 
 
 class _env:
@@ -55,7 +58,7 @@ def _runtime(blob, mode, **kw):
         return rwkvtts.SharedRwkvRuntime(blob, **kw)
 
 
-def _both(blob, reqs, modes=("off", "ffn", "att", "halves", "both"), **kw):
+def _both(blob, reqs, modes=("off", "ffn", "att", "halves", "both", "step"), **kw):
     """Token streams of every mode; the recurrent state after generation must be bitwise the
     first mode's as well (a 1-ulp difference that does not flip a token is still a difference)."""
     outs, profs, ref_states = [], [], None
@@ -101,6 +104,7 @@ def test_persist_fewer_rows_and_eager(blob04):
     assert "att_persist" in profs[2] and "wkv" in profs[0], profs[2].keys()
     assert "att_persist" in profs[3] and "ffn_persist" in profs[3], profs[3].keys()
     assert "layer_persist" in profs[4] and "att_persist" not in profs[4], profs[4].keys()
+    assert "step_persist" in profs[5] and "layer_persist" not in profs[5], profs[5].keys()
     om = oracle.Model(blob04)
     q, keep = to_struct(reqs[2])
     g, s, _ = om.generate(q)
