@@ -17,6 +17,7 @@ DECODE = {
     # 32 LN + 256 key + 256 value blocks of 256 threads
     "att_persist": (("k_att_persist<false, true>", "k_att_persist<false, false>"), 884 * 256),
     "ffn_persist": (("k_ffn_persist<false>",), 544 * 256),
+    "layer_persist": (("k_layer_persist<false, true>", "k_layer_persist<false, false>"), 1428 * 256),
 }
 
 
