@@ -178,6 +178,8 @@ def main():
                     help="prompt rows per engine step (all admitted prompts share it; outputs are chunk-invariant, bitwise)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-batch1", action="store_true", help="skip the config-2 (one request) leg")
+    ap.add_argument("--voc-delay-ms", type=float, default=0.0,
+                    help="start each batch's vocoder this long after its LM finished (pipelining A/B)")
     ap.add_argument("--no-graph-timing", dest="graph_timing", action="store_false",
                     help="per-kernel times from an eager HIP-event pass instead of in-graph stamps")
     ap.add_argument("--profile", action="store_true", help="per-kernel HIP-event pass (default on)")
@@ -270,6 +272,8 @@ def main():
     from concurrent.futures import ThreadPoolExecutor
 
     def vocode(out):
+        if args.voc_delay_ms > 0:  # start after the next batch's prefill (A/B switch)
+            time.sleep(args.voc_delay_ms / 1000.0)
         pcm = voc.decode_audio_batch([(g, s) for g, s in out])
         assert sum(p.size for p in pcm) == 320 * sum(len(s) for _, s in out), "vocoder output length mismatch"
         return len(pcm)

@@ -55,6 +55,10 @@ struct ConvArgs {
   const float* bias1;
   const int* ntok;     // tokens per utterance; input length = ntok * tin_mul
   const bf16_t* zeros; // >= 16 zero bytes (source of out-of-range window rows)
+  // channel-blocked planes: [C / 32][rows][32] per utterance, the chunk stride (rows * 32 elements)
+  // given; 0: channel-last [t][C]. A 32-channel chunk's window is then one contiguous run of
+  // 64-B rows instead of 64 B out of every C * 2-B row.
+  int64_t x_cs, y_cs;
   // XCD-aware 1-D grid (xmap = 1): the gy column tiles of time tile x run back to back on one XCD
   // (blocks b and b + 8 share one), so the input window they all read is fetched into that XCD's
   // L2 once instead of once per column tile
@@ -153,8 +157,11 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? 1 : 2) void k_conv(ConvArgs a)
 
   // This wave's share of the chunk's 16-row blocks: per-lane source pointers at channel 0,
   // computed once (a chunk adds c0); out-of-range window rows read the zero page.
+  // amask: blocks u of in-range window rows (they advance by the input's chunk stride; weight
+  // and zero-page rows advance by 32 channels)
   constexpr int MAXB = 16;
   const bf16_t* srcp[MAXB];
+  uint32_t amask = 0;
 #pragma unroll
   for (int u = 0; u < MAXB; ++u) {
     const int b = wave + NWV * u;
@@ -162,8 +169,12 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? 1 : 2) void k_conv(ConvArgs a)
     if (b < nAblk) {
       const int plane = b >= WRp / 16, row = (b - plane * (WRp / 16)) * 16 + lrow;
       const int piece = lslot ^ ((row >> 1) & 3), pos = wstart + row;
-      if (pos >= 0 && pos < Tin) src = (plane ? a.xl : a.xh) + xoff + (int64_t)pos * a.Ci + piece * 8;
-      else src = a.zeros + piece * 8;
+      if (pos >= 0 && pos < Tin) {
+        src = (plane ? a.xl : a.xh) + xoff + (int64_t)pos * (a.x_cs ? 32 : a.Ci) + piece * 8;
+        amask |= 1u << u;
+      } else {
+        src = a.zeros + piece * 8;
+      }
     } else if (b < nblk) {
       const int wb0 = b - nAblk, lo = wb0 >= nWblk, wb = wb0 - (lo ? nWblk : 0);
       const int tap = wb / (TN / 16), co = (wb % (TN / 16)) * 16 + lrow;
@@ -173,11 +184,11 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? 1 : 2) void k_conv(ConvArgs a)
     srcp[u] = src;
   }
   auto issue = [&](int ck, uint8_t* buf) {
-    const int c0 = ck * 32;
+    const int64_t c0 = ck * 32, aoff = a.x_cs ? ck * a.x_cs : c0;
 #pragma unroll
     for (int u = 0; u < MAXB; ++u) {
       const int b = wave + NWV * u;
-      if (b < nblk) glds16(srcp[u] + c0, buf + b * 1024);
+      if (b < nblk) glds16(srcp[u] + (((amask >> u) & 1) ? aoff : c0), buf + b * 1024);
     }
   };
 
@@ -348,6 +359,7 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? 1 : 2) void k_conv(ConvArgs a)
     }
     if (a.y) *(float4_*)(a.y + o) = v;
     if (a.yh) {
+      const int64_t op = a.y_cs ? yoff + ((co0 + c4) >> 5) * a.y_cs + (int64_t)(q * ostr + phase) * 32 + ((co0 + c4) & 31) : o;
       uint16_t h[4], l[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -355,8 +367,8 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? 1 : 2) void k_conv(ConvArgs a)
         h[e] = f32_to_bf16(pv);
         l[e] = f32_to_bf16(pv - bf16_to_f32(h[e]));
       }
-      *(uint2*)(a.yh + o) = make_uint2(h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16));
-      *(uint2*)(a.yl + o) = make_uint2(l[0] | ((uint32_t)l[1] << 16), l[2] | ((uint32_t)l[3] << 16));
+      *(uint2*)(a.yh + op) = make_uint2(h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16));
+      *(uint2*)(a.yl + op) = make_uint2(l[0] | ((uint32_t)l[1] << 16), l[2] | ((uint32_t)l[3] << 16));
     }
   }
 }
@@ -473,8 +485,8 @@ __global__ __launch_bounds__(128) void k_dw_ln(const float* x, float* y, bf16_t*
 // global loads (8 channels per load and plane; C % 8 == 0) at row stride C + 1 (conflict-free
 // walks); each thread then walks its 7 x C window against the weights (scalar operands).
 constexpr int kOutT = 256;
-__global__ __launch_bounds__(256) void k_conv_out(const bf16_t* xh, const bf16_t* xl, int64_t x_bs, int C,
-                                                  int tin_mul, const int* ntok, const float* w,
+__global__ __launch_bounds__(256) void k_conv_out(const bf16_t* xh, const bf16_t* xl, int64_t x_bs, int64_t x_cs,
+                                                  int C, int tin_mul, const int* ntok, const float* w,
                                                   const float* b, float* pcm, int64_t p_bs) {
   extern __shared__ float s_x[];
   const int req = blockIdx.y, T = ntok[req] * tin_mul, t0 = blockIdx.x * kOutT;
@@ -485,7 +497,7 @@ __global__ __launch_bounds__(256) void k_conv_out(const bf16_t* xh, const bf16_t
     const int r = i / c8n, c8 = (i - r * c8n) * 8, p = t0 - 3 + r;
     float* dst = s_x + r * LDX + c8;
     if (p >= 0 && p < T) {
-      const int64_t o = xo + (int64_t)p * C + c8;
+      const int64_t o = x_cs ? xo + (c8 >> 5) * x_cs + (int64_t)p * 32 + (c8 & 31) : xo + (int64_t)p * C + c8;
       const uint4 h = *(const uint4*)(xh + o), l = *(const uint4*)(xl + o);
       const uint32_t hw[4] = {h.x, h.y, h.z, h.w}, lw[4] = {l.x, l.y, l.z, l.w};
 #pragma unroll
@@ -525,6 +537,7 @@ __global__ void k_f32_split_bf16(const float* in, bf16_t* hi, bf16_t* lo, int64_
 struct Planes {  // activated activations as bf16 hi + lo (x = hi + lo)
   bf16_t* h = nullptr;
   bf16_t* l = nullptr;
+  int64_t cs = 0;  // channel-blocked layout's chunk stride (ConvArgs::x_cs); 0: channel-last
 };
 
 class Codec {
@@ -791,6 +804,7 @@ class Codec {
     a.mode = mode; a.dil = dil; a.pad = pad; a.s = s; a.bias = bias; a.rbias = o.rbias; a.rb_bs = o.rb_bs;
     a.gamma = o.gamma; a.res = o.res; a.act = o.act; a.y = o.y; a.yh = o.p.h; a.yl = o.p.l;
     a.y_alpha = o.alpha; a.y_bs = o.y_bs >= 0 ? o.y_bs : bs; a.ntok = d_ntok; a.zeros = zeros;
+    a.x_cs = x.cs; a.y_cs = o.p.cs;
     const int phases = mode == 1 ? s : 1;
     dim3 grid((unsigned)((Tmax * (int64_t)tin_mul + TM - 1) / TM), (unsigned)(phases * (Co / TN)), (unsigned)n);
     // XCD-aware order for the long-time-axis residual convs (conv7 and conv1 at >= 32 time tiles:
@@ -854,6 +868,7 @@ class Codec {
     a.gamma = nullptr; a.res = o.res; a.act = 0; a.y = o.y; a.yh = o.p.h; a.yl = o.p.l;
     a.y_alpha = o.alpha; a.y_bs = o.y_bs >= 0 ? o.y_bs : bs; a.ntok = d_ntok; a.zeros = zeros;
     a.mid_alpha = mid_alpha; a.w1 = w1; a.bias1 = b1;
+    a.x_cs = x.cs; a.y_cs = o.p.cs;
     a.xmap = 0;
     dim3 grid((unsigned)((Tmax * (int64_t)tin_mul + TM - 1) / TM), 1, (unsigned)n);
     pbeg();
@@ -980,11 +995,20 @@ class Codec {
                      F(0, 0, CD_LIN_B), o))) return rc;
     }
     // WaveGenerator: conv_in -> [snake -> convT -> 3 x residual unit] x n_up -> snake -> conv_out
+    // Its planes are channel-blocked ([C / 32][Tmax * mul][32] per utterance) unless
+    // RWKVTTS_CODEC_BLK=0 (A/B switch, read per call; the arithmetic is the same either way)
     const int64_t bs = (int64_t)Tmax * big_per_tok;
+    const char* blk_env = getenv("RWKVTTS_CODEC_BLK");
+    const bool blk = !blk_env || atoi(blk_env) != 0;
+    auto PB = [&](int i, int m) {  // pp[i] holding a tensor of Tmax * m rows
+      Planes q = pp[i];
+      q.cs = blk ? (int64_t)Tmax * m * 32 : 0;
+      return q;
+    };
     int C = d.dec_channels, mul = 1, cur = 0;
     {
       ConvOut o;
-      o.p = pp[cur];
+      o.p = PB(cur, 1);
       o.alpha = F(2, 0, CU_SNAKE);
       // conv_in reads the prenet planes with the prenet's per-utterance stride
       o.y_bs = bs;
@@ -996,9 +1020,9 @@ class Codec {
       const int Co = C / 2, s = d.up_rates[ub], K = d.up_kernels[ub];
       ConvOut ot;
       ot.y = xf;
-      ot.p = pp[cur ^ 1];
+      ot.p = PB(cur ^ 1, mul * s);
       ot.alpha = F(2, ub, CU_R0_A1);
-      if ((rc = conv(n, Tmax, stage_name("codec_convT", Co), pp[cur], bs, C, mul, B(2, ub, CU_T_W), K, Co, 1, 1, 0, s,
+      if ((rc = conv(n, Tmax, stage_name("codec_convT", Co), PB(cur, mul), bs, C, mul, B(2, ub, CU_T_W), K, Co, 1, 1, 0, s,
                      F(2, ub, CU_T_B), ot))) return rc;
       cur ^= 1;
       mul *= s;
@@ -1009,11 +1033,11 @@ class Codec {
           ConvOut of;
           of.y = r < 2 ? xf : nullptr;
           of.res = xf;
-          of.p = pp[cur ^ 1];
+          of.p = PB(cur ^ 1, mul);
           of.alpha = r < 2 ? F(2, ub, CU_R0_A1 + o + (CU_R1_A1 - CU_R0_A1))
                            : (ub + 1 < d.n_up ? F(2, ub + 1, CU_SNAKE) : F(0, 0, CD_SOUT_A));
           bool done = false;
-          if ((rc = resunit_fused(n, Tmax, stage_name("codec_resunit", C), pp[cur], bs, C, mul, B(2, ub, CU_R0_W7 + o),
+          if ((rc = resunit_fused(n, Tmax, stage_name("codec_resunit", C), PB(cur, mul), bs, C, mul, B(2, ub, CU_R0_W7 + o),
                                   F(2, ub, CU_R0_B7 + o), dils[r], F(2, ub, CU_R0_A2 + o), B(2, ub, CU_R0_W1 + o),
                                   F(2, ub, CU_R0_B1 + o), of, &done))) return rc;
           if (done) {
@@ -1022,9 +1046,9 @@ class Codec {
           }
         }
         ConvOut o7;
-        o7.p = pp[cur ^ 1];
+        o7.p = PB(cur ^ 1, mul);
         o7.alpha = F(2, ub, CU_R0_A2 + o);
-        if ((rc = conv(n, Tmax, stage_name("codec_res_conv7", C), pp[cur], bs, C, mul, B(2, ub, CU_R0_W7 + o), 7, C, 0, dils[r],
+        if ((rc = conv(n, Tmax, stage_name("codec_res_conv7", C), PB(cur, mul), bs, C, mul, B(2, ub, CU_R0_W7 + o), 7, C, 0, dils[r],
                        3 * dils[r], 1, F(2, ub, CU_R0_B7 + o), o7))) return rc;
         cur ^= 1;
         ConvOut o1;
@@ -1032,10 +1056,10 @@ class Codec {
         // or conv_out reads the planes, and the ConvTranspose rewrites xf): planes only
         o1.y = r < 2 ? xf : nullptr;
         o1.res = xf;
-        o1.p = pp[cur ^ 1];
+        o1.p = PB(cur ^ 1, mul);
         o1.alpha = r < 2 ? F(2, ub, CU_R0_A1 + o + (CU_R1_A1 - CU_R0_A1))
                          : (ub + 1 < d.n_up ? F(2, ub + 1, CU_SNAKE) : F(0, 0, CD_SOUT_A));
-        if ((rc = conv(n, Tmax, stage_name("codec_res_conv1", C), pp[cur], bs, C, mul, B(2, ub, CU_R0_W1 + o), 1, C, 0, 1, 0, 1,
+        if ((rc = conv(n, Tmax, stage_name("codec_res_conv1", C), PB(cur, mul), bs, C, mul, B(2, ub, CU_R0_W1 + o), 1, C, 0, 1, 0, 1,
                        F(2, ub, CU_R0_B1 + o), o1))) return rc;
         cur ^= 1;
       }
@@ -1043,7 +1067,7 @@ class Codec {
     pbeg();
     const size_t shm = (size_t)(kOutT + 6) * (C + 1) * sizeof(float);
     k_conv_out<<<dim3((unsigned)((Tmax * (int64_t)mul + kOutT - 1) / kOutT), n), 256, shm, stream>>>(
-        pp[cur].h, pp[cur].l, bs, C, mul, d_ntok, F(0, 0, CD_COUT_W), F(0, 0, CD_COUT_B), pcm,
+        pp[cur].h, pp[cur].l, bs, PB(cur, mul).cs, C, mul, d_ntok, F(0, 0, CD_COUT_W), F(0, 0, CD_COUT_B), pcm,
         (int64_t)Tmax * RWKVTTS_HOP);
     RT_HIP(hipGetLastError());
     pend("codec_conv_out");

@@ -207,3 +207,30 @@ def test_fused_residual_unit_bit_identical():
                 assert np.array_equal(x, y)
         finally:
             c.close()
+
+
+def test_channel_blocked_planes_bit_identical():
+    """The WaveGenerator's activation planes channel-blocked ([C / 32][rows][32], the default) or
+    channel-last (RWKVTTS_CODEC_BLK=0, read per call): only addresses change, so PCM is bitwise
+    equal -- with and without the fused residual units, the weight-lo kernels, ragged lengths."""
+    rs = np.random.default_rng(32)
+    for d, T, wlo in ((codec.CODEC_DIMS_TINY, 41, None), (codec.CODEC_DIMS_FULL, 9, None),
+                      (codec.CODEC_DIMS_FULL, 5, True)):
+        w = codec.synth_codec_blob(d, seed=12)
+        items = [(rs.integers(0, 4096, 32), rs.integers(0, 8192, T - 2 * i)) for i in range(3)]
+        c = _decoder(w, d, wlo)
+        try:
+            outs = []
+            for env in ({}, {"RWKVTTS_CODEC_BLK": "0"}, {"RWKVTTS_NO_RESFUSE": "1"},
+                        {"RWKVTTS_CODEC_BLK": "0", "RWKVTTS_NO_RESFUSE": "1"}):
+                os.environ.update(env)
+                try:
+                    outs.append(c.decode_audio_batch(items))
+                finally:
+                    for k in env:
+                        del os.environ[k]
+            for o in outs[1:]:
+                for x, y in zip(outs[0], o):
+                    assert np.array_equal(x, y)
+        finally:
+            c.close()
