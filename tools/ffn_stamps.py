@@ -1,7 +1,8 @@
 """Persistent-launch per-block stamps (layer 5 of the last decode step): k_ffn_persist
 (RWKVTTS_FFN_STAMPS; roles LayerNorm rows, key, value) or k_att_persist (RWKVTTS_ATT_STAMPS; roles
 LayerNorm rows, rkv, WKV, Wo): per role the min / median / max of each stamp in us from the
-launch's first block start. Usage: ffn_stamps.py [S] [ffn|att] (32 requests, S semantic)."""
+launch's first block start. Usage: ffn_stamps.py [S] [ffn|att|layer] [B] (B requests, default 32;
+S semantic; B < 16 sets RWKVTTS_PERSIST_MIN_ROWS=1 so the persistent launches run)."""
 import os
 import sys
 import tempfile
@@ -15,14 +16,17 @@ path = os.path.join(tempfile.mkdtemp(), "stamps.bin")
 os.environ["RWKVTTS_FFN_STAMPS" if which == "ffn" else "RWKVTTS_ATT_STAMPS"] = path
 if which == "att":  # the attention launch alone (two launches per layer)
     os.environ.setdefault("RWKVTTS_LAYER_PERSIST", "0")
+B = int(sys.argv[3]) if len(sys.argv) > 3 else 32
+if B < 16:
+    os.environ.setdefault("RWKVTTS_PERSIST_MIN_ROWS", "1")
 import rwkvtts  # noqa: E402
 from rwkvtts import weights as W  # noqa: E402
 
 S = int(sys.argv[1]) if len(sys.argv) > 1 else 32
 blob = W.synth_blob(W.DIMS_04B, seed=20251205)
-rt = rwkvtts.SharedRwkvRuntime(blob, max_slots=32, token_chunk_size=2048, use_graphs=True)
+rt = rwkvtts.SharedRwkvRuntime(blob, max_slots=max(B, 1), token_chunk_size=2048, use_graphs=True)
 reqs = []
-for i in range(32):
+for i in range(B):
     rs = np.random.RandomState(1000 + i)
     reqs.append(rwkvtts.TtsBatchRequest(text_tokens=rs.randint(12293, 77822, size=24).tolist(),
                                         property_tokens=[77823, 77838, 77869, 77845, 77830, 77826],
@@ -33,10 +37,12 @@ for rep in range(2):
     print(f"rep {rep}: decode {st['decode_ms'] / max(st['steps'], 1) * 1000:.1f} us/step")
 rt.close()
 a = np.fromfile(path, dtype=np.uint64).reshape(-1, 4).astype(np.float64)
+nw = 16 * B  # WKV workgroups: one per (row, head)
+ae = 244 + nw + 128
 roles = ({"ln": (0, 32), "key": (32, 288), "value": (288, 544)} if which == "ffn" else
-         {"ln": (0, 32), "rkv": (32, 244), "wkv": (244, 756), "wo": (756, 884)})
+         {"ln": (0, 32), "rkv": (32, 244), "wkv": (244, 244 + nw), "wo": (244 + nw, ae)})
 if which == "layer":  # k_layer_persist: the attention blocks, then the FFN blocks
-    roles.update({"ffn_ln": (884, 916), "key": (916, 1172), "value": (1172, 1428)})
+    roles.update({"ffn_ln": (ae, ae + 32), "key": (ae + 32, ae + 288), "value": (ae + 288, ae + 544)})
 nb = max(e for _, e in roles.values())
 t0 = a[:nb, 0][a[:nb, 0] > 0].min()
 names = ["start", "wait_done", "work_done", "end"]
