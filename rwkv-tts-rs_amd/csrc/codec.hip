@@ -763,10 +763,16 @@ class Codec {
        // tiles (124 KB) let them share the CU: decode step 0.883 -> 0.875 ms in the bench, +0.7 %
        // samples/s (same-box A/B x2, tools/bench_ab.sh) for +1 ms of vocoder time. Tests
        // bit-identical either way: the per-element accumulation order does not depend on TN.
+      // Round 4: the decode step's persistent workgroups (k_att_persist / k_ffn_persist) take
+      // 36.6 KB of LDS, which fits beside a 64-wide tile at dilation 1 only. 48-wide tiles
+      // (RWKVTTS_CONV7_TN=48) leave room at every dilation: bench A/Bs (13 alternating pairs over
+      // three boxes, profiles/r04_conv7_tile_ab.txt) +0.1 to +1.2 % samples/s, within the boxes'
+      // run-to-run spread, for +1.5 ms of vocoder time; 64 stays the default.
       static const int tn7 = getenv("RWKVTTS_CONV7_TN") ? atoi(getenv("RWKVTTS_CONV7_TN")) : 64;  // A/B switch
       const int wr = (256 + span + 15) & ~15;
       if (KT == 7 && mode == 0 && tn7 == 96 && Co % 96 == 0 && 2 * (size_t)(2 * wr + ntaps_max * 96) * 64 <= 160 * 1024)
         TN = 96;
+      if (KT == 7 && mode == 0 && tn7 == 48 && Co % 48 == 0) TN = 48;
       // ConvTranspose: 96-wide tiles measured faster at 96 and 384 output channels (2.54 -> 2.14,
       // 2.30 -> 2.10 ms per batch), slower at 192 (2.51 -> 2.62), equal at 768
       static const int tnT = getenv("RWKVTTS_CONVT_TN") ? atoi(getenv("RWKVTTS_CONVT_TN")) : -1;  // A/B switch
