@@ -150,45 +150,58 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? 1 : 2) void k_conv(ConvArgs a)
   const int nWblk = ntaps * (TN / 16);  // one weight plane's blocks
   const int nAblk = 2 * WRp / 16, nblk = nAblk + (WLO ? 2 : 1) * nWblk;
   const int buf_bytes = nblk * 1024;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, g = lane >> 4;
+  // wave index read back as a scalar: every per-wave decision below (which staging blocks a wave
+  // issues) is then a scalar branch instead of an exec-masked one
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), li = lane & 15, g = lane >> 4;
   const int64_t xoff = req * a.x_bs;
   const int nck = a.Ci / 32;
   const int lrow = lane >> 2, lslot = lane & 3;
 
-  // This wave's share of the chunk's 16-row blocks: per-lane source pointers at channel 0,
-  // computed once (a chunk adds c0); out-of-range window rows read the zero page.
-  // amask: blocks u of in-range window rows (they advance by the input's chunk stride; weight
-  // and zero-page rows advance by 32 channels)
+  // This wave's share of the chunk's 16-row blocks, staged by buffer loads straight into LDS:
+  // per block u a 32-bit byte offset (per lane, computed once) into one of four buffer resources
+  // (this utterance's input hi / lo plane, the weights' hi / lo plane); a chunk adds a scalar
+  // offset (the input's chunk stride, or 32 channels of weights). Out-of-range window rows get
+  // an offset past the resources' range, which the buffer load returns as zeros.
   constexpr int MAXB = 16;
-  const bf16_t* srcp[MAXB];
-  uint32_t amask = 0;
+  constexpr uint32_t kOob = 0x80000000u;
+  auto rsrc = [](const void* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7fffffff, 0x00020000);
+  };
+  const __amdgpu_buffer_rsrc_t rxh = rsrc(a.xh + xoff), rxl = rsrc(a.xl + xoff), rwh = rsrc(a.w),
+                               rwl = rsrc(WLO ? a.wl : a.w);
+  uint32_t voff[MAXB];
 #pragma unroll
   for (int u = 0; u < MAXB; ++u) {
     const int b = wave + NWV * u;
-    const bf16_t* src = a.zeros;
+    uint32_t o = kOob;
     if (b < nAblk) {
       const int plane = b >= WRp / 16, row = (b - plane * (WRp / 16)) * 16 + lrow;
       const int piece = lslot ^ ((row >> 1) & 3), pos = wstart + row;
-      if (pos >= 0 && pos < Tin) {
-        src = (plane ? a.xl : a.xh) + xoff + (int64_t)pos * (a.x_cs ? 32 : a.Ci) + piece * 8;
-        amask |= 1u << u;
-      } else {
-        src = a.zeros + piece * 8;
-      }
+      if (pos >= 0 && pos < Tin) o = (uint32_t)(pos * (a.x_cs ? 32 : a.Ci) + piece * 8) * 2u;
     } else if (b < nblk) {
       const int wb0 = b - nAblk, lo = wb0 >= nWblk, wb = wb0 - (lo ? nWblk : 0);
       const int tap = wb / (TN / 16), co = (wb % (TN / 16)) * 16 + lrow;
       const int piece = lslot ^ ((co >> 1) & 3);
-      src = (lo ? a.wl : a.w) + ((int64_t)(co0 + co) * a.K + k0 + tap * kstep) * a.Ci + piece * 8;
+      o = (uint32_t)((((co0 + co) * a.K + k0 + tap * kstep) * a.Ci + piece * 8) * 2);
     }
-    srcp[u] = src;
+    voff[u] = o;
   }
   auto issue = [&](int ck, uint8_t* buf) {
-    const int64_t c0 = ck * 32, aoff = a.x_cs ? ck * a.x_cs : c0;
+    const int aso = (int)((a.x_cs ? ck * a.x_cs : ck * 32) * 2), wso = ck * 64;  // bytes
 #pragma unroll
     for (int u = 0; u < MAXB; ++u) {
-      const int b = wave + NWV * u;
-      if (b < nblk) glds16(srcp[u] + (((amask >> u) & 1) ? aoff : c0), buf + b * 1024);
+      const int b = __builtin_amdgcn_readfirstlane(wave + NWV * u);  // wave-uniform: scalar branches
+      if (b >= nblk) continue;
+      auto* dst = (__attribute__((address_space(3))) void*)(buf + b * 1024);
+      // one call site per resource: the resource stays in SGPRs
+      if (b < nAblk) {
+        if (b >= WRp / 16) __builtin_amdgcn_raw_ptr_buffer_load_lds(rxl, dst, 16, voff[u], aso, 0, 0);
+        else __builtin_amdgcn_raw_ptr_buffer_load_lds(rxh, dst, 16, voff[u], aso, 0, 0);
+      } else if (WLO && b - nAblk >= nWblk) {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rwl, dst, 16, voff[u], wso, 0, 0);
+      } else {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rwh, dst, 16, voff[u], wso, 0, 0);
+      }
     }
   };
 
