@@ -506,21 +506,35 @@ __global__ __launch_bounds__(256) void k_conv_out(const bf16_t* xh, const bf16_t
   if (t0 >= T) return;
   const int LDX = C + 1, rows = kOutT + 6, c8n = C / 8;
   const int64_t xo = req * x_bs;
-  for (int i = threadIdx.x; i < rows * c8n; i += 256) {
-    const int r = i / c8n, c8 = (i - r * c8n) * 8, p = t0 - 3 + r;
-    float* dst = s_x + r * LDX + c8;
-    if (p >= 0 && p < T) {
-      const int64_t o = x_cs ? xo + (c8 >> 5) * x_cs + (int64_t)p * 32 + (c8 & 31) : xo + (int64_t)p * C + c8;
-      const uint4 h = *(const uint4*)(xh + o), l = *(const uint4*)(xl + o);
-      const uint32_t hw[4] = {h.x, h.y, h.z, h.w}, lw[4] = {l.x, l.y, l.z, l.w};
+  // staged in batches of 8 pieces per thread: all 16 loads of a batch are requested before the
+  // first conversion, so the window's memory latency is paid once per batch, not once per piece
+  constexpr int kBatch = 8;
+  const int total = rows * c8n;
+  for (int i0 = threadIdx.x; i0 < total; i0 += 256 * kBatch) {
+    uint4 h[kBatch], l[kBatch];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
+    for (int j = 0; j < kBatch; ++j) {
+      const int i = i0 + 256 * j;
+      const int r = i / c8n, c8 = (i - r * c8n) * 8, p = t0 - 3 + r;
+      h[j] = l[j] = make_uint4(0u, 0u, 0u, 0u);
+      if (i < total && p >= 0 && p < T) {
+        const int64_t o = x_cs ? xo + (c8 >> 5) * x_cs + (int64_t)p * 32 + (c8 & 31) : xo + (int64_t)p * C + c8;
+        h[j] = *(const uint4*)(xh + o);
+        l[j] = *(const uint4*)(xl + o);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kBatch; ++j) {
+      const int i = i0 + 256 * j;
+      if (i >= total) break;
+      const int r = i / c8n, c8 = (i - r * c8n) * 8;
+      float* dst = s_x + r * LDX + c8;
+      const uint32_t hw[4] = {h[j].x, h[j].y, h[j].z, h[j].w}, lw[4] = {l[j].x, l[j].y, l[j].z, l[j].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {  // zero words (rows outside the utterance) give +0
         dst[2 * e] = as_f32(hw[e] << 16) + as_f32(lw[e] << 16);
         dst[2 * e + 1] = as_f32(hw[e] & 0xFFFF0000u) + as_f32(lw[e] & 0xFFFF0000u);
       }
-    } else {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) dst[e] = 0.0f;
     }
   }
   __syncthreads();
