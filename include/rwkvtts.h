@@ -355,6 +355,17 @@ int rwkvtts_set_profiling(rwkvtts_engine* e, int on);
 int rwkvtts_profile_entry(rwkvtts_engine* e, int idx, char* name, int name_cap, int64_t* launches,
                           double* total_ms);
 
+/* Test hook, not part of the drop-in surface (no reference counterpart): runs the production
+ * decode-step sampler/controller k_advance (sample_logits_with_top_p_k + the phase controllers of
+ * normal_mode_inference.rs:222-391 / zero_shot_inference.rs, as the decode graphs run it) on
+ * caller-given logit rows [n_rows][8193] and controller states, n_steps launches; exact = 1 forces
+ * the exact sequential-sum walk. `rows` points to n_rows records of 72 bytes: int32 mode (0 normal,
+ * 1 zero-shot), phase (0 global, 2 semantic), top_k, fixed, n_sem, hard_min, win_bits, win_len;
+ * uint32 key[8] (ChaCha12 key of the phase's stream); uint64 draw (next u32 draw index).
+ * Outputs out_tok / out_used / out_phase are [n_steps][n_rows]. */
+int rwkvtts_debug_advance(rwkvtts_engine* e, const float* logits, int n_rows, const void* rows, int exact,
+                          int n_steps, int32_t* out_tok, int32_t* out_used, int32_t* out_phase);
+
 /* ---- codec: BiCodecDetokenize via ORT (lightweight_tts_pipeline.rs:606-622,706-730) ----- */
 typedef struct rwkvtts_codec rwkvtts_codec;
 typedef struct {

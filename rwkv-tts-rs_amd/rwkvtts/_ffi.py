@@ -131,6 +131,10 @@ EXPORTS = {
     "rwkvtts_manager_get_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ManagerStats)]),
     "rwkvtts_get_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Stats)]),
     "rwkvtts_set_profiling": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    # test hook (tests/test_gpu_advance.py): the decode-step sampler on caller-given rows
+    "rwkvtts_debug_advance": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                             ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                             ctypes.c_void_p]),
     "rwkvtts_profile_entry": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
                                              ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)]),
     "rwkvtts_codec_blob_bytes": (ctypes.c_int64, [ctypes.POINTER(CodecDims)]),

@@ -44,9 +44,7 @@ def rt():
 
 
 def _gpu(rt, logits, rows, exact):
-    f = _ffi.lib().rwkvtts_debug_advance
-    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
-                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    f = _ffi.lib().rwkvtts_debug_advance  # argtypes from _ffi.EXPORTS
     n = len(rows)
     arr = (Row * n)(*rows)
     lg = np.ascontiguousarray(logits, dtype=np.float32)
