@@ -215,6 +215,10 @@ struct FfnSync {     // (both persistent launches)
                      // workgroups request their weights after the LN wait (with their X)
   uint64_t* stamps;  // debug (RWKVTTS_FFN_STAMPS): [block][4] s_memrealtime: start, wait done, work
                      // done, end (null in production)
+  // dispatch-time prefetches held back by a fixed time (s_memrealtime ticks of 10 ns; 0 = none),
+  // so the LayerNorm rows at the head of the launch run with less traffic beside them:
+  // d_w the rkv / key weight streams, d_late the value / Wo weights, d_s the WKV state + LoRA-up
+  int d_w, d_late, d_s;
 };
 
 // one layer's arguments of the one-launch decode step (k_step_persist reads them from a device table)

@@ -665,6 +665,12 @@ __device__ inline void sync_arrive(int* c, int replicas = 1) {
   if (threadIdx.x < replicas)
     __hip_atomic_fetch_add((gint_t*)(c + threadIdx.x * kSyncStride), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// hold a prefetch back until `ticks` (10 ns) after the launch's first s_memrealtime read here
+__device__ inline void hold_until(int ticks) {
+  if (ticks <= 0) return;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)ticks) __builtin_amdgcn_s_sleep(2);
+}
 // handed-off bytes are read with sc1 (L1-bypassing) buffer loads only
 __device__ inline u32x4_ ld_sc1_b128(__amdgpu_buffer_rsrc_t r, int off_bytes) {
   return __builtin_amdgcn_raw_buffer_load_b128(r, off_bytes, 0, 16);
@@ -860,12 +866,14 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
     // requested after it, so the poll is not queued behind the weights and the LN rows' loads do
     // not compete with them)
     const bool late_w = ROLE == 1 ? (sy.opts & 4) != 0 : (sy.opts & 16) != 0;
+    hold_until(sy.d_w);
     if (!late_w) load_w();
     sync_wait(sy.cnt + kSyncStride * (blockIdx.x & (kLnReplicas - 1)), sy.ln_rows, sy.err, 1, sy.opts);
     sync_stamp(sy, 1);
     load_x();
     if (late_w) load_w();
   } else if constexpr (ROLE == 4) {
+    hold_until(sy.d_late);
     load_w();
     const int h0 = kbeg >> 6;  // the K-slice's first head (64 channels per head)
     for (int hh = h0; hh < h0 + (KS >> 6); ++hh) sync_wait(sy.cnt + kSyncStride * (kAttWkv + hh), sy.ln_rows, sy.err, 8, sy.opts);
@@ -874,6 +882,7 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
   } else if constexpr (ROLE == 2) {
     if (sy.opts & 1)  // weights after the LN rows
       sync_wait(sy.cnt + kSyncStride * (blockIdx.x & (kLnReplicas - 1)), sy.ln_rows, sy.err, 4, sy.opts);
+    hold_until(sy.d_late);
     load_w();
     sync_wait(sy.cnt + kSyncStride * (kLnReplicas + split), sy.key_per_slice, sy.err, 2, sy.opts);
     sync_stamp(sy, 1);
@@ -1473,6 +1482,23 @@ void launch_relu2_planes(const float* part, int nx, int64_t pstride, int ld, int
 // (the caller runs the three launches). ln / key / val: the three launches' arguments as built by
 // the engine; cnt / cnt_prev: this and the previous layer's counter blocks ((1 + kFfnSlices) x
 // kSyncStride ints, zero before this layer's first use); err: the give-up word.
+// Holds of the dispatch-time prefetches (FfnSync::d_w / d_late / d_s). Default: the rkv / key
+// weight streams wait 1 µs, so the LayerNorm rows at the head of each persistent launch load their
+// slabs with less traffic beside them while the weights still land before the LayerNorm ends
+// (same-box decode A/B at B = 32: 771-776 -> 756-764 µs per step, tokens unchanged; holding the
+// value / Wo weights or the WKV state is slower, profiles/r04h_pf_hold_ab.txt).
+// RWKVTTS_PF_HOLD="w,late,s" (10 ns ticks) overrides; read once per process (A/B switch).
+static void prefetch_holds(FfnSync& sy) {
+  static int h[3] = {-1, 0, 0};
+  if (h[0] < 0) {
+    h[0] = 100;
+    if (const char* e = getenv("RWKVTTS_PF_HOLD")) sscanf(e, "%d,%d,%d", &h[0], &h[1], &h[2]);
+  }
+  sy.d_w = h[0];
+  sy.d_late = h[1];
+  sy.d_s = h[2];
+}
+
 struct FfnPrep {
   LnMixArgs l;
   GemmArgs ka, va;
@@ -1517,6 +1543,7 @@ static bool prep_ffn_persist(const LnMixArgs& ln, const GemmArgs& key, const Gem
   sy.key_per_slice = key.xalign * key.k_split;
   sy.stamps = stamps;
   sy.opts = opts;
+  prefetch_holds(sy);
   sy.n_prev = kLnReplicas + kFfnSlices;
   P.nv = vt * val.k_split;
   return true;
@@ -2242,6 +2269,7 @@ __device__ __attribute__((always_inline)) void wkv6_body(const WkvArgs& a, const
     // (opts bit 3: only once the LN rows are published -- the LN phase then runs without this
     // prefetch beside it; the rkv phase still hides it)
     if (sy.opts & 8) sync_wait(sy.cnt + kSyncStride * (kAttLn + (blockIdx.x & (kLnReplicas - 1))), sy.ln_rows, sy.err, 64, sy.opts);
+    hold_until(sy.d_s);
 #pragma unroll
     for (int u = 0; u < 9; ++u) lw[u] = pl[u * 256 + t];
     load_state(slot);
@@ -2568,6 +2596,7 @@ static bool prep_att_persist(const LnMixArgs& ln, const GemmArgs& rkv, const Wkv
   sy.lora_target = lora_tiles * rkv.k_split;
   sy.C = ln.C;
   sy.opts = opts;
+  prefetch_holds(sy);
   sy.stamps = stamps;
   return true;
 }
