@@ -217,8 +217,10 @@ struct FfnSync {     // (both persistent launches)
                      // done, end (null in production)
   // dispatch-time prefetches held back by a fixed time (s_memrealtime ticks of 10 ns; 0 = none),
   // so the LayerNorm rows at the head of the launch run with less traffic beside them:
-  // d_w the rkv / key weight streams, d_late the value / Wo weights, d_s the WKV state + LoRA-up
-  int d_w, d_late, d_s;
+  // d_w the rkv / key weight streams, d_late the Wo weights, d_s the WKV state + LoRA-up, d_v the
+  // FFN value weights
+  int d_w, d_late, d_s, d_v;
+  int d_k;  // the FFN key weight streams (d_w: the rkv ones)
 };
 
 // one layer's arguments of the one-launch decode step (k_step_persist reads them from a device table)

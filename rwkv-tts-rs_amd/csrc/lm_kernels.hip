@@ -866,7 +866,7 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
     // requested after it, so the poll is not queued behind the weights and the LN rows' loads do
     // not compete with them)
     const bool late_w = ROLE == 1 ? (sy.opts & 4) != 0 : (sy.opts & 16) != 0;
-    hold_until(sy.d_w);
+    hold_until(ROLE == 1 ? sy.d_k : sy.d_w);
     if (!late_w) load_w();
     sync_wait(sy.cnt + kSyncStride * (blockIdx.x & (kLnReplicas - 1)), sy.ln_rows, sy.err, 1, sy.opts);
     sync_stamp(sy, 1);
@@ -882,7 +882,7 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
   } else if constexpr (ROLE == 2) {
     if (sy.opts & 1)  // weights after the LN rows
       sync_wait(sy.cnt + kSyncStride * (blockIdx.x & (kLnReplicas - 1)), sy.ln_rows, sy.err, 4, sy.opts);
-    hold_until(sy.d_late);
+    hold_until(sy.d_v);
     load_w();
     sync_wait(sy.cnt + kSyncStride * (kLnReplicas + split), sy.key_per_slice, sy.err, 2, sy.opts);
     sync_stamp(sy, 1);
@@ -1487,16 +1487,19 @@ void launch_relu2_planes(const float* part, int nx, int64_t pstride, int ld, int
 // slabs with less traffic beside them while the weights still land before the LayerNorm ends
 // (same-box decode A/B at B = 32: 771-776 -> 756-764 µs per step, tokens unchanged; holding the
 // value / Wo weights or the WKV state is slower, profiles/r04h_pf_hold_ab.txt).
-// RWKVTTS_PF_HOLD="w,late,s" (10 ns ticks) overrides; read once per process (A/B switch).
+// RWKVTTS_PF_HOLD="rkv,wo,state,value[,key]" (10 ns ticks; key defaults to rkv) overrides; read once per process (A/B switch).
 static void prefetch_holds(FfnSync& sy) {
-  static int h[3] = {-1, 0, 0};
+  static int h[5] = {-1, 0, 0, 0, 100};
   if (h[0] < 0) {
     h[0] = 100;
-    if (const char* e = getenv("RWKVTTS_PF_HOLD")) sscanf(e, "%d,%d,%d", &h[0], &h[1], &h[2]);
+    if (const char* e = getenv("RWKVTTS_PF_HOLD"))
+      if (sscanf(e, "%d,%d,%d,%d,%d", &h[0], &h[1], &h[2], &h[3], &h[4]) < 5) h[4] = h[0];
   }
   sy.d_w = h[0];
   sy.d_late = h[1];
   sy.d_s = h[2];
+  sy.d_v = h[3];
+  sy.d_k = h[4];
 }
 
 struct FfnPrep {
