@@ -143,7 +143,11 @@ class Engine {
   // write-through (sc1) output stores per launch class, same bit order as xmap_mask_, plus
   // bit 6 ln_att, bit 7 ln_ffn
   int wt_mask_ = 0xFF;
-  int persist_min_rows_ = 16;  // RWKVTTS_PERSIST_MIN_ROWS: decode steps with fewer rows take the separate launches
+  // RWKVTTS_PERSIST_MIN_ROWS: decode steps with fewer rows take the separate launches. 1 since the
+  // 1-us weight-stream hold: the persistent halves then win at every batch size measured (B = 1:
+  // 637-642 -> 622 us per step, B = 8: 693 -> 677-679, B = 32: 771-782 -> 754-768;
+  // profiles/r04h7_small_batch_ab.txt)
+  int persist_min_rows_ = 1;
   int ffn_persist_ = 5;     // RWKVTTS_FFN_PERSIST: decode steps' FFN half as one launch (k_ffn_persist);
                             // 0 off, else 1 + 2 x launch options (5: long poll sleep, the measured best)
   int* ffn_sync_ = nullptr; // its hand-off counters: [L][kFfnSyncInts] (give-up code: d_ctrl_[S_])

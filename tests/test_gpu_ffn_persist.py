@@ -18,8 +18,7 @@ from helpers import make_request, synth_text, to_struct
 pytestmark = pytest.mark.gpu
 
 
-# (RWKVTTS_PERSIST_MIN_ROWS=1: the persistent forms also for the small row counts tested here;
-# by default decode steps below 16 rows take the separate launches)
+# (RWKVTTS_PERSIST_MIN_ROWS=1, the default since round 4: the persistent forms at every row count)
 # "halves": both halves persistent as two launches per layer; "both": one launch per layer
 # (k_layer_persist); "step": one launch per decode step (k_step_persist)
 _M = {"RWKVTTS_PERSIST_MIN_ROWS": "1"}
