@@ -250,22 +250,8 @@ def main():
         assert sum(p.size for p in pcm) == 320 * n, "vocoder output length mismatch"
         return n
 
-    # in-graph kernel timing (rwkvtts_set_profiling mode 2): the decode graphs captured during the
-    # warmup carry launch-timeline slots; the last step of every decode window of the timed region
-    # is sampled (per launch: first workgroup start -> last workgroup end)
-    if args.graph_timing:
-        rt.set_profiling(2)
     for w in range(args.warmup):
         run(-1 - w)
-    if args.graph_timing:
-        rt.set_profiling(2)  # (clears what the warmup accumulated)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    sem_tokens = 0
-    decode_ms = 0.0
-    dec_steps = 0
     # Steps are pipelined the way a server overlaps requests: the vocoder of batch s runs on its
     # own HIP stream (worker thread; ctypes releases the GIL) while the LM decodes batch s + 1.
     # Every batch's PCM is complete inside the timed region.
@@ -278,32 +264,50 @@ def main():
         assert sum(p.size for p in pcm) == 320 * sum(len(s) for _, s in out), "vocoder output length mismatch"
         return len(pcm)
 
-    futs = []
-    gen_ms = prefill_ms = 0.0
-    with ThreadPoolExecutor(max_workers=1) as pool:
-        for s in range(args.steps):
-            tg = time.perf_counter()
-            out = rt.generate_batch(requests(s))
-            gen_ms += 1000.0 * (time.perf_counter() - tg)
-            sem_tokens += sum(len(x) for _, x in out)
-            st = rt.stats()
-            decode_ms += st["decode_ms"]
-            prefill_ms += st["prefill_ms"]
-            dec_steps += st["steps"]
-            futs.append(pool.submit(vocode, out) if args.pipeline else None)
-            if not args.pipeline:
-                vocode(out)
-        for f in futs:
-            if f is not None:
-                f.result()
+    def pipelined(steps, step0):
+        acc = {"gen_ms": 0.0, "decode_ms": 0.0, "prefill_ms": 0.0, "dec_steps": 0, "sem_tokens": 0, "out": None}
+        futs = []
+        with ThreadPoolExecutor(max_workers=1) as pool:
+            for s in range(step0, step0 + steps):
+                tg = time.perf_counter()
+                out = rt.generate_batch(requests(s))
+                acc["gen_ms"] += 1000.0 * (time.perf_counter() - tg)
+                acc["sem_tokens"] += sum(len(x) for _, x in out)
+                st = rt.stats()
+                acc["decode_ms"] += st["decode_ms"]
+                acc["prefill_ms"] += st["prefill_ms"]
+                acc["dec_steps"] += st["steps"]
+                acc["out"] = out
+                futs.append(pool.submit(vocode, out) if args.pipeline else None)
+                if not args.pipeline:
+                    vocode(out)
+            for f in futs:
+                if f is not None:
+                    f.result()
+        return acc
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    acc = pipelined(args.steps, 0)  # the timed region: no instrumentation in the decode graphs
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    gprof = rt.profile() if args.graph_timing else {}
-    if args.graph_timing:
-        rt.set_profiling(0)
+    gen_ms, decode_ms, prefill_ms = acc["gen_ms"], acc["decode_ms"], acc["prefill_ms"]
+    dec_steps, sem_tokens, out = acc["dec_steps"], acc["sem_tokens"], acc["out"]
     elapsed, total_tokens = D.reduce_run(elapsed, sem_tokens, device="cuda")
+    # in-graph kernel timing (rwkvtts_set_profiling mode 2), in a SEPARATE pass after the timed region
+    # (ADVICE r4): the decode graphs are recaptured with launch-timeline slots and two more batches
+    # run pipelined exactly as timed (the vocoder of each beside the next one's decode); the last step
+    # of every decode window is sampled (per launch: first workgroup start -> last workgroup end)
+    gprof = {}
+    if args.graph_timing and rank == 0:
+        rt.set_profiling(2)
+        pipelined(2, 10**5)
+        gprof = rt.profile()
+        rt.set_profiling(0)
     samples = total_tokens * 320
     value = samples / elapsed
     audio_s = samples / 16000.0
@@ -348,8 +352,9 @@ def main():
                         "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
                         "traffic_source": tsrc, "bytes_per_launch": per_launch[dom],
                         "avg_us": round(kernels[dom]["avg_us"], 2),
-                        "avg_us_source": ("in-graph launch stamps of the timed region's decode steps (last step "
-                                          "of every decode window: first workgroup start -> last workgroup end)"
+                        "avg_us_source": ("in-graph launch stamps of a separate pass after the timed region (2 "
+                                          "batches pipelined as timed, the vocoder beside the decode; last step of "
+                                          "every decode window: first workgroup start -> last workgroup end)"
                                           if gprof else "HIP events on the engine stream, eager launches (one batch)"),
                         "rocprof": rocprof_decode(dom)}
         # vocoder: MFMA-bound conv stack, achieved TFLOP/s per class and for the whole decoder

@@ -331,6 +331,8 @@ typedef struct {
   double bcast_ms;                          /* upload + broadcast wall time at create */
   int32_t waiters;                          /* threads blocked in rwkvtts_manager_wait now */
   int32_t reserved;
+  int32_t persistent[RWKVTTS_MAX_ENGINES];  /* 1: the engine runs the persistent decode launches (at most
+                                               one engine per GPU, across processes: rwkvtts_stats) */
 } rwkvtts_manager_stats;
 int rwkvtts_manager_get_stats(rwkvtts_manager* m, rwkvtts_manager_stats* out);
 
@@ -343,6 +345,9 @@ typedef struct {
   double sample_ms;         /* sampler kernels inside decode steps */
   int64_t decode_rows;      /* sum over decode steps of active rows */
   int32_t profile_kernel_count;
+  int32_t persistent;       /* 1: this engine holds its GPU's persistent-launch slot (the first engine
+                               created on the device in any process, RWKVTTS_LOCK_DIR lock file);
+                               others run the separate launches (same outputs, bit for bit) */
 } rwkvtts_stats;
 int rwkvtts_get_stats(rwkvtts_engine* e, rwkvtts_stats* out);
 

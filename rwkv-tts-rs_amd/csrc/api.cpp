@@ -145,6 +145,7 @@ int rwkvtts_get_stats(rwkvtts_engine* e, rwkvtts_stats* out) {
   LOCK(e);
   *out = e->eng.stats;
   out->profile_kernel_count = (int32_t)e->eng.prof.size();
+  out->persistent = e->eng.persistent() ? 1 : 0;
   return RWKVTTS_OK;
 }
 

@@ -109,6 +109,16 @@ class Engine {
   // Checks a request before admission; fills `why` and returns false for a bad one.
   bool validate(const rwkvtts_request& q, std::string& why) const;
   int max_slots() const { return S_; }
+  // whether this engine holds its device's persistent-launch slot (claim_persistent)
+  bool persistent() const { return att_persist_ != 0 || ffn_persist_ != 0; }
+  // true once after serve() returned an error because a persistent hand-off wait timed out: the
+  // unit's jobs failed, the give-up word, every hand-off counter block and the failed slots were
+  // reset, and the engine serves again (the manager keeps it; the next batch runs normally)
+  bool take_recovered() {
+    const bool r = recovered_;
+    recovered_ = false;
+    return r;
+  }
   int64_t max_active = 0;  // most slots decoding at once (serve)
   int64_t admissions_ = 0;  // requests admitted over the engine's life (test hook counter)
 
@@ -134,6 +144,18 @@ class Engine {
   void prof_end(const char* name, hipEvent_t ev);
   int flush_prof();
   int dump_stamps();
+  // after a timed-out persistent hand-off: zero the give-up word and every persistent counter block
+  // on the engine's stream and wait for it (the jobs of the failed units have already been failed;
+  // their slots are reset at their next admission, slot_reset)
+  int reset_persistent();
+  int lock_fd_ = -1;          // the cross-process lock of the persistent slot (claim_persistent)
+  int persist_fault_ = 0;     // give-up code of the last failed unit (finish_unit), 0 if none
+  bool recovered_ = false;
+  std::vector<std::pair<int*, size_t>> sync_bufs_;  // every persistent counter block (reset_persistent)
+  // RWKVTTS_TEST_DROP_ARRIVE=1 at creation (test hook): a device word set to 1; the first rkv
+  // workgroup of a persistent attention launch that finds it set clears it and skips its head
+  // arrival, so that head's WKV workgroups time out once (tests/test_gpu_persist_recovery.py)
+  int* d_drop_ = nullptr;
 
   void state_permute(const float* std_block, float* dev_block);
   void state_unpermute(const float* dev_block, float* std_block);

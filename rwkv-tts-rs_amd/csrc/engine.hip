@@ -3,7 +3,10 @@
 // DynamicBatchManager's sequential slot-0 loop (src/dynamic_batch_manager.rs:409-551).
 #include "engine.h"
 
+#include <fcntl.h>
 #include <string.h>
+#include <sys/file.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <chrono>
@@ -24,33 +27,65 @@ int Engine::alloc(T** p, size_t count) {
   return RWKVTTS_OK;
 }
 
-// At most ONE engine per device (in this process) runs the persistent launches. Two persistent
-// launches in flight on one GPU can deadlock: workgroups are dealt to the 8 XCDs round-robin and
-// each XCD dispatches its share in order, so when another launch fills one XCD, a launch's
-// consumers may be resident on other XCDs while producers they wait for are not -- and the other
-// launch's consumers may wait the same way. Separate launches never wait on one another, so one
-// persistent engine beside any number of others (and the vocoder) always makes progress. The
-// first engine created on a device takes the slot; it is released when that engine is destroyed.
+// At most ONE engine per device runs the persistent launches. Two persistent launches in flight
+// on one GPU can deadlock: workgroups are dealt to the 8 XCDs round-robin and each XCD dispatches
+// its share in order, so when another launch fills one XCD, a launch's consumers may be resident
+// on other XCDs while producers they wait for are not -- and the other launch's consumers may
+// wait the same way. Separate launches never wait on one another, so one persistent engine beside
+// any number of others (and the vocoder) always makes progress. The first engine created on a
+// device takes the slot; it is released when that engine is destroyed. Within a process a map
+// guards it; across processes an exclusive flock on a file named by the device's PCI bus id
+// (RWKVTTS_LOCK_DIR, default /tmp): a second process on the same GPU finds the lock held and runs
+// the separate launches. (Processes that do not share the lock directory -- separate containers on
+// one GPU -- are not covered: there the bounded waits turn a deadlock into failed units, which the
+// engine recovers from, Engine::reset_persistent.)
 namespace {
 std::mutex g_persist_mu;
 std::map<int, const void*> g_persist_owner;  // device -> the engine holding the persistent slot
+
+// -1: held by another process; -2: no lock file (no cross-process guard); else the locked fd
+int lock_device_file(int device) {
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, (int)sizeof(bus) - 1, device) != hipSuccess || !bus[0])
+    snprintf(bus, sizeof(bus), "device%d", device);
+  for (char* c = bus; *c; ++c)
+    if (*c == '/' || *c == ' ') *c = '_';
+  const char* dir = getenv("RWKVTTS_LOCK_DIR");
+  const std::string path = std::string(dir && dir[0] ? dir : "/tmp") + "/rwkvtts_persist_" + bus + ".lock";
+  const int fd = open(path.c_str(), O_RDONLY | O_CREAT | O_CLOEXEC, 0666);
+  if (fd < 0) return -2;
+  if (flock(fd, LOCK_EX | LOCK_NB) != 0) {
+    close(fd);
+    return -1;
+  }
+  return fd;
+}
 }  // namespace
 
-static bool claim_persistent(int device, const void* who) {
+static bool claim_persistent(int device, const void* who, int* lock_fd) {
   std::lock_guard<std::mutex> lk(g_persist_mu);
   auto it = g_persist_owner.find(device);
   if (it != g_persist_owner.end() && it->second != who) return false;
+  if (it == g_persist_owner.end()) {
+    const int fd = lock_device_file(device);
+    if (fd == -1) return false;  // another process on this GPU holds it
+    *lock_fd = fd;
+  }
   g_persist_owner[device] = who;
   return true;
 }
-static void release_persistent(int device, const void* who) {
+static void release_persistent(int device, const void* who, int* lock_fd) {
   std::lock_guard<std::mutex> lk(g_persist_mu);
   auto it = g_persist_owner.find(device);
-  if (it != g_persist_owner.end() && it->second == who) g_persist_owner.erase(it);
+  if (it != g_persist_owner.end() && it->second == who) {
+    g_persist_owner.erase(it);
+    if (*lock_fd >= 0) close(*lock_fd);  // (closing the descriptor releases the flock)
+    *lock_fd = -1;
+  }
 }
 
 Engine::~Engine() {
-  release_persistent(device_, this);
+  release_persistent(device_, this, &lock_fd_);
   hipSetDevice(device_);
   if (stream_) hipStreamSynchronize(stream_);
   for (auto& g : graphs_) hipGraphExecDestroy(g.second);
@@ -131,7 +166,7 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
   if (const char* lp = getenv("RWKVTTS_LAYER_PERSIST")) layer_persist_ = atoi(lp);
   if (const char* sp = getenv("RWKVTTS_STEP_PERSIST")) step_persist_ = atoi(sp);
   if (const char* pm = getenv("RWKVTTS_PERSIST_MIN_ROWS")) persist_min_rows_ = atoi(pm);
-  if ((ffn_persist_ || att_persist_) && !claim_persistent(desc.device, this)) ffn_persist_ = att_persist_ = 0;
+  if ((ffn_persist_ || att_persist_) && !claim_persistent(desc.device, this, &lock_fd_)) ffn_persist_ = att_persist_ = 0;
   if (const char* gp = getenv("RWKVTTS_GEMM_STAMPS")) {
     dbg_gstamp_path_ = gp;
     RT_OK(alloc(&dbg_gstamps_, 2 * 4096 * 4));
@@ -317,13 +352,19 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
   // k_ffn_persist hand-off counters: one block per layer (zeroed here; each launch zeroes the
   // previous layer's block)
   RT_OK(alloc(&ffn_sync_, (size_t)Lc * kFfnSyncInts));
-  RT_HIP(hipMemset(ffn_sync_, 0, (size_t)Lc * kFfnSyncInts * sizeof(int)));
   RT_OK(alloc(&step_sync_, (size_t)Lc * kStepSyncInts));  // k_step_persist's (ln_out re-zeroes them)
-  RT_HIP(hipMemset(step_sync_, 0, (size_t)Lc * kStepSyncInts * sizeof(int)));
   RT_OK(alloc(&layer_sync_, (size_t)Lc * kLayerSyncInts));  // k_layer_persist's
-  RT_HIP(hipMemset(layer_sync_, 0, (size_t)Lc * kLayerSyncInts * sizeof(int)));
   RT_OK(alloc(&att_sync_, (size_t)Lc * kAttSyncInts));  // k_att_persist's, the same scheme
-  RT_HIP(hipMemset(att_sync_, 0, (size_t)Lc * kAttSyncInts * sizeof(int)));
+  sync_bufs_ = {{ffn_sync_, (size_t)Lc * kFfnSyncInts * sizeof(int)},
+                {step_sync_, (size_t)Lc * kStepSyncInts * sizeof(int)},
+                {layer_sync_, (size_t)Lc * kLayerSyncInts * sizeof(int)},
+                {att_sync_, (size_t)Lc * kAttSyncInts * sizeof(int)}};
+  for (auto& b : sync_bufs_) RT_HIP(hipMemset(b.first, 0, b.second));
+  if (getenv("RWKVTTS_TEST_DROP_ARRIVE")) {
+    RT_OK(alloc(&d_drop_, 64));
+    const int one = 1;
+    RT_HIP(hipMemcpy(d_drop_, &one, sizeof(int), hipMemcpyHostToDevice));
+  }
   RT_OK(alloc(&vfirst_, RC));
   RT_OK(alloc(&xo_hi_, RC));
   RT_OK(alloc(&xo_lo_, RC));
@@ -649,7 +690,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
       att_persisted = launch_att_persist(m, g, k, go, att_sync_ + (size_t)l * kAttSyncInts,
                                          att_sync_ + (size_t)((l + Lc - 1) % Lc) * kAttSyncInts,
                                          (int*)(d_ctrl_ + S_), R, H_, stream_, l == 5 ? dbg_astamps2_ : nullptr,
-                                         att_persist_ >> 1);
+                                         att_persist_ >> 1, d_drop_);
       if (att_persisted) {
         prof_end("att_persist", ev);
       } else {
@@ -1356,7 +1397,9 @@ int Engine::finish_unit(int b, bool prefill, std::vector<Active>& act, std::vect
   // null-stream sync), one synchronisation, then the jobs are handed back
   const SlotCtrl* snap = h_ctrl_ + (size_t)b * (S_ + 1);
   if (const int code = *(const int*)(snap + S_)) {
-    set_error("persistent FFN launch: a hand-off wait timed out (code " + std::to_string(code) + ")");
+    // the unit's outputs are garbage: its jobs fail (serve), the persistent state is reset there
+    persist_fault_ = code;
+    set_error("persistent decode launch: a hand-off wait timed out (code " + std::to_string(code) + ")");
     return RWKVTTS_EHIP;
   }
   bool copied = false;
@@ -1645,6 +1688,13 @@ int Engine::serve(JobSource& src) {
     }
   }
   if (pending.valid || rc != RWKVTTS_OK) (void)hipStreamSynchronize(stream_);
+  if (persist_fault_) {  // a timed-out hand-off: the engine recovers and keeps serving
+    const int code = persist_fault_;
+    persist_fault_ = 0;
+    recovered_ = reset_persistent() == RWKVTTS_OK;
+    set_error("persistent decode launch: a hand-off wait timed out (code " + std::to_string(code) +
+              "); the unit's requests failed, the engine was reset");
+  }
   for (int i = 0; i < 2; ++i) {
     hipEventDestroy(ev0[i]);
     hipEventDestroy(ev1[i]);
@@ -1658,6 +1708,14 @@ int Engine::serve(JobSource& src) {
     return rc;
   }
   return dump_stamps();
+}
+
+int Engine::reset_persistent() {
+  RT_HIP(hipSetDevice(device_));
+  RT_HIP(hipMemsetAsync(d_ctrl_ + S_, 0, sizeof(SlotCtrl), stream_));
+  for (auto& b : sync_bufs_) RT_HIP(hipMemsetAsync(b.first, 0, b.second, stream_));
+  RT_HIP(hipStreamSynchronize(stream_));
+  return RWKVTTS_OK;
 }
 
 int Engine::dump_stamps() {

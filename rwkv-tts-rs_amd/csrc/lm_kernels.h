@@ -221,6 +221,9 @@ struct FfnSync {     // (both persistent launches)
   // FFN value weights
   int d_w, d_late, d_s, d_v;
   int d_k;  // the FFN key weight streams (d_w: the rkv ones)
+  // test hook (RWKVTTS_TEST_DROP_ARRIVE, null in production): the first rkv workgroup to find *drop
+  // set clears it and skips its head arrival (a hand-off that never completes: the waits time out)
+  int* drop;
 };
 
 // one layer's arguments of the one-launch decode step (k_step_persist reads them from a device table)
@@ -243,7 +246,8 @@ int step_blocks_per_layer(const LayerArgs& a);
 // launch (k_att_persist); false if the shapes are not covered.
 constexpr int kAttSyncInts = 48 * 64;  // counter block per layer (lm_kernels.hip kAtt*)
 bool launch_att_persist(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs& wkv, const GemmArgs& wo, int* cnt,
-                        int* cnt_prev, int* err, int R, int H, hipStream_t st, uint64_t* stamps, int opts);
+                        int* cnt_prev, int* err, int R, int H, hipStream_t st, uint64_t* stamps, int opts,
+                        int* drop = nullptr);
 // A decode step's whole layer (both halves) as ONE persistent launch (k_layer_persist); the
 // counter block is kLayerSyncInts.
 constexpr int kLayerSyncInts = (48 + 8 + 8 + 16) * 64;

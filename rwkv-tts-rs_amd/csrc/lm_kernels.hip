@@ -658,10 +658,14 @@ __device__ inline void sync_wait_sum(const int* c, int shards, int target, int* 
   __syncthreads();
 }
 // publish: every wave's write-through (sc1) stores drained, then ONE lane counts the workgroup in
-// (replicas > 1: lanes 0..replicas-1 of wave 0 add to one replica each, kSyncStride ints apart)
-__device__ inline void sync_arrive(int* c, int replicas = 1) {
+// (replicas > 1: lanes 0..replicas-1 of wave 0 add to one replica each, kSyncStride ints apart).
+// drop (test hook, replicas == 1 only): lane 0 skips the add once if it finds *drop set
+__device__ inline void sync_arrive(int* c, int replicas = 1, int* drop = nullptr) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if (drop && threadIdx.x == 0 &&
+      __hip_atomic_exchange((gint_t*)drop, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
+    return;
   if (threadIdx.x < replicas)
     __hip_atomic_fetch_add((gint_t*)(c + threadIdx.x * kSyncStride), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -788,20 +792,24 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
       for (int u = 0; u < PERP; ++u) {
         const int c = threadIdx.x + u * 256;
         const int r = c / CH, k8 = (c % CH) * 8;
-        const int src = min(xrow0 + r, a.M - 1);
-        const int o = (src * ldx + kbeg + k8) * 2;
-        vh[u] = __builtin_bit_cast(short8, ld_sc1_b128(rh, o));
-        vl[u] = __builtin_bit_cast(short8, ld_sc1_b128(rl, o));
+        const int o = ((xrow0 + r) * ldx + kbeg + k8) * 2;
+        vh[u] = vl[u] = (short8){0, 0, 0, 0, 0, 0, 0, 0};
+        if (xrow0 + r < a.M) {
+          vh[u] = __builtin_bit_cast(short8, ld_sc1_b128(rh, o));
+          vl[u] = __builtin_bit_cast(short8, ld_sc1_b128(rl, o));
+        }
       }
     } else {
 #pragma unroll
     for (int u = 0; u < PERP; ++u) {
       const int c = threadIdx.x + u * 256;
       const int r = c / CH, k8 = (c % CH) * 8;
-      const int src = min(xrow0 + r, a.M - 1);
-      const int64_t o = (int64_t)src * ldx + kbeg + k8;
-      vh[u] = *(const short8*)(Xhi + o);
-      vl[u] = *(const short8*)(Xlo + o);
+      const int64_t o = (int64_t)(xrow0 + r) * ldx + kbeg + k8;
+      vh[u] = vl[u] = (short8){0, 0, 0, 0, 0, 0, 0, 0};
+      if (xrow0 + r < a.M) {
+        vh[u] = *(const short8*)(Xhi + o);
+        vl[u] = *(const short8*)(Xlo + o);
+      }
     }
     }
   } else {
@@ -813,8 +821,9 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
         for (int u = 0; u < PERR; ++u) {
           const int c = threadIdx.x + u * 256;
           const int r = c / (KS / 4), k4 = (c % (KS / 4)) * 4;
-          const int src = min(xrow0 + r, a.M - 1);
-          xr[p][u] = __builtin_bit_cast(float4_, ld_sc1_b128(rp, (src * a.x_ld + kbeg + k4) * 4));
+          xr[p][u] = (float4_){0.f, 0.f, 0.f, 0.f};
+          if (xrow0 + r < a.M)
+            xr[p][u] = __builtin_bit_cast(float4_, ld_sc1_b128(rp, ((xrow0 + r) * a.x_ld + kbeg + k4) * 4));
         }
       }
     } else {
@@ -824,8 +833,9 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
       for (int u = 0; u < PERR; ++u) {
         const int c = threadIdx.x + u * 256;
         const int r = c / (KS / 4), k4 = (c % (KS / 4)) * 4;
-        const int src = min(xrow0 + r, a.M - 1);
-        xr[p][u] = *(const float4_*)(a.x_part + p * a.x_part_stride + (int64_t)src * a.x_ld + kbeg + k4);
+        xr[p][u] = (float4_){0.f, 0.f, 0.f, 0.f};
+        if (xrow0 + r < a.M)
+          xr[p][u] = *(const float4_*)(a.x_part + p * a.x_part_stride + (int64_t)(xrow0 + r) * a.x_ld + kbeg + k4);
       }
     }
   }
@@ -892,7 +902,8 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
     load_w();
   }
   for (;;) {
-  // 3) X -> LDS (rows past M hold a copy of row M-1; their outputs are not stored)
+  // 3) X -> LDS (rows past M are zeros, never loaded: an MFMA output row depends on its own X row
+  // only, and those rows' outputs are not stored -- a one-row step reads 1/32 of the X bytes)
   if constexpr (XMODE == kXPlanes) {
 #pragma unroll
     for (int u = 0; u < PERP; ++u) {
@@ -1089,7 +1100,7 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
   }
   if constexpr (ROLE == 3) {
     const int c0 = col_off + (tile - tstart) * 64;  // this tile's first output column
-    if (c0 < 3 * sy.C) sync_arrive(sy.cnt + kSyncStride * (kAttHead + ((c0 % sy.C) >> 6)));
+    if (c0 < 3 * sy.C) sync_arrive(sy.cnt + kSyncStride * (kAttHead + ((c0 % sy.C) >> 6)), 1, sy.drop);
     else sync_arrive(sy.cnt + kSyncStride * kAttLora, kLnReplicas);
   }
 }
@@ -1488,13 +1499,19 @@ void launch_relu2_planes(const float* part, int nx, int64_t pstride, int ld, int
 // (same-box decode A/B at B = 32: 771-776 -> 756-764 µs per step, tokens unchanged; holding the
 // value / Wo weights or the WKV state is slower, profiles/r04h_pf_hold_ab.txt).
 // RWKVTTS_PF_HOLD="rkv,wo,state,value[,key]" (10 ns ticks; key defaults to rkv) overrides; read once per process (A/B switch).
+struct PfHolds {
+  int h[5];
+};
 static void prefetch_holds(FfnSync& sy) {
-  static int h[5] = {-1, 0, 0, 0, 100};
-  if (h[0] < 0) {
-    h[0] = 100;
+  // parsed once, by a thread-safe static initialiser (engines on several devices may launch from
+  // their owner threads at the same time)
+  static const PfHolds ph = [] {
+    PfHolds p{{100, 0, 0, 0, 100}};
     if (const char* e = getenv("RWKVTTS_PF_HOLD"))
-      if (sscanf(e, "%d,%d,%d,%d,%d", &h[0], &h[1], &h[2], &h[3], &h[4]) < 5) h[4] = h[0];
-  }
+      if (sscanf(e, "%d,%d,%d,%d,%d", &p.h[0], &p.h[1], &p.h[2], &p.h[3], &p.h[4]) < 5) p.h[4] = p.h[0];
+    return p;
+  }();
+  const int* h = ph.h;
   sy.d_w = h[0];
   sy.d_late = h[1];
   sy.d_s = h[2];
@@ -2653,9 +2670,11 @@ __global__ __launch_bounds__(256, 2) void k_step_persist(const LayerArgs* __rest
 }
 
 bool launch_att_persist(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs& wkv, const GemmArgs& wo, int* cnt,
-                        int* cnt_prev, int* err, int R, int H, hipStream_t st, uint64_t* stamps, int opts) {
+                        int* cnt_prev, int* err, int R, int H, hipStream_t st, uint64_t* stamps, int opts,
+                        int* drop) {
   AttPrep P;
   if (!prep_att_persist(ln, rkv, wkv, wo, cnt, cnt_prev, err, R, H, stamps, opts, P)) return false;
+  P.sy.drop = drop;
   const bool emb = ln.emb != nullptr;
   LnMixArgs& l = P.l;
   GemmArgs& ga = P.ga;

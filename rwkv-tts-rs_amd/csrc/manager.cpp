@@ -127,6 +127,7 @@ class Worker : public JobSource {
   std::atomic<int> load{0};  // requests routed here and not finished
   std::atomic<bool> dead{false};
   std::atomic<int64_t> served{0}, max_active{0}, steps{0};
+  std::atomic<int> persistent{0};
   int init_rc = 1;  // 1 = initialising
   std::string init_err;
 
@@ -421,6 +422,7 @@ class Manager {
       s->served[i] = workers_[i]->served.load();
       s->max_active[i] = workers_[i]->max_active.load();
       s->steps[i] = workers_[i]->steps.load();
+      s->persistent[i] = workers_[i]->persistent.load();
     }
   }
 
@@ -531,6 +533,7 @@ void Worker::run(rwkvtts_engine_desc desc, const void* w, size_t bytes) {
   int rc = eng.init(desc, w, bytes, 1);  // w: the broadcast copy on this engine's device
   {
     std::lock_guard<std::mutex> lk(m_->init_mu_);
+    persistent = rc == RWKVTTS_OK && eng.persistent() ? 1 : 0;  // (published before init_rc)
     init_rc = rc;
     if (rc != RWKVTTS_OK) init_err = "device " + std::to_string(desc.device);
   }
@@ -539,6 +542,12 @@ void Worker::run(rwkvtts_engine_desc desc, const void* w, size_t bytes) {
   while (true) {
     rc = eng.serve(*this);
     progress(eng);
+    if (rc != RWKVTTS_OK && eng.take_recovered()) {
+      // a persistent hand-off timed out: serve failed the unit's jobs (dynamic_batch_manager.rs:387-392:
+      // a failed inference fails its own requests) and reset the engine, which keeps serving its inbox
+      fprintf(stderr, "rwkvtts manager: engine %d (device %d): %s\n", idx_, desc.device, rwkvtts_last_error());
+      continue;
+    }
     if (rc != RWKVTTS_OK) {
       // the error text lives in this (engine) thread: log it, callers only see the status code
       fprintf(stderr, "rwkvtts manager: engine %d (device %d) failed (%d): %s\n", idx_, desc.device, rc,

@@ -77,7 +77,7 @@ class Stats(ctypes.Structure):
     _fields_ = [("steps", ctypes.c_int64), ("prefill_steps", ctypes.c_int64),
                 ("decode_ms", ctypes.c_double), ("prefill_ms", ctypes.c_double),
                 ("sample_ms", ctypes.c_double), ("decode_rows", ctypes.c_int64),
-                ("profile_kernel_count", ctypes.c_int32)]
+                ("profile_kernel_count", ctypes.c_int32), ("persistent", ctypes.c_int32)]
 
 
 class ManagerDesc(ctypes.Structure):
@@ -91,7 +91,8 @@ class ManagerStats(ctypes.Structure):
                 ("served", ctypes.c_int64 * MAX_ENGINES), ("max_active", ctypes.c_int64 * MAX_ENGINES),
                 ("steps", ctypes.c_int64 * MAX_ENGINES), ("bcast_ranks", ctypes.c_int32),
                 ("bcast_rccl", ctypes.c_int32), ("bcast_ms", ctypes.c_double),
-                ("waiters", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                ("waiters", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("persistent", ctypes.c_int32 * MAX_ENGINES)]
 
 
 class CodecDims(ctypes.Structure):

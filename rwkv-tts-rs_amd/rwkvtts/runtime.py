@@ -424,15 +424,24 @@ class DynamicBatchManager:
             if self._closing or not getattr(self, "_h", None):
                 return
             self._closing = True
-            while True:
-                s = _ffi.ManagerStats()
-                check(lib().rwkvtts_manager_get_stats(self._h, ctypes.byref(s)), "manager_get_stats")
-                if self._inflight <= s.waiters:
-                    break
-                gate.wait(0.005)
-        lib().rwkvtts_manager_destroy(self._h)
-        with gate:
-            self._h = None
+            # wait until every call in flight is a waiter blocked inside the native wait (destroy
+            # returns those); a failing stats poll ends the wait -- destroy runs in any case once
+            # _closing is set, so the native manager, its threads and device memory never leak
+            try:
+                while True:
+                    s = _ffi.ManagerStats()
+                    if lib().rwkvtts_manager_get_stats(self._h, ctypes.byref(s)) != _ffi.OK:
+                        break
+                    if self._inflight <= s.waiters:
+                        break
+                    gate.wait(0.005)
+            except BaseException:
+                pass
+        try:
+            lib().rwkvtts_manager_destroy(self._h)
+        finally:
+            with gate:
+                self._h = None
 
     def __del__(self):
         try:
@@ -507,4 +516,4 @@ class DynamicBatchManager:
         return {"submitted": s.submitted, "completed": s.completed, "batches": s.batches,
                 "served": list(s.served[:n]), "max_active": list(s.max_active[:n]), "steps": list(s.steps[:n]),
                 "bcast_ranks": s.bcast_ranks, "bcast_rccl": s.bcast_rccl, "bcast_ms": s.bcast_ms,
-                "waiters": s.waiters}
+                "waiters": s.waiters, "persistent": list(s.persistent[:n])}

@@ -118,8 +118,10 @@ def test_persist_f16_bitwise():
 
 
 def test_persist_under_the_manager_two_engines_one_device(blob04):
-    """Two engines on one device decoding at the same time: two persistent launches in flight on
-    the GPU together (dependencies only point to lower block indices: no deadlock)."""
+    """Two engines on one device decoding at the same time. Only the first engine created on the
+    device holds the persistent slot (claim_persistent: two persistent launches in flight on one GPU
+    can deadlock); the second runs the separate launches beside it, so one persistent launch and
+    separate launches are in flight together -- asserted through the manager's per-engine flag."""
     with _env(MODES["both"]):
         m = rwkvtts.DynamicBatchManager(blob04, rwkvtts.DynamicBatchConfig(max_batch_size=64, collect_timeout_ms=5),
                                         devices=[0, 0], max_slots=32, token_chunk_size=512)
@@ -128,6 +130,7 @@ def test_persist_under_the_manager_two_engines_one_device(blob04):
         got = m.generate_tts_batch(reqs)
         st = m.stats()
         assert all(n > 0 for n in st["served"]), st
+        assert sorted(st["persistent"]) == [0, 1], st  # exactly one engine per device is persistent
     finally:
         m.close()
     rt = _runtime(blob04, False, max_slots=32, token_chunk_size=512, use_graphs=True)

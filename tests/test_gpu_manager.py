@@ -133,6 +133,7 @@ def test_manager_config4_eight_engines_256_requests():
         assert st["completed"] == n_req and sum(st["served"]) == n_req, st
         assert all(n > 0 for n in st["served"]), ("an engine served nothing", st["served"])
         assert max(st["max_active"]) <= 32, st
+        assert sum(st["persistent"]) == 1, st  # one persistent engine on the device, 7 separate-launch ones
         for i in range(n_req):
             assert len(got[i][0]) == 32 and len(got[i][1]) == 3 + i % 4, i
         om = oracle.Model(blob)
