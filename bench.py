@@ -107,7 +107,6 @@ def algorithmic_bytes(d, R, head_rows):
     # the launches they replace (per launch; not added to per_step again)
     per["att_persist"] = per["ln_mix_att"] + per["gemm_rkv_lora"] + per["wkv"] + per["gemm_wo"]
     per["ffn_persist"] = per["ln_mix_ffn"] + per["gemm_ffn_key"] + per["gemm_ffn_value"]
-    per["layer_persist"] = per["att_persist"] + per["ffn_persist"]
     per_step["gemm_head"] = head_rows * C * 2 + R * head_rows * 4
     per_step["embed"] = R * C * 2
     return per, per_step

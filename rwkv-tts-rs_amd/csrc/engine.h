@@ -176,16 +176,6 @@ class Engine {
   int att_persist_ = 5;     // RWKVTTS_ATT_PERSIST: decode steps' attention half as one launch (k_att_persist),
                             // same encoding
   int* att_sync_ = nullptr; // its hand-off counters: [L][kAttSyncInts]
-  int step_persist_ = 0;    // RWKVTTS_STEP_PERSIST=1 (with LAYER_PERSIST=1): all layers of a step in ONE
-                            // launch (k_step_persist; measured slower still)
-  int* step_sync_ = nullptr; // its counters: [L][kStepSyncInts] (zeroed by the ln_out launch after it)
-  std::map<int, LayerArgs*> step_tables_;  // device argument tables per row count
-  std::map<int, int> step_nb_;             // blocks per layer per row count
-  std::vector<LayerArgs>* collect_ = nullptr;  // build_step_table's collect pass of launch_forward
-  int build_step_table(int R);
-  int layer_persist_ = 0;   // RWKVTTS_LAYER_PERSIST=1: both halves persistent -> ONE launch per layer
-                            // (k_layer_persist; measured slower than two)
-  int* layer_sync_ = nullptr; // its counters: [L][kLayerSyncInts]
   int xalign_mask_ = 4;     // GemmArgs::xalign per class: bit 0 rkv (-> WKV heads), bit 2 ffn key (-> value K-slices)
   int device_ = 0;
   int f16_ = 0;  // fp16 matrices (else bf16): MFMA f16 and f16 activation planes

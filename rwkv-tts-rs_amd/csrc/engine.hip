@@ -163,8 +163,6 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
   if (const char* xa = getenv("RWKVTTS_XALIGN_MASK")) xalign_mask_ = (int)strtol(xa, nullptr, 0);
   if (const char* fp = getenv("RWKVTTS_FFN_PERSIST")) ffn_persist_ = atoi(fp);
   if (const char* ap = getenv("RWKVTTS_ATT_PERSIST")) att_persist_ = atoi(ap);
-  if (const char* lp = getenv("RWKVTTS_LAYER_PERSIST")) layer_persist_ = atoi(lp);
-  if (const char* sp = getenv("RWKVTTS_STEP_PERSIST")) step_persist_ = atoi(sp);
   if (const char* pm = getenv("RWKVTTS_PERSIST_MIN_ROWS")) persist_min_rows_ = atoi(pm);
   if ((ffn_persist_ || att_persist_) && !claim_persistent(desc.device, this, &lock_fd_)) ffn_persist_ = att_persist_ = 0;
   if (const char* gp = getenv("RWKVTTS_GEMM_STAMPS")) {
@@ -352,12 +350,8 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
   // k_ffn_persist hand-off counters: one block per layer (zeroed here; each launch zeroes the
   // previous layer's block)
   RT_OK(alloc(&ffn_sync_, (size_t)Lc * kFfnSyncInts));
-  RT_OK(alloc(&step_sync_, (size_t)Lc * kStepSyncInts));  // k_step_persist's (ln_out re-zeroes them)
-  RT_OK(alloc(&layer_sync_, (size_t)Lc * kLayerSyncInts));  // k_layer_persist's
   RT_OK(alloc(&att_sync_, (size_t)Lc * kAttSyncInts));  // k_att_persist's, the same scheme
   sync_bufs_ = {{ffn_sync_, (size_t)Lc * kFfnSyncInts * sizeof(int)},
-                {step_sync_, (size_t)Lc * kStepSyncInts * sizeof(int)},
-                {layer_sync_, (size_t)Lc * kLayerSyncInts * sizeof(int)},
                 {att_sync_, (size_t)Lc * kAttSyncInts * sizeof(int)}};
   for (auto& b : sync_bufs_) RT_HIP(hipMemset(b.first, 0, b.second));
   if (getenv("RWKVTTS_TEST_DROP_ARRIVE")) {
@@ -557,27 +551,6 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
   bool use_att = att_persist_ && inplace && big && !dbg_exp_ && Lc >= 2 && !dbg_stamps_ && !dbg_gstamps_ &&
                  !any_quant && emb_fused;
   bool use_ffn = ffn_persist_ && inplace && big && !dbg_exp_ && Lc >= 2 && !dbg_gstamps_ && !any_quant;
-  // both halves persistent: one launch per layer (k_layer_persist) unless RWKVTTS_LAYER_PERSIST=0
-  bool use_layer = use_att && use_ffn && layer_persist_;
-  // ... and all layers in ONE launch (k_step_persist) with RWKVTTS_STEP_PERSIST: its argument
-  // table for R rows is built once (run_step, before a capture) by a collect pass of this function
-  bool use_step = use_layer && step_persist_;
-  if (collect_) {
-    if (!use_step) return RWKVTTS_OK;  // (no table: nothing to collect, nothing launched)
-  } else if (use_step) {
-    auto it = step_tables_.find(R);
-    if (it == step_tables_.end()) {
-      RT_OK(build_step_table(R));
-      it = step_tables_.find(R);
-    }
-    if (!it->second) {
-      use_step = false;  // shapes not covered: the per-layer launches (which fall back themselves)
-    } else {
-      prof_begin(&ev);
-      launch_step_persist(it->second, Lc, step_nb_[R], f16_ != 0, tl_next("step_persist"), stream_);
-      prof_end("step_persist", ev);
-    }
-  }
   if (!emb_fused) {
     prof_begin(&ev);
     launch_embed(d_tok_, d_rows_, &d_ctrl_[0].next_token, (int)(sizeof(SlotCtrl) / 4), emb_,
@@ -585,9 +558,9 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     prof_end("embed", ev);
   }
   const int64_t RC = (int64_t)Rmax_ * C;
-  for (int l = 0; l < Lc && !(use_step && !collect_); ++l) {
+  // ---- att: residual (+ previous layer's ffn partials) -> LN1 -> 6 mixes (layer l's arguments)
+  auto ln_att_args = [&](int l) {
     const LayerW& w = L_[l];
-    // ---- att: residual (+ previous layer's ffn partials) -> LN1 -> 6 mixes
     LnMixArgs m{};
     m.f16 = f16_;
     m.h_in = h0_;
@@ -622,6 +595,33 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
       m.ln0_b = ln0_b_;
       m.n_vocab = dims.n_vocab;
     }
+    return m;
+  };
+  // ---- the final LayerNorm of the logits rows
+  auto ln_out_args = [&]() {
+    LnMixArgs o{};
+    o.f16 = f16_;
+    o.h_in = h0_;
+    o.h_out = nullptr;
+    o.part = partF_;
+    o.n_part = splitF_;
+    o.ldp = C;
+    o.part_stride = RC;
+    o.ln_w = lnout_w_;
+    o.ln_b = lnout_b_;
+    o.n_mix = 1;
+    o.x_hi = xo_hi_;
+    o.x_lo = xo_lo_;
+    o.mix_stride = RC;
+    o.ldx = C;
+    o.shift = nullptr;
+    o.C = C;
+    o.row_map = d_lg_rows_;
+    return o;
+  };
+  for (int l = 0; l < Lc; ++l) {
+    const LayerW& w = L_[l];
+    LnMixArgs m = ln_att_args(l);
     // ---- r, k, v and the LoRA-down projections (w, a, v, g) in one launch (7 segments)
     GemmArgs g{};
     g.f16 = f16_;
@@ -679,12 +679,25 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     if (w.quant) { go.q_fmt = w.quant; go.qw = w.q_o; go.qs = w.s_o; go.q_shift = w.qs_o; }
     go.wt = (wt_mask_ >> 1) & 1;
     go.exp = dbg_exp_ >> 8;
+    // ---- ffn: residual + Wo partials -> LN2 -> mix
+    LnMixArgs f = m;
+    f.emb = nullptr;  // (layer 0's embedding fusion belongs to the attention LayerNorm only)
+    f.h_in = h1_;
+    f.h_out = h0_;
+    f.part = partO_;
+    f.n_part = splitO_;
+    f.ln_w = w.ln2_w;
+    f.ln_b = w.ln2_b;
+    f.n_mix = 1;
+    f.mu[0] = w.ffn_xk;
+    f.x_hi = xf_hi_;
+    f.x_lo = xf_lo_;
+    f.shift = ffn_sh_;
+    f.wt = (wt_mask_ >> 7) & 1;
     // decode steps: the attention half as ONE persistent launch (k_att_persist: LN1 + mixes, rkv +
     // LoRA-down, WKV, Wo with in-launch hand-offs; bit-identical outputs) where the shapes allow it
     bool att_persisted = false;
-    if (use_layer) {
-      att_persisted = true;  // launched with the FFN half below (k_layer_persist)
-    } else if (use_att) {
+    if (use_att) {
       m.tl = g.tl = k.tl = go.tl = tl_next("att_persist");
       prof_begin(&ev);
       att_persisted = launch_att_persist(m, g, k, go, att_sync_ + (size_t)l * kAttSyncInts,
@@ -721,21 +734,6 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
       if (!(dbg_exp_ & 0x40000)) launch_gemm(go, stream_);
       prof_end("gemm_wo", ev);
     }
-    // ---- ffn: residual + Wo partials -> LN2 -> mix
-    LnMixArgs f = m;
-    f.emb = nullptr;  // (layer 0's embedding fusion belongs to the attention LayerNorm only)
-    f.h_in = h1_;
-    f.h_out = h0_;
-    f.part = partO_;
-    f.n_part = splitO_;
-    f.ln_w = w.ln2_w;
-    f.ln_b = w.ln2_b;
-    f.n_mix = 1;
-    f.mu[0] = w.ffn_xk;
-    f.x_hi = xf_hi_;
-    f.x_lo = xf_lo_;
-    f.shift = ffn_sh_;
-    f.wt = (wt_mask_ >> 7) & 1;
     GemmArgs gk{};
     gk.f16 = f16_;
     gk.nseg = 1;
@@ -772,54 +770,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     // decode steps: the whole FFN half as ONE persistent launch (k_ffn_persist, in-launch
     // hand-offs; bit-identical outputs) where the shapes allow it
     bool persisted = false;
-    if (collect_) {  // building the one-launch step's argument table (no launches)
-      LayerArgs la;
-      if (!prep_layer_args(m, g, k, go, f, gk, gv, step_sync_ + (size_t)l * kStepSyncInts,
-                           l == 0 ? nullptr : step_sync_ + (size_t)(l - 1) * kStepSyncInts, (int*)(d_ctrl_ + S_), R,
-                           H_, att_persist_ >> 1, la)) {
-        RT_CHECK(l == 0, RWKVTTS_EHIP, "one-launch step: a layer after layer 0 is not covered");
-        collect_->clear();  // layer 0 not covered: no table
-        return RWKVTTS_OK;
-      }
-      collect_->push_back(la);
-      continue;
-    }
-    if (use_layer) {
-      f.tl = gk.tl = gv.tl = m.tl = g.tl = k.tl = go.tl = tl_next("layer_persist");
-      prof_begin(&ev);
-      persisted = launch_layer_persist(m, g, k, go, f, gk, gv, layer_sync_ + (size_t)l * kLayerSyncInts,
-                                       layer_sync_ + (size_t)((l + Lc - 1) % Lc) * kLayerSyncInts,
-                                       (int*)(d_ctrl_ + S_), R, H_, stream_, l == 5 ? dbg_astamps2_ : nullptr,
-                                       att_persist_ >> 1);
-      if (persisted) {
-        prof_end("layer_persist", ev);
-      } else {
-        // layer 0 not covered: no launch was made for this layer yet -- the separate launches of
-        // both halves, and for the rest of this forward
-        RT_CHECK(l == 0, RWKVTTS_EHIP, "persistent layer launch: a layer after layer 0 fell back");
-        use_layer = use_att = use_ffn = false;
-        if (tl_base() && tl_n_ > 0) {
-          --tl_n_;
-          if ((int)tl_names_.size() > tl_n_) tl_names_.resize(tl_n_);
-        }
-        m.tl = tl_next("ln_att");
-        prof_begin(&ev);
-        RT_CHECK(launch_ln_mix(m, R, stream_) >= 0, RWKVTTS_EUNSUPPORTED, "layer-0 embedding fusion: unsupported shape");
-        prof_end("ln_mix_att", ev);
-        g.tl = tl_next("gemm_rkv");
-        prof_begin(&ev);
-        launch_gemm(g, stream_);
-        prof_end("gemm_rkv_lora", ev);
-        k.tl = tl_next("wkv");
-        prof_begin(&ev);
-        launch_wkv(k, n_seg, H_, stream_);
-        prof_end("wkv", ev);
-        go.tl = tl_next("gemm_wo");
-        prof_begin(&ev);
-        launch_gemm(go, stream_);
-        prof_end("gemm_wo", ev);
-      }
-    } else if (use_ffn) {
+    if (use_ffn) {
       f.tl = gk.tl = gv.tl = tl_next("ffn_persist");
       prof_begin(&ev);
       persisted = launch_ffn_persist(f, gk, gv, ffn_sync_ + (size_t)l * kFfnSyncInts,
@@ -853,30 +804,8 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
       prof_end("gemm_ffn_value", ev);
     }
   }
-  if (collect_) return RWKVTTS_OK;
   if (n_lg > 0) {
-    LnMixArgs o{};
-    o.f16 = f16_;
-    o.h_in = h0_;
-    o.h_out = nullptr;
-    o.part = partF_;
-    o.n_part = splitF_;
-    o.ldp = C;
-    o.part_stride = RC;
-    o.ln_w = lnout_w_;
-    o.ln_b = lnout_b_;
-    o.n_mix = 1;
-    o.x_hi = xo_hi_;
-    o.x_lo = xo_lo_;
-    o.mix_stride = RC;
-    o.ldx = C;
-    o.shift = nullptr;
-    o.C = C;
-    o.row_map = d_lg_rows_;
-    if (use_step) {  // the step launch's hand-off counters, zero again for the next step
-      o.zero = step_sync_;
-      o.zero_n = Lc * (kStepSyncInts / kSyncStride);
-    }
+    LnMixArgs o = ln_out_args();
     o.tl = tl_next("ln_out");
     prof_begin(&ev);
     launch_ln_mix(o, n_lg, stream_);
@@ -932,25 +861,6 @@ int Engine::upload_plan(const StepPlan& p) {
 }
 
 // Runs one forward step. Decode steps (tok_from_ctrl) replay a cached hipGraph.
-int Engine::build_step_table(int R) {
-  std::vector<LayerArgs> v;
-  collect_ = &v;
-  const int rc = launch_forward(R, R, R, std::min(8193, dims.n_vocab), true, true);
-  collect_ = nullptr;
-  RT_OK(rc);
-  if (v.empty()) {  // the one-launch form does not apply to R rows: remembered, no step launch
-    step_tables_[R] = nullptr;
-    return RWKVTTS_OK;
-  }
-  RT_CHECK((int)v.size() == dims.n_layer, RWKVTTS_EHIP, "one-launch step: a layer fell back");
-  LayerArgs* d = nullptr;
-  RT_OK(alloc(&d, v.size()));
-  RT_HIP(hipMemcpy(d, v.data(), sizeof(LayerArgs) * v.size(), hipMemcpyHostToDevice));
-  step_tables_[R] = d;
-  step_nb_[R] = step_blocks_per_layer(v[0]);
-  return RWKVTTS_OK;
-}
-
 int Engine::set_graph_timing(bool on) {
   RT_HIP(hipSetDevice(device_));
   if (on && !d_gt_) {
@@ -980,7 +890,6 @@ int Engine::run_step(const StepPlan& p, bool upload) {
     if (it == graphs_.end()) {
       // the one-launch step's argument table is uploaded before the capture (no synchronous copy
       // may happen inside it)
-      if (step_persist_ && !step_tables_.count(R)) RT_OK(build_step_table(R));
       // one capture at a time per process: engines owned by different threads (the manager's
       // workers) never capture / instantiate concurrently
       static std::mutex capture_mu;

@@ -51,10 +51,6 @@ struct LnMixArgs {
   const float* ln0_w;
   const float* ln0_b;
   int n_vocab;
-  // ln_out after a one-launch decode step (k_step_persist): block 0 zeroes zero_n hand-off counters
-  // (64 ints apart) from zero, for the next step's launch
-  int* zero;
-  int zero_n;
 };
 
 struct GemmSeg {
@@ -67,9 +63,7 @@ struct GemmSeg {
   int tile_start;      // first 64-column tile index of this segment
 };
 
-// NSEG_ segments and NTINFO_ tile descriptors (the arrays last, so every instantiation shares the
-// scalar fields' layout): GemmArgs (8, 128) everywhere; GemmArgs1 (1, 1) for single-segment
-// launches inside the persistent layer launch, whose kernel arguments must stay under 4 KB.
+// NSEG_ segments and NTINFO_ tile descriptors (the arrays last)
 template <int NSEG_, int NTINFO_>
 struct GemmArgsT {
   int nseg;
@@ -125,16 +119,6 @@ struct GemmArgsT {
   uint32_t tinfo[NTINFO_];
 };
 using GemmArgs = GemmArgsT<8, 128>;
-using GemmArgs1 = GemmArgsT<1, 1>;
-// a single-segment launch's arguments without the segment / descriptor tables
-inline GemmArgs1 gemm_args1(const GemmArgs& a) {
-  GemmArgs1 b;
-  static_assert(offsetof(GemmArgs, seg) == offsetof(GemmArgs1, seg), "shared scalar layout");
-  memcpy((void*)&b, (const void*)&a, offsetof(GemmArgs, seg));
-  b.seg[0] = a.seg[0];
-  b.tinfo[0] = 0;
-  return b;
-}
 
 struct WkvArgs {
   const float* part;   // [n_part][R][ldp]
@@ -205,11 +189,6 @@ struct FfnSync {     // (both persistent launches)
   int head_target;   // attention: rkv workgroups per head (3 tiles x splits)
   int lora_target;   // attention: LoRA-down workgroups (tiles x splits)
   int C;             // attention: channels (r / k / v columns [0, 3C), LoRA-down beyond)
-  int* val_done;     // one-launch step: FFN value workgroups count into shard blockIdx % 8 ...
-  const int* prev_val_done;  // ... and the next layer's LN1 rows wait for the sum of the 8 shards
-  int val_target;    //     of the previous layer (= its value workgroups)
-  int* wo_done;      // one-launch layer: Wo workgroups count in here (kLnReplicas replicas) ...
-  int wo_target;     // ... and the FFN LayerNorm rows wait for all of them
   int opts;          // bit 0: value workgroups request their weights only once the LN rows are
                      // published (not at dispatch); bit 1: longer sleep between polls; bit 2: key
                      // workgroups request their weights after the LN wait (with their X)
@@ -221,39 +200,18 @@ struct FfnSync {     // (both persistent launches)
   // FFN value weights
   int d_w, d_late, d_s, d_v;
   int d_k;  // the FFN key weight streams (d_w: the rkv ones)
+
   // test hook (RWKVTTS_TEST_DROP_ARRIVE, null in production): the first rkv workgroup to find *drop
   // set clears it and skips its head arrival (a hand-off that never completes: the waits time out)
   int* drop;
 };
 
-// one layer's arguments of the one-launch decode step (k_step_persist reads them from a device table)
-struct LayerArgs {
-  LnMixArgs ln;      // LN1 + mixes (layer 0: the embedding form)
-  GemmArgs ga;       // rkv + LoRA-down
-  WkvArgs wa;
-  GemmArgs1 go;      // Wo
-  LnMixArgs lf;      // LN2 + mix
-  GemmArgs1 ka, va;  // FFN key / value
-  FfnSync sy, sf;
-};
-constexpr int kStepSyncInts = (48 + 8 + 8 + 16 + 8) * 64;  // layer block + value-done shards
-bool prep_layer_args(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs& wkv, const GemmArgs& wo,
-                     const LnMixArgs& lf, const GemmArgs& key, const GemmArgs& val, int* cnt, const int* prev_cnt,
-                     int* err, int R, int H, int opts, LayerArgs& out);
-void launch_step_persist(const LayerArgs* dT, int n_layers, int nb, bool f16, unsigned long long* tl, hipStream_t st);
-int step_blocks_per_layer(const LayerArgs& a);
 // The attention half of a decode step (LN1 + mixes, rkv + LoRA-down, WKV, Wo) as ONE persistent
 // launch (k_att_persist); false if the shapes are not covered.
-constexpr int kAttSyncInts = 48 * 64;  // counter block per layer (lm_kernels.hip kAtt*)
+constexpr int kAttSyncInts = kAttCounters * kSyncStride;  // counter block per layer (lm_kernels.hip kAtt*)
 bool launch_att_persist(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs& wkv, const GemmArgs& wo, int* cnt,
                         int* cnt_prev, int* err, int R, int H, hipStream_t st, uint64_t* stamps, int opts,
                         int* drop = nullptr);
-// A decode step's whole layer (both halves) as ONE persistent launch (k_layer_persist); the
-// counter block is kLayerSyncInts.
-constexpr int kLayerSyncInts = (48 + 8 + 8 + 16) * 64;
-bool launch_layer_persist(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs& wkv, const GemmArgs& wo,
-                          const LnMixArgs& lf, const GemmArgs& key, const GemmArgs& val, int* cnt, int* cnt_prev,
-                          int* err, int R, int H, hipStream_t st, uint64_t* stamps, int opts);
 bool launch_ffn_persist(const LnMixArgs& ln, const GemmArgs& key, const GemmArgs& val, int* cnt, int* cnt_prev,
                         int* err, int R, hipStream_t st, uint64_t* stamps = nullptr, int opts = 0);
 // Fills a.tw / a.tinfo / a.n_tinfo when the segments' packed weights are contiguous in 64-column

@@ -426,8 +426,6 @@ __device__ __attribute__((always_inline)) void ln1024_body(const LnMixArgs& a, c
 template <bool F16, int MODE, int NMIX, int NP, bool EMB = false>
 __global__ __launch_bounds__(256) void k_ln1024(LnMixArgs a) {
   tl_begin(a.tl);
-  if (a.zero && blockIdx.x == 0)
-    for (int i = threadIdx.x; i < a.zero_n; i += 256) a.zero[i * 64] = 0;
   ln1024_body<F16, MODE, NMIX, NP, EMB>(a, blockIdx.x);
   tl_end(a.tl);
 }
@@ -639,35 +637,17 @@ __device__ inline void sync_wait(const int* c, int target, int* err, int code, i
   }
   __syncthreads();
 }
-// wait until the sum of `shards` counters (kSyncStride ints apart) reaches target (one lane polls)
-__device__ inline void sync_wait_sum(const int* c, int shards, int target, int* err, int code) {
-  if (threadIdx.x == 0) {
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    for (;;) {
-      int sum = 0;
-      for (int i = 0; i < shards; ++i)
-        sum += __hip_atomic_load((gint_t*)(c + i * kSyncStride), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (sum >= target) break;
-      __builtin_amdgcn_s_sleep(8);
-      if (__builtin_amdgcn_s_memrealtime() - t0 > 5000000ull) {
-        __hip_atomic_fetch_or((gint_t*)err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-  }
-  __syncthreads();
-}
 // publish: every wave's write-through (sc1) stores drained, then ONE lane counts the workgroup in
 // (replicas > 1: lanes 0..replicas-1 of wave 0 add to one replica each, kSyncStride ints apart).
 // drop (test hook, replicas == 1 only): lane 0 skips the add once if it finds *drop set
-__device__ inline void sync_arrive(int* c, int replicas = 1, int* drop = nullptr) {
+__device__ inline void sync_arrive(int* c, int replicas = 1, int* drop = nullptr, int inc = 1) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (drop && threadIdx.x == 0 &&
       __hip_atomic_exchange((gint_t*)drop, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
     return;
   if (threadIdx.x < replicas)
-    __hip_atomic_fetch_add((gint_t*)(c + threadIdx.x * kSyncStride), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add((gint_t*)(c + threadIdx.x * kSyncStride), inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // hold a prefetch back until `ticks` (10 ns) after the launch's first s_memrealtime read here
 __device__ inline void hold_until(int ticks) {
@@ -784,6 +764,12 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
   if constexpr (QW) {
     if (threadIdx.x < 16) s_qlut[threadIdx.x] = kNF4[threadIdx.x];
   }
+  // kXRelu2 element map: chunk u of this thread -> (row, first column) of the K-slice (chunk c =
+  // tid + 256 u: row c / (KS / 4)). (Round 5 measured a per-wave map for the persistent value role --
+  // wave w = key tile 4 split + w, each wave waiting for its own tile: 1 % slower at 32 rows,
+  // tools/experiments/r05_ln_tail_value_stream.patch.)
+  auto x_row = [&](int u) { return (int)((threadIdx.x + u * 256) / (KS / 4)); };
+  auto x_col = [&](int u) { return (int)(((threadIdx.x + u * 256) % (KS / 4)) * 4); };
   auto load_x = [&]() {
   if constexpr (XMODE == kXPlanes) {
     if constexpr (ROLE != 0) {  // handed-off planes: sc1 loads only
@@ -813,14 +799,13 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
     }
     }
   } else {
-    if constexpr (ROLE != 0) {  // handed-off key slabs: sc1 loads only
+    if constexpr (ROLE != 0) {  // handed-off key slabs: sc1 loads only (x_row / x_col: the wave-tile map)
 #pragma unroll
       for (int p = 0; p < NX; ++p) {
         const auto rp = wt_rsrc(a.x_part + p * a.x_part_stride);
 #pragma unroll
         for (int u = 0; u < PERR; ++u) {
-          const int c = threadIdx.x + u * 256;
-          const int r = c / (KS / 4), k4 = (c % (KS / 4)) * 4;
+          const int r = x_row(u), k4 = x_col(u);
           xr[p][u] = (float4_){0.f, 0.f, 0.f, 0.f};
           if (xrow0 + r < a.M)
             xr[p][u] = __builtin_bit_cast(float4_, ld_sc1_b128(rp, ((xrow0 + r) * a.x_ld + kbeg + k4) * 4));
@@ -931,7 +916,7 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
       __syncthreads();
 #pragma unroll
       for (int u = 0; u < PERR; ++u) {
-        const int r = (threadIdx.x + u * 256) / (KS / 4);
+        const int r = x_row(u);
         const float m = fmaxf(fmaxf(y4[u][0], y4[u][1]), fmaxf(y4[u][2], y4[u][3]));
         if (m >= 32768.f) atomicMax(&s_rexp[r], as_u32(m));  // non-negative floats order as uints
       }
@@ -939,8 +924,7 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
     }
 #pragma unroll
     for (int u = 0; u < PERR; ++u) {
-      const int c = threadIdx.x + u * 256;
-      const int r = c / (KS / 4), k4 = (c % (KS / 4)) * 4;
+      const int r = x_row(u), k4 = x_col(u);
       float y[4] = {y4[u][0], y4[u][1], y4[u][2], y4[u][3]};
       if constexpr (F16) {
         const uint32_t mb = s_rexp[r];
@@ -1092,12 +1076,6 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
   }
   if constexpr (ROLE != 0) sync_stamp(sy, 2);
   if constexpr (ROLE == 1) sync_arrive(sy.cnt + kSyncStride * (kLnReplicas + tile / sy.key_group));
-  if constexpr (ROLE == 2) {
-    if (sy.val_done) sync_arrive(sy.val_done + kSyncStride * (blockIdx.x & (kLnReplicas - 1)));
-  }
-  if constexpr (ROLE == 4) {
-    if (sy.wo_done) sync_arrive(sy.wo_done, kLnReplicas);
-  }
   if constexpr (ROLE == 3) {
     const int c0 = col_off + (tile - tstart) * 64;  // this tile's first output column
     if (c0 < 3 * sy.C) sync_arrive(sy.cnt + kSyncStride * (kAttHead + ((c0 % sy.C) >> 6)), 1, sy.drop);
@@ -2270,7 +2248,7 @@ __device__ __attribute__((always_inline)) void wkv6_body(const WkvArgs& a, const
       vp[p] = pp[2 * C + c];
     }
     }
-    if constexpr (ROLE == 1)  // (layer 0's WKV may have written it in this same launch: k_step_persist)
+    if constexpr (ROLE == 1)
       vf = a.layer > 0 ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
                                                      wt_rsrc(a.v_first + (int64_t)row * a.ldv), c * 4, 0, 16))
                        : 0.f;
@@ -2494,7 +2472,10 @@ __global__ __launch_bounds__(256) void k_wkv6(WkvArgs a) {
 //   blocks [+n_key, +n_wkv)        WKV workgroups (slot, head; head h on one XCD): LoRA-up rows and
 //                                  state at dispatch, wait for the head's tiles and the LoRA-down
 //                                  tiles, partials by sc1 loads, z row written through, counted
-//                                  into the head's WKV counter;
+//                                  into the head's WKV counter (two slots per workgroup, so that
+//                                  every WKV workgroup is resident at dispatch, measured slower in
+//                                  round 5: 758 -> 803 us per step at B = 32, 624 -> 655 at B = 1 --
+//                                  a slot's WKV arithmetic is latency the second slot does not hide);
 //   blocks [+n_wkv, +n_wo)         Wo workgroups (XCD-aware): weights at dispatch, wait for the
 //                                  WKV workgroups of their K-slice's two heads, z by sc1 loads.
 // Dependencies point to lower block indices only (see k_ffn_persist); outputs are the four
@@ -2519,49 +2500,6 @@ __global__ __launch_bounds__(256, 2) void k_att_persist(LnMixArgs ln, GemmArgs g
     wkv6_body<F16, 1>(wa, b, 0, sy);
   } else {
     gemm2_body<2, 4, kXPlanes, F16, 1, 0, false, 4>(go, b - sy.n_wkv, 0, sy);
-  }
-  sync_stamp(sy, 3);
-  tl_end(ln.tl);
-}
-
-// ------------------------------------------------------------------------------------
-// layer_persist: a decode step's WHOLE layer as one launch: k_att_persist's blocks, then
-// k_ffn_persist's, whose LayerNorm rows wait for every Wo workgroup (wo_done replicas) and read
-// the residual and the Wo slabs by sc1 loads. One launch boundary per layer instead of two.
-// ------------------------------------------------------------------------------------
-template <bool F16, bool EMB>
-__global__ __launch_bounds__(256, 2) void k_layer_persist(LnMixArgs ln, GemmArgs ga, WkvArgs wa, GemmArgs1 go,
-                                                          LnMixArgs lf, GemmArgs1 ka, GemmArgs1 va, FfnSync sy,
-                                                          FfnSync sf) {
-  int b = blockIdx.x;
-  tl_begin(ln.tl);
-  sync_stamp(sy, 0);
-  const int n_att = sy.n_ln_blocks + sy.n_key + sy.n_wkv + 16 * go.k_split;
-  if (b < n_att) {
-    if (b < sy.n_ln_blocks) {
-      if (b == 0 && threadIdx.x < sy.n_prev) sy.cnt_prev[threadIdx.x * kSyncStride] = 0;
-      if (b < sy.ln_rows) {
-        if constexpr (EMB) ln1024_body<F16, 1, 6, 0, true>(ln, b);
-        else ln1024_body<F16, 1, 6, 16>(ln, b);
-        sync_arrive(sy.cnt + kSyncStride * kAttLn, kLnReplicas);
-      }
-    } else if ((b -= sy.n_ln_blocks) < sy.n_key) {
-      gemm2_body<2, 8, kXPlanes, F16, 1, 2, false, 3>(ga, b % sy.rkv_tiles, b / sy.rkv_tiles, sy);
-    } else if ((b -= sy.n_key) < sy.n_wkv) {
-      wkv6_body<F16, 1>(wa, b, 0, sy);
-    } else {
-      gemm2_body<2, 4, kXPlanes, F16, 1, 0, false, 4>(go, b - sy.n_wkv, 0, sy);
-    }
-  } else if ((b -= n_att) < sf.n_ln_blocks) {
-    if (b < sf.ln_rows) {
-      sync_wait(sy.wo_done + kSyncStride * (blockIdx.x & (kLnReplicas - 1)), sy.wo_target, sf.err, 128, sf.opts);
-      ln1024_body<F16, 1, 1, 8, false, true>(lf, b);
-      sync_arrive(sf.cnt, kLnReplicas);
-    }
-  } else if ((b -= sf.n_ln_blocks) < sf.n_key) {
-    gemm2_body<2, 8, kXPlanes, F16, 1, 0, false, 1>(ka, b, 0, sf);
-  } else {
-    gemm2_body<2, 8, kXRelu2, F16, 4, 0, false, 2>(va, b - sf.n_key, 0, sf);
   }
   sync_stamp(sy, 3);
   tl_end(ln.tl);
@@ -2621,54 +2559,6 @@ static bool prep_att_persist(const LnMixArgs& ln, const GemmArgs& rkv, const Wkv
   return true;
 }
 
-// ------------------------------------------------------------------------------------
-// step_persist: a decode step's 24 layers as ONE launch: layer l's k_layer_persist blocks at
-// [l * nb, (l + 1) * nb), their arguments read from a device table (LayerArgs[L]); layer l's LN1
-// rows wait for the previous layer's FFN value workgroups (8 shards) and read its residual and
-// slabs by sc1 loads. Counters are zeroed by the ln_out launch that follows (LnMixArgs::zero).
-// ------------------------------------------------------------------------------------
-template <bool F16>
-__global__ __launch_bounds__(256, 2) void k_step_persist(const LayerArgs* __restrict__ T, int nb,
-                                                         unsigned long long* tl) {
-  const int layer = blockIdx.x / nb;
-  int b = blockIdx.x - layer * nb;
-  const LayerArgs& A = T[layer];
-  const FfnSync& sy = A.sy;
-  const FfnSync& sf = A.sf;
-  tl_begin(tl);
-  const int n_att = sy.n_ln_blocks + sy.n_key + sy.n_wkv + 16 * A.go.k_split;
-  if (b < n_att) {
-    if (b < sy.n_ln_blocks) {
-      if (b < sy.ln_rows) {
-        if (layer == 0) {
-          ln1024_body<F16, 1, 6, 0, true>(A.ln, b);
-        } else {
-          sync_wait_sum(sy.prev_val_done, kLnReplicas, sy.val_target, sy.err, 256);
-          ln1024_body<F16, 1, 6, 16, false, true>(A.ln, b);
-        }
-        sync_arrive(sy.cnt + kSyncStride * kAttLn, kLnReplicas);
-      }
-    } else if ((b -= sy.n_ln_blocks) < sy.n_key) {
-      gemm2_body<2, 8, kXPlanes, F16, 1, 2, false, 3>(A.ga, b % sy.rkv_tiles, b / sy.rkv_tiles, sy);
-    } else if ((b -= sy.n_key) < sy.n_wkv) {
-      wkv6_body<F16, 1>(A.wa, b, 0, sy);
-    } else {
-      gemm2_body<2, 4, kXPlanes, F16, 1, 0, false, 4>(A.go, b - sy.n_wkv, 0, sy);
-    }
-  } else if ((b -= n_att) < sf.n_ln_blocks) {
-    if (b < sf.ln_rows) {
-      sync_wait(sy.wo_done + kSyncStride * (blockIdx.x & (kLnReplicas - 1)), sy.wo_target, sf.err, 128, sf.opts);
-      ln1024_body<F16, 1, 1, 8, false, true>(A.lf, b);
-      sync_arrive(sf.cnt, kLnReplicas);
-    }
-  } else if ((b -= sf.n_ln_blocks) < sf.n_key) {
-    gemm2_body<2, 8, kXPlanes, F16, 1, 0, false, 1>(A.ka, b, 0, sf);
-  } else {
-    gemm2_body<2, 8, kXRelu2, F16, 4, 0, false, 2>(A.va, b - sf.n_key, 0, sf);
-  }
-  tl_end(tl);
-}
-
 bool launch_att_persist(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs& wkv, const GemmArgs& wo, int* cnt,
                         int* cnt_prev, int* err, int R, int H, hipStream_t st, uint64_t* stamps, int opts,
                         int* drop) {
@@ -2692,88 +2582,6 @@ bool launch_att_persist(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs&
     else RT_LAUNCH((k_att_persist<false, false>), grid, dim3(256), lds, st, l, ga, wa, gw, sy);
   }
   return true;
-}
-
-bool launch_layer_persist(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs& wkv, const GemmArgs& wo,
-                          const LnMixArgs& lf, const GemmArgs& key, const GemmArgs& val, int* cnt, int* cnt_prev,
-                          int* err, int R, int H, hipStream_t st, uint64_t* stamps, int opts) {
-  // counter block: [0, kAttCounters) attention, [kAttCounters, +kLnReplicas) Wo done,
-  // [kLayerFfn, +kLnReplicas + kFfnSlices) FFN (FfnSync's own layout from there)
-  constexpr int kWoDone = kAttCounters, kFfn = kAttCounters + kLnReplicas;
-  AttPrep A;
-  FfnPrep F;
-  if (!prep_att_persist(ln, rkv, wkv, wo, cnt, cnt_prev, err, R, H, stamps, opts, A)) return false;
-  if (!prep_ffn_persist(lf, key, val, cnt + kSyncStride * kFfn, cnt_prev + kSyncStride * kFfn, err, R, nullptr, opts,
-                        F))
-    return false;
-  A.sy.n_prev = kFfn + kLnReplicas + kFfnSlices;  // block 0 zeroes the previous layer's whole block
-  A.sy.wo_done = cnt + kSyncStride * kWoDone;
-  A.sy.wo_target = 16 * wo.k_split;
-  F.sy.n_prev = 0;
-  const int n_att = A.sy.n_ln_blocks + A.sy.n_key + A.sy.n_wkv + 16 * wo.k_split;
-  const size_t lds = (size_t)2 * 16 * (8 * 32 + 8) * 2 * 2;
-  const dim3 grid(n_att + F.sy.n_ln_blocks + F.sy.n_key + F.nv);
-  const bool emb = ln.emb != nullptr;
-  const GemmArgs1 gw1 = gemm_args1(A.gw), ka1 = gemm_args1(F.ka), va1 = gemm_args1(F.va);
-  static_assert(sizeof(LnMixArgs) * 2 + sizeof(GemmArgs) + sizeof(WkvArgs) + 3 * sizeof(GemmArgs1) +
-                        2 * sizeof(FfnSync) <= 4096, "k_layer_persist's arguments must fit 4 KB");
-#define LP(F16_, EMB_)                                                                                       \
-  RT_LAUNCH((k_layer_persist<F16_, EMB_>), grid, dim3(256), lds, st, A.l, A.ga, A.wa, gw1, F.l, ka1, va1, A.sy, F.sy)
-  if (ln.f16) {
-    if (emb) LP(true, true);
-    else LP(true, false);
-  } else {
-    if (emb) LP(false, true);
-    else LP(false, false);
-  }
-#undef LP
-  return true;
-}
-
-// One layer of the one-launch step: its k_layer_persist arguments plus the layer-to-layer hand-off
-// (this layer's value-done shards, the previous layer's to wait for). cnt: this layer's
-// kStepSyncInts block; prev_cnt: the previous layer's (null for layer 0). No zeroing in-launch.
-bool prep_layer_args(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs& wkv, const GemmArgs& wo,
-                     const LnMixArgs& lf, const GemmArgs& key, const GemmArgs& val, int* cnt, const int* prev_cnt,
-                     int* err, int R, int H, int opts, LayerArgs& out) {
-  constexpr int kWoDone = kAttCounters, kFfn = kAttCounters + kLnReplicas, kValDone = kFfn + kLnReplicas + kFfnSlices;
-  AttPrep A;
-  FfnPrep F;
-  int* dummy_prev = cnt + kSyncStride * 1;  // (prep requires cnt != cnt_prev; n_prev = 0 below)
-  if (!prep_att_persist(ln, rkv, wkv, wo, cnt, dummy_prev, err, R, H, nullptr, opts, A)) return false;
-  if (!prep_ffn_persist(lf, key, val, cnt + kSyncStride * kFfn, dummy_prev, err, R, nullptr, opts, F)) return false;
-  if ((prev_cnt == nullptr) != (ln.emb != nullptr)) return false;  // layer 0 (embedding form) has no predecessor
-  A.sy.n_prev = 0;
-  A.sy.cnt_prev = nullptr;
-  A.sy.wo_done = cnt + kSyncStride * kWoDone;
-  A.sy.wo_target = 16 * wo.k_split;
-  A.sy.prev_val_done = prev_cnt ? prev_cnt + kSyncStride * kValDone : nullptr;
-  A.sy.val_target = F.nv;
-  F.sy.n_prev = 0;
-  F.sy.cnt_prev = nullptr;
-  F.sy.val_done = cnt + kSyncStride * kValDone;
-  out.ln = A.l;
-  out.ga = A.ga;
-  out.wa = A.wa;
-  out.go = gemm_args1(A.gw);
-  out.lf = F.l;
-  out.ka = gemm_args1(F.ka);
-  out.va = gemm_args1(F.va);
-  out.sy = A.sy;
-  out.sf = F.sy;
-  return true;
-}
-
-int step_blocks_per_layer(const LayerArgs& a) {
-  return a.sy.n_ln_blocks + a.sy.n_key + a.sy.n_wkv + 16 * a.go.k_split + a.sf.n_ln_blocks + a.sf.n_key +
-         (a.va.seg[0].N + 63) / 64 * a.va.k_split;
-}
-
-void launch_step_persist(const LayerArgs* dT, int n_layers, int nb, bool f16, unsigned long long* tl, hipStream_t st) {
-  const size_t lds = (size_t)2 * 16 * (8 * 32 + 8) * 2 * 2;
-  const dim3 grid(n_layers * nb);
-  if (f16) RT_LAUNCH((k_step_persist<true>), grid, dim3(256), lds, st, dT, nb, tl);
-  else RT_LAUNCH((k_step_persist<false>), grid, dim3(256), lds, st, dT, nb, tl);
 }
 
 int wkv_perm_layout(int Dw, int Da, int Dv, int Dg, int n_part, int max_slots, int variant) {

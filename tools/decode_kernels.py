@@ -13,12 +13,14 @@ DECODE = {
     "wkv": (("k_wkv6<false, false>", "k_wkv6<false>"), 131072),
     "ln_mix_att": (("k_ln1024<false, 1, 6, 16",), 8192),
     "ln_mix_ffn": (("k_ln1024<false, 1, 1, 8",), 8192),
-    # the persistent decode launches (round 4): 32 LN + 212 rkv + 512 WKV + 128 Wo blocks and
-    # 32 LN + 256 key + 256 value blocks of 256 threads
-    "att_persist": (("k_att_persist<false, true>", "k_att_persist<false, false>"), 884 * 256),
-    "ffn_persist": (("k_ffn_persist<false>",), 544 * 256),
-    "layer_persist": (("k_layer_persist<false, true>", "k_layer_persist<false, false>"), 1428 * 256),
+    # the persistent decode launches: 32 LN + 212 rkv + 512 WKV + 128 Wo blocks and 32 LN + 256 key +
+    # 256 value blocks of 256 threads
+    "att_persist": (("k_att_persist<false,",), 884 * 256),
+    "ffn_persist": (("k_ffn_persist<false",), 544 * 256),
 }
+# persistent attention launch grid (threads) -> rows of the decode step: 32 LN + 212 rkv + 16 R WKV +
+# 128 Wo blocks (the tail form: 212 + 16 R + 128 + 32 LN2 blocks, the same count for layers > 0)
+ATT_GRIDS = {(372 + 16 * r) * 256: r for r in range(1, 33)}
 
 
 def match(acc, prefixes, grid):

@@ -1,7 +1,7 @@
 """Persistent-launch per-block stamps (layer 5 of the last decode step): k_ffn_persist
 (RWKVTTS_FFN_STAMPS; roles LayerNorm rows, key, value) or k_att_persist (RWKVTTS_ATT_STAMPS; roles
 LayerNorm rows, rkv, WKV, Wo): per role the min / median / max of each stamp in us from the
-launch's first block start. Usage: ffn_stamps.py [S] [ffn|att|layer] [B] (B requests, default 32;
+launch's first block start. Usage: ffn_stamps.py [S] [ffn|att] [B] (B requests, default 32;
 S semantic; B < 16 sets RWKVTTS_PERSIST_MIN_ROWS=1 so the persistent launches run)."""
 import os
 import sys
@@ -14,8 +14,6 @@ sys.path.insert(0, os.path.join(ROOT, "rwkv-tts-rs_amd"))
 which = sys.argv[2] if len(sys.argv) > 2 else "ffn"
 path = os.path.join(tempfile.mkdtemp(), "stamps.bin")
 os.environ["RWKVTTS_FFN_STAMPS" if which == "ffn" else "RWKVTTS_ATT_STAMPS"] = path
-if which == "att":  # the attention launch alone (two launches per layer)
-    os.environ.setdefault("RWKVTTS_LAYER_PERSIST", "0")
 B = int(sys.argv[3]) if len(sys.argv) > 3 else 32
 if B < 16:
     os.environ.setdefault("RWKVTTS_PERSIST_MIN_ROWS", "1")
@@ -41,8 +39,6 @@ nw = 16 * B  # WKV workgroups: one per (row, head)
 ae = 244 + nw + 128
 roles = ({"ln": (0, 32), "key": (32, 288), "value": (288, 544)} if which == "ffn" else
          {"ln": (0, 32), "rkv": (32, 244), "wkv": (244, 244 + nw), "wo": (244 + nw, ae)})
-if which == "layer":  # k_layer_persist: the attention blocks, then the FFN blocks
-    roles.update({"ffn_ln": (ae, ae + 32), "key": (ae + 32, ae + 288), "value": (ae + 288, ae + 544)})
 nb = max(e for _, e in roles.values())
 t0 = a[:nb, 0][a[:nb, 0] > 0].min()
 names = ["start", "wait_done", "work_done", "end"]
