@@ -170,6 +170,9 @@ class Engine {
   // 637-642 -> 622 us per step, B = 8: 693 -> 677-679, B = 32: 771-782 -> 754-768;
   // profiles/r04h7_small_batch_ab.txt)
   int persist_min_rows_ = 1;
+  // one-row decode steps: the row-fused persistent form (each GEMM workgroup computes the row's
+  // LayerNorm itself; lm_kernels.h launch_att_persist). RWKVTTS_FUSE_LN1=0 turns it off.
+  bool fuse_ln1_ = true;
   int ffn_persist_ = 5;     // RWKVTTS_FFN_PERSIST: decode steps' FFN half as one launch (k_ffn_persist);
                             // 0 off, else 1 + 2 x launch options (5: long poll sleep, the measured best)
   int* ffn_sync_ = nullptr; // its hand-off counters: [L][kFfnSyncInts] (give-up code: d_ctrl_[S_])

@@ -164,6 +164,7 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
   if (const char* fp = getenv("RWKVTTS_FFN_PERSIST")) ffn_persist_ = atoi(fp);
   if (const char* ap = getenv("RWKVTTS_ATT_PERSIST")) att_persist_ = atoi(ap);
   if (const char* pm = getenv("RWKVTTS_PERSIST_MIN_ROWS")) persist_min_rows_ = atoi(pm);
+  if (const char* fl = getenv("RWKVTTS_FUSE_LN1")) fuse_ln1_ = atoi(fl) != 0;
   if ((ffn_persist_ || att_persist_) && !claim_persistent(desc.device, this, &lock_fd_)) ffn_persist_ = att_persist_ = 0;
   if (const char* gp = getenv("RWKVTTS_GEMM_STAMPS")) {
     dbg_gstamp_path_ = gp;
@@ -703,7 +704,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
       att_persisted = launch_att_persist(m, g, k, go, att_sync_ + (size_t)l * kAttSyncInts,
                                          att_sync_ + (size_t)((l + Lc - 1) % Lc) * kAttSyncInts,
                                          (int*)(d_ctrl_ + S_), R, H_, stream_, l == 5 ? dbg_astamps2_ : nullptr,
-                                         att_persist_ >> 1, d_drop_);
+                                         att_persist_ >> 1, d_drop_, fuse_ln1_);
       if (att_persisted) {
         prof_end("att_persist", ev);
       } else {
@@ -776,7 +777,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
       persisted = launch_ffn_persist(f, gk, gv, ffn_sync_ + (size_t)l * kFfnSyncInts,
                                      ffn_sync_ + (size_t)((l + Lc - 1) % Lc) * kFfnSyncInts,
                                      (int*)(d_ctrl_ + S_), R, stream_, l == 5 ? dbg_fstamps_ : nullptr,
-                                     ffn_persist_ >> 1);
+                                     ffn_persist_ >> 1, fuse_ln1_);
       if (persisted) {
         prof_end("ffn_persist", ev);
       } else {

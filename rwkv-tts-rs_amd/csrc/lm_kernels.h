@@ -161,7 +161,8 @@ int launch_ln_mix(const LnMixArgs& a, int n_out_rows, hipStream_t st);
 int launch_gemm(const GemmArgs& a, hipStream_t st);
 // The FFN half of a decode step (LN2 + mix, key GEMM, relu^2, value GEMM) as ONE persistent launch
 // with in-launch hand-offs (k_ffn_persist); false if the shapes are not covered.
-constexpr int kFfnSyncInts = 24 * 64;  // counter block per layer: (8 LN replicas + 16 K-slices) x 256 B
+constexpr int kFfnKeyDone = 24;       // row-fused form: key workgroups done (the shift writer waits)
+constexpr int kFfnSyncInts = 25 * 64;  // counter block per layer: (8 LN replicas + 16 K-slices + 1) x 256 B
 // ---- persistent launches: hand-off counters and their arguments (lm_kernels.hip) ----------
 // Inter-workgroup hand-offs of the persistent FFN launch (k_ffn_persist): counters kSyncStride
 // ints (256 B) apart (see lm_kernels.hip for each launch's layout).
@@ -173,7 +174,8 @@ constexpr int kAttLn = 0;      // kLnReplicas: LayerNorm rows published
 constexpr int kAttHead = 8;    // 16: head h's r / k / v tiles published (3 tiles x the K-splits)
 constexpr int kAttLora = 24;   // kLnReplicas: the LoRA-down tiles published
 constexpr int kAttWkv = 32;    // 16: WKV workgroups of head h done (one per row)
-constexpr int kAttCounters = 48;
+constexpr int kAttRkvDone = 48; // row-fused form: rkv workgroups done (the shift writer waits)
+constexpr int kAttCounters = 49;
 struct FfnSync {     // (both persistent launches)
   int* cnt;          // this layer's counters (zero at launch)
   int* cnt_prev;     // the counters of the layer launched before this one: zeroed by block 0
@@ -185,6 +187,7 @@ struct FfnSync {     // (both persistent launches)
   int key_group;     // FFN: key column tiles per value K-slice
   int key_per_slice; // FFN: key workgroups per value K-slice (key_group x key splits)
   int n_wkv;         // attention: WKV workgroups
+  int n_val;         // FFN: value workgroups
   int rkv_tiles;     // attention: column tiles of the rkv launch (its grid is tiles x splits)
   int head_target;   // attention: rkv workgroups per head (3 tiles x splits)
   int lora_target;   // attention: LoRA-down workgroups (tiles x splits)
@@ -209,11 +212,17 @@ struct FfnSync {     // (both persistent launches)
 // The attention half of a decode step (LN1 + mixes, rkv + LoRA-down, WKV, Wo) as ONE persistent
 // launch (k_att_persist); false if the shapes are not covered.
 constexpr int kAttSyncInts = kAttCounters * kSyncStride;  // counter block per layer (lm_kernels.hip kAtt*)
+// fused_ln (one decode row, no embedding form): the row-fused form -- no LayerNorm blocks; every
+// rkv / key workgroup computes the row's LayerNorm itself from the residual and the partial slabs
+// (68 / 36 KB) and stages only its K-slice's mix, and one trailing workgroup stores the residual
+// and the new token-shift row once every GEMM workgroup has read the old one (kAttRkvDone /
+// kFfnKeyDone). Replaces the LayerNorm phase and its hand-off at batch 1.
 bool launch_att_persist(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs& wkv, const GemmArgs& wo, int* cnt,
                         int* cnt_prev, int* err, int R, int H, hipStream_t st, uint64_t* stamps, int opts,
-                        int* drop = nullptr);
+                        int* drop = nullptr, bool fused_ln = false);
 bool launch_ffn_persist(const LnMixArgs& ln, const GemmArgs& key, const GemmArgs& val, int* cnt, int* cnt_prev,
-                        int* err, int R, hipStream_t st, uint64_t* stamps = nullptr, int opts = 0);
+                        int* err, int R, hipStream_t st, uint64_t* stamps = nullptr, int opts = 0,
+                        bool fused_ln = false);
 // Fills a.tw / a.tinfo / a.n_tinfo when the segments' packed weights are contiguous in 64-column
 // tiles and every segment's X is seg[0]'s planes plus a multiple of x_mix_stride; returns whether
 // the table applies (otherwise the kernel looks the segment up).

@@ -279,6 +279,20 @@ __global__ __launch_bounds__(256) void k_ln_mix(LnMixArgs a) {
   }
 }
 
+// The C = 1024 LayerNorm of one row in a 256-thread workgroup, thread t holding columns
+// [4t, 4t + 4): two one-barrier block sums (mean, then the centred second moment), x = d * rstd * w
+// + b. Shared by ln1024_body and the row-fused GEMM roles (gemm2_body ROLE 5 / 6), so both give the
+// same bits.
+__device__ __attribute__((always_inline)) inline void ln1024_apply(float4_& x, const float4_& w, const float4_& b,
+                                                                   float* red, int slot_base) {
+  constexpr int C = 1024;
+  const float mean = block_sum_1b((x[0] + x[1]) + (x[2] + x[3]), red, slot_base) * (1.0f / C);
+  const float4_ d = x - mean;
+  const float var = block_sum_1b((d[0] * d[0] + d[1] * d[1]) + (d[2] * d[2] + d[3] * d[3]), red, slot_base + 1) * (1.0f / C);
+  const float rstd = 1.0f / sqrtf(var + 1e-5f);
+  x = d * rstd * w + b;
+}
+
 // ------------------------------------------------------------------------------------
 // ln1024: k_ln_mix for C = 1024 with the weight format, the mix count and the partial-slab count
 // as template parameters (no per-element guards, no runtime format select, packed hardware
@@ -378,13 +392,7 @@ __device__ __attribute__((always_inline)) void ln1024_body(const LnMixArgs& a, c
     if (wt) store_wt(wt_rsrc(e_hout), (int)(((int64_t)row * C + c) * 4), v);
     else *(float4_*)(e_hout + (int64_t)row * C + c) = v;
   }
-  auto ln = [&](float4_& x, int slot_base) {
-    const float mean = block_sum_1b((x[0] + x[1]) + (x[2] + x[3]), red, slot_base) * (1.0f / C);
-    const float4_ d = x - mean;
-    const float var = block_sum_1b((d[0] * d[0] + d[1] * d[1]) + (d[2] * d[2] + d[3] * d[3]), red, slot_base + 1) * (1.0f / C);
-    const float rstd = 1.0f / sqrtf(var + 1e-5f);
-    x = d * rstd * w + b;
-  };
+  auto ln = [&](float4_& x, int slot_base) { ln1024_apply(x, w, b, red, slot_base); };
   ln(v, 0);
   auto store = [&](const float4_& x, bf16_t* hi, bf16_t* lo, int64_t idx) {
     uint32_t h0, l0, h1, l1;
@@ -665,10 +673,14 @@ __device__ inline u32x4_ ld_sc1_b128(__amdgpu_buffer_rsrc_t r, int off_bytes) {
 // first, then wait for its K-slice's key slabs, read them by sc1 loads). ROLE 3: rkv workgroup of
 // k_att_persist (as ROLE 1; publishes to its head's counter, or the LoRA-down counter). ROLE 4:
 // Wo workgroup (weights first, then wait for the WKV workgroups of its K-slice's two heads).
+// ROLE 5 / 6: the row-fused forms of ROLE 3 / 1 (one decode row): weights at dispatch, then the
+// row's LayerNorm computed here from the residual and the partial slabs (*lr: LN1 with 16 value
+// slabs / LN2 with 8 Wo slabs; ln1024_apply, the LayerNorm rows' arithmetic bit for bit) and only
+// this K-slice's mix staged as row 0 of the X image -- no LayerNorm rows, no hand-off before the GEMM.
 // by: the split index of an xmap-0 grid (blockIdx.y for a plain launch).
 template <int MT, int KSTEPS, int XMODE, bool F16, int NX, int MS, bool QW, int ROLE, class GA>
 __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int bx, const int by,
-                                                          const FfnSync& sy) {
+                                                          const FfnSync& sy, const LnMixArgs* lr = nullptr) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ uint32_t s_rexp[MT * 16];  // f16 relu^2 rows: bits of the row maximum if >= 2^15
   __shared__ float s_qlut[QW ? 16 : 1];  // QW: the NF4 code table
@@ -720,10 +732,12 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
   }
   int qf = 0;  // QW: this tile's weight format (0: 16-bit fragments)
   if constexpr (QW && MS != 2) qf = a.q_fmt;
+  int tile_mix = 0;  // (MS 2) the tile's mix plane
   if constexpr (MS == 2) {
     const uint32_t ti = a.tinfo[tile];
     if constexpr (QW) qf = (ti >> 31) ? a.q_fmt : 0;
     const int mix = ti & 7;
+    tile_mix = mix;
     Wm = a.tw + (int64_t)tile * 64 * a.K;
     Xhi += mix * a.x_mix_stride;
     Xlo += mix * a.x_mix_stride;
@@ -773,42 +787,39 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
   auto load_x = [&]() {
   if constexpr (XMODE == kXPlanes) {
     if constexpr (ROLE != 0) {  // handed-off planes: sc1 loads only
+      // rows past M: an offset past the buffer's range, which the load returns as zeros with no
+      // memory traffic (a one-row step reads 1/32 of the X bytes; no per-load branch: an
+      // exec-masked branch around each load cost the 32-row step 4 %, round 5)
       const auto rh = wt_rsrc(Xhi), rl = wt_rsrc(Xlo);
 #pragma unroll
       for (int u = 0; u < PERP; ++u) {
         const int c = threadIdx.x + u * 256;
         const int r = c / CH, k8 = (c % CH) * 8;
-        const int o = ((xrow0 + r) * ldx + kbeg + k8) * 2;
-        vh[u] = vl[u] = (short8){0, 0, 0, 0, 0, 0, 0, 0};
-        if (xrow0 + r < a.M) {
-          vh[u] = __builtin_bit_cast(short8, ld_sc1_b128(rh, o));
-          vl[u] = __builtin_bit_cast(short8, ld_sc1_b128(rl, o));
-        }
+        const int o = xrow0 + r < a.M ? ((xrow0 + r) * ldx + kbeg + k8) * 2 : (int)0x80000000u;
+        vh[u] = __builtin_bit_cast(short8, ld_sc1_b128(rh, o));
+        vl[u] = __builtin_bit_cast(short8, ld_sc1_b128(rl, o));
       }
     } else {
 #pragma unroll
     for (int u = 0; u < PERP; ++u) {
       const int c = threadIdx.x + u * 256;
       const int r = c / CH, k8 = (c % CH) * 8;
-      const int64_t o = (int64_t)(xrow0 + r) * ldx + kbeg + k8;
-      vh[u] = vl[u] = (short8){0, 0, 0, 0, 0, 0, 0, 0};
-      if (xrow0 + r < a.M) {
-        vh[u] = *(const short8*)(Xhi + o);
-        vl[u] = *(const short8*)(Xlo + o);
-      }
+      const int src = min(xrow0 + r, a.M - 1);
+      const int64_t o = (int64_t)src * ldx + kbeg + k8;
+      vh[u] = *(const short8*)(Xhi + o);
+      vl[u] = *(const short8*)(Xlo + o);
     }
     }
   } else {
-    if constexpr (ROLE != 0) {  // handed-off key slabs: sc1 loads only (x_row / x_col: the wave-tile map)
+    if constexpr (ROLE != 0) {  // handed-off key slabs: sc1 loads only (rows past M: zeros, as above)
 #pragma unroll
       for (int p = 0; p < NX; ++p) {
         const auto rp = wt_rsrc(a.x_part + p * a.x_part_stride);
 #pragma unroll
         for (int u = 0; u < PERR; ++u) {
           const int r = x_row(u), k4 = x_col(u);
-          xr[p][u] = (float4_){0.f, 0.f, 0.f, 0.f};
-          if (xrow0 + r < a.M)
-            xr[p][u] = __builtin_bit_cast(float4_, ld_sc1_b128(rp, ((xrow0 + r) * a.x_ld + kbeg + k4) * 4));
+          const int o = xrow0 + r < a.M ? ((xrow0 + r) * a.x_ld + kbeg + k4) * 4 : (int)0x80000000u;
+          xr[p][u] = __builtin_bit_cast(float4_, ld_sc1_b128(rp, o));
         }
       }
     } else {
@@ -818,9 +829,8 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
       for (int u = 0; u < PERR; ++u) {
         const int c = threadIdx.x + u * 256;
         const int r = c / (KS / 4), k4 = (c % (KS / 4)) * 4;
-        xr[p][u] = (float4_){0.f, 0.f, 0.f, 0.f};
-        if (xrow0 + r < a.M)
-          xr[p][u] = *(const float4_*)(a.x_part + p * a.x_part_stride + (int64_t)(xrow0 + r) * a.x_ld + kbeg + k4);
+        const int src = min(xrow0 + r, a.M - 1);
+        xr[p][u] = *(const float4_*)(a.x_part + p * a.x_part_stride + (int64_t)src * a.x_ld + kbeg + k4);
       }
     }
   }
@@ -874,6 +884,40 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
     for (int hh = h0; hh < h0 + (KS >> 6); ++hh) sync_wait(sy.cnt + kSyncStride * (kAttWkv + hh), sy.ln_rows, sy.err, 8, sy.opts);
     sync_stamp(sy, 1);
     load_x();
+  } else if constexpr (ROLE == 5 || ROLE == 6) {
+    static_assert(MT == 1 && XMODE == kXPlanes, "row-fused LayerNorm: one row, planes");
+    load_w();
+    // the row's LayerNorm (all 256 threads: thread t owns columns [4t, 4t + 4)), then this
+    // K-slice's mix split into row 0 of the X image (rows 1..15 are never stored)
+    constexpr int C = 1024, NPL = ROLE == 5 ? 16 : 8;
+    __shared__ float s_lnred[16];
+    const LnMixArgs& L = *lr;
+    const int c = 4 * (int)threadIdx.x;
+    const float* mup = L.mu[0];
+    if constexpr (ROLE == 5) {
+#pragma unroll
+      for (int m = 1; m < 6; ++m)
+        if (tile_mix == m) mup = L.mu[m];
+    }
+    const float4_ lw = ld4(L.ln_w + c), lb = ld4(L.ln_b + c), mu = ld4(mup + c);
+    float4_ v = ld4(L.h_in + c);
+    float4_ tp[NPL];
+#pragma unroll
+    for (int p = 0; p < NPL; ++p) tp[p] = ld4(L.part + p * L.part_stride + c);
+    const int4 info = L.rows[0];
+    const float4_ pv = ld4(L.shift + (((int64_t)info.w * L.S + info.x) * L.L + L.layer) * C + c);
+#pragma unroll
+    for (int p = 0; p < NPL; ++p) v += tp[p];
+    ln1024_apply(v, lw, lb, s_lnred, 0);
+    if (c >= kbeg && c < kbeg + KS) {
+      const float4_ x = v + (pv - v) * mu;
+      uint32_t h0, l0, h1, l1;
+      split2<F16>(x[0], x[1], h0, l0);
+      split2<F16>(x[2], x[3], h1, l1);
+      *(uint2*)(xh + (c - kbeg)) = make_uint2(h0, h1);
+      *(uint2*)(xl + (c - kbeg)) = make_uint2(l0, l1);
+    }
+    sync_stamp(sy, 1);
   } else if constexpr (ROLE == 2) {
     if (sy.opts & 1)  // weights after the LN rows
       sync_wait(sy.cnt + kSyncStride * (blockIdx.x & (kLnReplicas - 1)), sy.ln_rows, sy.err, 4, sy.opts);
@@ -887,9 +931,12 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
     load_w();
   }
   for (;;) {
-  // 3) X -> LDS (rows past M are zeros, never loaded: an MFMA output row depends on its own X row
-  // only, and those rows' outputs are not stored -- a one-row step reads 1/32 of the X bytes)
-  if constexpr (XMODE == kXPlanes) {
+  // 3) X -> LDS (rows past M: zeros in the persistent roles (never fetched), a copy of row M-1 in the
+  // plain launches; an MFMA output row depends on its own X row only, and those rows' outputs are not
+  // stored)
+  if constexpr (ROLE == 5 || ROLE == 6) {
+    // (staged by the row-fused LayerNorm above)
+  } else if constexpr (XMODE == kXPlanes) {
 #pragma unroll
     for (int u = 0; u < PERP; ++u) {
       const int c = threadIdx.x + u * 256;
@@ -1076,10 +1123,36 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
   }
   if constexpr (ROLE != 0) sync_stamp(sy, 2);
   if constexpr (ROLE == 1) sync_arrive(sy.cnt + kSyncStride * (kLnReplicas + tile / sy.key_group));
+  if constexpr (ROLE == 6) {  // K-slice counter (replica 0) and key-done (lane 1)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+      __hip_atomic_fetch_add((gint_t*)(sy.cnt + kSyncStride * (kLnReplicas + tile / sy.key_group)), 1,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 1)
+      __hip_atomic_fetch_add((gint_t*)(sy.cnt + kSyncStride * kFfnKeyDone), 1, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+  }
   if constexpr (ROLE == 3) {
     const int c0 = col_off + (tile - tstart) * 64;  // this tile's first output column
     if (c0 < 3 * sy.C) sync_arrive(sy.cnt + kSyncStride * (kAttHead + ((c0 % sy.C) >> 6)), 1, sy.drop);
     else sync_arrive(sy.cnt + kSyncStride * kAttLora, kLnReplicas);
+  }
+  if constexpr (ROLE == 5) {  // as ROLE 3, plus rkv-done (lane 8) for the shift writer
+    const int c0 = col_off + (tile - tstart) * 64;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (c0 < 3 * sy.C) {
+      if (threadIdx.x == 0)
+        __hip_atomic_fetch_add((gint_t*)(sy.cnt + kSyncStride * (kAttHead + ((c0 % sy.C) >> 6))), 1,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (threadIdx.x < kLnReplicas) {
+      __hip_atomic_fetch_add((gint_t*)(sy.cnt + kSyncStride * (kAttLora + threadIdx.x)), 1, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (threadIdx.x == 8)
+      __hip_atomic_fetch_add((gint_t*)(sy.cnt + kSyncStride * kAttRkvDone), 1, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -1107,22 +1180,37 @@ __global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
 // three-launch path's, bit for bit (same bodies, same orders). Block 0 zeroes the counters of
 // the previously launched layer (that launch has finished: stream order).
 // ------------------------------------------------------------------------------------
-template <bool F16>
-__global__ __launch_bounds__(256, 2) void k_ffn_persist(LnMixArgs ln, GemmArgs ka, GemmArgs va, FfnSync sy) {
+// FUSED (row-fused form, one decode row): no LayerNorm blocks; key workgroups compute the row's LN2
+// themselves (gemm2_body ROLE 6); the last workgroup (after the value ones) waits until every key
+// workgroup has staged (kFfnKeyDone) and stores the residual and the new token-shift row.
+// Workgroups per CU the persistent kernels' register budgets are sized for (2: 256 VGPRs, two waves
+// per SIMD; 3 caps a kernel at 168 VGPRs so that three workgroups are resident per CU).
+#ifndef RWKVTTS_FFN_WPC
+#define RWKVTTS_FFN_WPC 2
+#endif
+#ifndef RWKVTTS_ATT_WPC
+#define RWKVTTS_ATT_WPC 2
+#endif
+template <bool F16, bool FUSED>
+__global__ __launch_bounds__(256, RWKVTTS_FFN_WPC) void k_ffn_persist(LnMixArgs ln, GemmArgs ka, GemmArgs va, FfnSync sy) {
   int b = blockIdx.x;
   tl_begin(ln.tl);
   sync_stamp(sy, 0);
+  if (b == 0 && threadIdx.x < sy.n_prev) sy.cnt_prev[threadIdx.x * kSyncStride] = 0;
   if (b < sy.n_ln_blocks) {
-    if (b == 0 && threadIdx.x < sy.n_prev) sy.cnt_prev[threadIdx.x * kSyncStride] = 0;
     if (b < sy.ln_rows) {
       ln1024_body<F16, 1, 1, 8>(ln, b);
       sync_stamp(sy, 2);
       sync_arrive(sy.cnt, kLnReplicas);
     }
   } else if ((b -= sy.n_ln_blocks) < sy.n_key) {
-    gemm2_body<2, 8, kXPlanes, F16, 1, 0, false, 1>(ka, b, 0, sy);
-  } else {
-    gemm2_body<2, 8, kXRelu2, F16, 4, 0, false, 2>(va, b - sy.n_key, 0, sy);
+    if constexpr (FUSED) gemm2_body<1, 8, kXPlanes, F16, 1, 0, false, 6>(ka, b, 0, sy, &ln);
+    else gemm2_body<2, 8, kXPlanes, F16, 1, 0, false, 1>(ka, b, 0, sy);
+  } else if ((b -= sy.n_key) < sy.n_val || !FUSED) {
+    gemm2_body<2, 8, kXRelu2, F16, 4, 0, false, 2>(va, b, 0, sy);
+  } else if constexpr (FUSED) {  // the shift writer
+    sync_wait(sy.cnt + kSyncStride * kFfnKeyDone, sy.n_key, sy.err, 1024, sy.opts);
+    ln1024_body<F16, 1, 0, 8>(ln, 0);
   }
   sync_stamp(sy, 3);
   tl_end(ln.tl);
@@ -1542,23 +1630,36 @@ static bool prep_ffn_persist(const LnMixArgs& ln, const GemmArgs& key, const Gem
   sy.stamps = stamps;
   sy.opts = opts;
   prefetch_holds(sy);
-  sy.n_prev = kLnReplicas + kFfnSlices;
+  sy.n_prev = kLnReplicas + kFfnSlices + 1;  // (+ kFfnKeyDone)
   P.nv = vt * val.k_split;
+  sy.n_val = P.nv;
   return true;
 }
 
 bool launch_ffn_persist(const LnMixArgs& ln, const GemmArgs& key, const GemmArgs& val, int* cnt, int* cnt_prev,
-                        int* err, int R, hipStream_t st, uint64_t* stamps, int opts) {
+                        int* err, int R, hipStream_t st, uint64_t* stamps, int opts, bool fused_ln) {
   FfnPrep P;
   if (!prep_ffn_persist(ln, key, val, cnt, cnt_prev, err, R, stamps, opts, P)) return false;
+  const bool fused = fused_ln && R == 1 && ln.inplace;
+  int n_fix = 0;
+  if (fused) {
+    P.sy.n_ln_blocks = 0;
+    P.sy.d_k = 0;
+    n_fix = 1;
+  }
   LnMixArgs& l = P.l;
   GemmArgs& ka = P.ka;
   GemmArgs& va = P.va;
   FfnSync& sy = P.sy;
   const size_t lds = (size_t)2 * 16 * (8 * 32 + 8) * 2 * 2;
-  const dim3 grid(sy.n_ln_blocks + sy.n_key + P.nv);
-  if (key.f16) RT_LAUNCH((k_ffn_persist<true>), grid, dim3(256), lds, st, l, ka, va, sy);
-  else RT_LAUNCH((k_ffn_persist<false>), grid, dim3(256), lds, st, l, ka, va, sy);
+  const dim3 grid(sy.n_ln_blocks + sy.n_key + P.nv + n_fix);
+  if (key.f16) {
+    if (fused) RT_LAUNCH((k_ffn_persist<true, true>), grid, dim3(256), lds, st, l, ka, va, sy);
+    else RT_LAUNCH((k_ffn_persist<true, false>), grid, dim3(256), lds, st, l, ka, va, sy);
+  } else {
+    if (fused) RT_LAUNCH((k_ffn_persist<false, true>), grid, dim3(256), lds, st, l, ka, va, sy);
+    else RT_LAUNCH((k_ffn_persist<false, false>), grid, dim3(256), lds, st, l, ka, va, sy);
+  }
   return true;
 }
 
@@ -2481,13 +2582,16 @@ __global__ __launch_bounds__(256) void k_wkv6(WkvArgs a) {
 // Dependencies point to lower block indices only (see k_ffn_persist); outputs are the four
 // launches', bit for bit. Block 0 zeroes the previous layer's counters.
 // ------------------------------------------------------------------------------------
-template <bool F16, bool EMB>
-__global__ __launch_bounds__(256, 2) void k_att_persist(LnMixArgs ln, GemmArgs ga, WkvArgs wa, GemmArgs go, FfnSync sy) {
+// FUSED (row-fused form, one decode row, layers > 0): no LayerNorm blocks; rkv workgroups compute
+// the row's LN1 themselves (gemm2_body ROLE 5); the last workgroup waits until every rkv workgroup
+// has staged (kAttRkvDone) and stores the residual and the new token-shift row.
+template <bool F16, bool EMB, bool FUSED>
+__global__ __launch_bounds__(256, RWKVTTS_ATT_WPC) void k_att_persist(LnMixArgs ln, GemmArgs ga, WkvArgs wa, GemmArgs go, FfnSync sy) {
   int b = blockIdx.x;
   tl_begin(ln.tl);
   sync_stamp(sy, 0);
+  if (b == 0 && threadIdx.x < sy.n_prev) sy.cnt_prev[threadIdx.x * kSyncStride] = 0;
   if (b < sy.n_ln_blocks) {
-    if (b == 0 && threadIdx.x < sy.n_prev) sy.cnt_prev[threadIdx.x * kSyncStride] = 0;
     if (b < sy.ln_rows) {
       if constexpr (EMB) ln1024_body<F16, 1, 6, 0, true>(ln, b);
       else ln1024_body<F16, 1, 6, 16>(ln, b);
@@ -2495,11 +2599,15 @@ __global__ __launch_bounds__(256, 2) void k_att_persist(LnMixArgs ln, GemmArgs g
       sync_arrive(sy.cnt + kSyncStride * kAttLn, kLnReplicas);
     }
   } else if ((b -= sy.n_ln_blocks) < sy.n_key) {
-    gemm2_body<2, 8, kXPlanes, F16, 1, 2, false, 3>(ga, b % sy.rkv_tiles, b / sy.rkv_tiles, sy);
+    if constexpr (FUSED) gemm2_body<1, 8, kXPlanes, F16, 1, 2, false, 5>(ga, b % sy.rkv_tiles, b / sy.rkv_tiles, sy, &ln);
+    else gemm2_body<2, 8, kXPlanes, F16, 1, 2, false, 3>(ga, b % sy.rkv_tiles, b / sy.rkv_tiles, sy);
   } else if ((b -= sy.n_key) < sy.n_wkv) {
     wkv6_body<F16, 1>(wa, b, 0, sy);
-  } else {
-    gemm2_body<2, 4, kXPlanes, F16, 1, 0, false, 4>(go, b - sy.n_wkv, 0, sy);
+  } else if ((b -= sy.n_wkv) < 16 * go.k_split || !FUSED) {
+    gemm2_body<2, 4, kXPlanes, F16, 1, 0, false, 4>(go, b, 0, sy);
+  } else if constexpr (FUSED && !EMB) {  // the shift writer
+    sync_wait(sy.cnt + kSyncStride * kAttRkvDone, sy.n_key, sy.err, 2048, sy.opts);
+    ln1024_body<F16, 1, 0, 16>(ln, 0);
   }
   sync_stamp(sy, 3);
   tl_end(ln.tl);
@@ -2561,10 +2669,17 @@ static bool prep_att_persist(const LnMixArgs& ln, const GemmArgs& rkv, const Wkv
 
 bool launch_att_persist(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs& wkv, const GemmArgs& wo, int* cnt,
                         int* cnt_prev, int* err, int R, int H, hipStream_t st, uint64_t* stamps, int opts,
-                        int* drop) {
+                        int* drop, bool fused_ln) {
   AttPrep P;
   if (!prep_att_persist(ln, rkv, wkv, wo, cnt, cnt_prev, err, R, H, stamps, opts, P)) return false;
   P.sy.drop = drop;
+  const bool fused = fused_ln && R == 1 && ln.emb == nullptr && ln.inplace;
+  int n_fix = 0;  // the row-fused form's shift writer
+  if (fused) {
+    P.sy.n_ln_blocks = 0;
+    P.sy.d_w = 0;  // (the hold only kept the weight streams off the LayerNorm rows' loads)
+    n_fix = 1;
+  }
   const bool emb = ln.emb != nullptr;
   LnMixArgs& l = P.l;
   GemmArgs& ga = P.ga;
@@ -2573,13 +2688,15 @@ bool launch_att_persist(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs&
   FfnSync& sy = P.sy;
   const int n_wo = 16 * wo.k_split;
   const size_t lds = (size_t)2 * 16 * (8 * 32 + 8) * 2 * 2;  // the rkv body's X image (the largest)
-  const dim3 grid(sy.n_ln_blocks + sy.n_key + sy.n_wkv + n_wo);
+  const dim3 grid(sy.n_ln_blocks + sy.n_key + sy.n_wkv + n_wo + n_fix);
   if (ln.f16) {
-    if (emb) RT_LAUNCH((k_att_persist<true, true>), grid, dim3(256), lds, st, l, ga, wa, gw, sy);
-    else RT_LAUNCH((k_att_persist<true, false>), grid, dim3(256), lds, st, l, ga, wa, gw, sy);
+    if (emb) RT_LAUNCH((k_att_persist<true, true, false>), grid, dim3(256), lds, st, l, ga, wa, gw, sy);
+    else if (fused) RT_LAUNCH((k_att_persist<true, false, true>), grid, dim3(256), lds, st, l, ga, wa, gw, sy);
+    else RT_LAUNCH((k_att_persist<true, false, false>), grid, dim3(256), lds, st, l, ga, wa, gw, sy);
   } else {
-    if (emb) RT_LAUNCH((k_att_persist<false, true>), grid, dim3(256), lds, st, l, ga, wa, gw, sy);
-    else RT_LAUNCH((k_att_persist<false, false>), grid, dim3(256), lds, st, l, ga, wa, gw, sy);
+    if (emb) RT_LAUNCH((k_att_persist<false, true, false>), grid, dim3(256), lds, st, l, ga, wa, gw, sy);
+    else if (fused) RT_LAUNCH((k_att_persist<false, false, true>), grid, dim3(256), lds, st, l, ga, wa, gw, sy);
+    else RT_LAUNCH((k_att_persist<false, false, false>), grid, dim3(256), lds, st, l, ga, wa, gw, sy);
   }
   return true;
 }

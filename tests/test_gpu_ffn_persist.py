@@ -25,7 +25,9 @@ _M = {"RWKVTTS_PERSIST_MIN_ROWS": "1"}
 MODES = {"off": dict(_M, RWKVTTS_FFN_PERSIST="0", RWKVTTS_ATT_PERSIST="0"),
          "ffn": dict(_M, RWKVTTS_FFN_PERSIST="5", RWKVTTS_ATT_PERSIST="0"),
          "att": dict(_M, RWKVTTS_FFN_PERSIST="0", RWKVTTS_ATT_PERSIST="5"),
-         "both": dict(_M, RWKVTTS_FFN_PERSIST="5", RWKVTTS_ATT_PERSIST="5")}
+         "both": dict(_M, RWKVTTS_FFN_PERSIST="5", RWKVTTS_ATT_PERSIST="5"),
+         # one-row steps without the row-fused LayerNorm form (its LayerNorm rows as at R > 1)
+         "both_rows": dict(_M, RWKVTTS_FFN_PERSIST="5", RWKVTTS_ATT_PERSIST="5", RWKVTTS_FUSE_LN1="0")}
 
 
 class _env:
@@ -102,6 +104,21 @@ def test_persist_fewer_rows_and_eager(blob04):
     q, keep = to_struct(reqs[2])
     g, s, _ = om.generate(q)
     assert b[2] == (g, s)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+def test_persist_one_row_fused_layernorm_bitwise(dtype):
+    """One decode row (a lone request): the persistent halves run their row-fused form (no LayerNorm
+    workgroups: every rkv / key workgroup computes the row's LayerNorm itself, a trailing workgroup
+    stores the residual and the token-shift row). Bitwise the separate launches' and the LayerNorm-row
+    form's tokens and recurrent state, graph replay and eager."""
+    dt = rwkvtts._ffi.DTYPE_F16 if dtype == "f16" else rwkvtts._ffi.DTYPE_BF16
+    blob = W.synth_blob(W.DIMS_04B, seed=11, dtype=dt)
+    reqs = [make_request(synth_text(500), seed=5, fixed=40)]
+    for graphs in (True, False):
+        outs, _ = _both(blob, reqs, modes=("off", "both", "both_rows"), max_slots=4, token_chunk_size=512,
+                        use_graphs=graphs)
+        assert outs[1] == outs[0] and outs[2] == outs[0], graphs
 
 
 def test_persist_f16_bitwise():

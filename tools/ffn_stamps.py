@@ -39,6 +39,9 @@ nw = 16 * B  # WKV workgroups: one per (row, head)
 ae = 244 + nw + 128
 roles = ({"ln": (0, 32), "key": (32, 288), "value": (288, 544)} if which == "ffn" else
          {"ln": (0, 32), "rkv": (32, 244), "wkv": (244, 244 + nw), "wo": (244 + nw, ae)})
+if B == 1 and os.environ.get("RWKVTTS_FUSE_LN1", "1") != "0":  # the row-fused form (layer 5: no LN blocks)
+    roles = ({"key": (0, 256), "value": (256, 512), "shift": (512, 513)} if which == "ffn" else
+             {"rkv": (0, 212), "wkv": (212, 228), "wo": (228, 356), "shift": (356, 357)})
 nb = max(e for _, e in roles.values())
 t0 = a[:nb, 0][a[:nb, 0] > 0].min()
 names = ["start", "wait_done", "work_done", "end"]

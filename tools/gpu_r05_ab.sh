@@ -14,6 +14,7 @@ for r in 1 2; do for b in ${BS:-1 32}; do for V in $VARIANTS; do
   echo -n "B=$b $V: "; env $E RWKVTTS_LIB=$PWD/$L DB_B=$b timeout -k 10 120 python -u tools/decode_bench.py 256 1 | grep -oE "decode [0-9.]+ us/step.*tokens [0-9a-f]+" || exit 1
 done; done; done > $O/ab.txt 2>&1
 cat $O/ab.txt
+[ "${STAMP_BS:-}" = none ] && exit 0
 for w in att ffn; do for b in ${STAMP_BS:-1 32}; do
   env $STAMP_ENV timeout -k 10 120 python3 tools/ffn_stamps.py 32 $w $b > $O/stamps_b${b}_$w.txt 2>&1 || exit 1
 done; done
