@@ -161,8 +161,10 @@ int launch_ln_mix(const LnMixArgs& a, int n_out_rows, hipStream_t st);
 int launch_gemm(const GemmArgs& a, hipStream_t st);
 // The FFN half of a decode step (LN2 + mix, key GEMM, relu^2, value GEMM) as ONE persistent launch
 // with in-launch hand-offs (k_ffn_persist); false if the shapes are not covered.
-constexpr int kFfnKeyDone = 24;       // row-fused form: key workgroups done (the shift writer waits)
-constexpr int kFfnSyncInts = 25 * 64;  // counter block per layer: (8 LN replicas + 16 K-slices + 1) x 256 B
+constexpr int kFfnSyncInts = 24 * 64;  // counter block per layer: (8 LN replicas + 16 K-slices) x 256 B
+// row-fused form (no LayerNorm rows): key workgroups done (the shift writer waits), in LN replica 1's
+// counter. (A 25th counter staggered every later device allocation: 2 % slower decode at 32 rows.)
+constexpr int kFfnKeyDone = 1;
 // ---- persistent launches: hand-off counters and their arguments (lm_kernels.hip) ----------
 // Inter-workgroup hand-offs of the persistent FFN launch (k_ffn_persist): counters kSyncStride
 // ints (256 B) apart (see lm_kernels.hip for each launch's layout).
@@ -174,8 +176,8 @@ constexpr int kAttLn = 0;      // kLnReplicas: LayerNorm rows published
 constexpr int kAttHead = 8;    // 16: head h's r / k / v tiles published (3 tiles x the K-splits)
 constexpr int kAttLora = 24;   // kLnReplicas: the LoRA-down tiles published
 constexpr int kAttWkv = 32;    // 16: WKV workgroups of head h done (one per row)
-constexpr int kAttRkvDone = 48; // row-fused form: rkv workgroups done (the shift writer waits)
-constexpr int kAttCounters = 49;
+constexpr int kAttCounters = 48;
+constexpr int kAttRkvDone = kAttLn + 1;  // row-fused form (no LayerNorm rows): rkv workgroups done
 struct FfnSync {     // (both persistent launches)
   int* cnt;          // this layer's counters (zero at launch)
   int* cnt_prev;     // the counters of the layer launched before this one: zeroed by block 0

@@ -886,9 +886,10 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
     load_x();
   } else if constexpr (ROLE == 5 || ROLE == 6) {
     static_assert(MT == 1 && XMODE == kXPlanes, "row-fused LayerNorm: one row, planes");
-    load_w();
     // the row's LayerNorm (all 256 threads: thread t owns columns [4t, 4t + 4)), then this
-    // K-slice's mix split into row 0 of the X image (rows 1..15 are never stored)
+    // K-slice's mix split into row 0 of the X image (rows 1..15 are never stored). The LayerNorm
+    // inputs (L2 / MALL hits, written by the previous launch) are requested BEFORE the weight stream
+    // (HBM, behind the launch-start burst): loads return in order, so the sums wait for these alone.
     constexpr int C = 1024, NPL = ROLE == 5 ? 16 : 8;
     __shared__ float s_lnred[16];
     const LnMixArgs& L = *lr;
@@ -899,12 +900,15 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
       for (int m = 1; m < 6; ++m)
         if (tile_mix == m) mup = L.mu[m];
     }
-    const float4_ lw = ld4(L.ln_w + c), lb = ld4(L.ln_b + c), mu = ld4(mup + c);
     float4_ v = ld4(L.h_in + c);
     float4_ tp[NPL];
 #pragma unroll
     for (int p = 0; p < NPL; ++p) tp[p] = ld4(L.part + p * L.part_stride + c);
+    const float4_ lw = ld4(L.ln_w + c), lb = ld4(L.ln_b + c);
+    load_w();
+    // (after the weights: the token-shift row's address waits for the row descriptor)
     const int4 info = L.rows[0];
+    const float4_ mu = ld4(mup + c);
     const float4_ pv = ld4(L.shift + (((int64_t)info.w * L.S + info.x) * L.L + L.layer) * C + c);
 #pragma unroll
     for (int p = 0; p < NPL; ++p) v += tp[p];
@@ -1630,7 +1634,7 @@ static bool prep_ffn_persist(const LnMixArgs& ln, const GemmArgs& key, const Gem
   sy.stamps = stamps;
   sy.opts = opts;
   prefetch_holds(sy);
-  sy.n_prev = kLnReplicas + kFfnSlices + 1;  // (+ kFfnKeyDone)
+  sy.n_prev = kLnReplicas + kFfnSlices;
   P.nv = vt * val.k_split;
   sy.n_val = P.nv;
   return true;
@@ -1645,6 +1649,7 @@ bool launch_ffn_persist(const LnMixArgs& ln, const GemmArgs& key, const GemmArgs
   if (fused) {
     P.sy.n_ln_blocks = 0;
     P.sy.d_k = 0;
+    P.sy.opts &= ~1;  // (no LayerNorm rows for the value workgroups to wait for)
     n_fix = 1;
   }
   LnMixArgs& l = P.l;
