@@ -1200,8 +1200,11 @@ __global__ __launch_bounds__(256, RWKVTTS_FFN_WPC) void k_ffn_persist(LnMixArgs 
   int b = blockIdx.x;
   tl_begin(ln.tl);
   sync_stamp(sy, 0);
-  if (b == 0 && threadIdx.x < sy.n_prev) sy.cnt_prev[threadIdx.x * kSyncStride] = 0;
+  // (the previous layer's counters are zeroed inside a role branch -- LayerNorm block 0, or the
+  // row-fused form's shift writer: a test ahead of the branch made every workgroup wait for its
+  // kernel arguments first, 2 % of the 32-row decode step)
   if (b < sy.n_ln_blocks) {
+    if (b == 0 && threadIdx.x < sy.n_prev) sy.cnt_prev[threadIdx.x * kSyncStride] = 0;
     if (b < sy.ln_rows) {
       ln1024_body<F16, 1, 1, 8>(ln, b);
       sync_stamp(sy, 2);
@@ -1213,6 +1216,7 @@ __global__ __launch_bounds__(256, RWKVTTS_FFN_WPC) void k_ffn_persist(LnMixArgs 
   } else if ((b -= sy.n_key) < sy.n_val || !FUSED) {
     gemm2_body<2, 8, kXRelu2, F16, 4, 0, false, 2>(va, b, 0, sy);
   } else if constexpr (FUSED) {  // the shift writer
+    if (threadIdx.x < sy.n_prev) sy.cnt_prev[threadIdx.x * kSyncStride] = 0;
     sync_wait(sy.cnt + kSyncStride * kFfnKeyDone, sy.n_key, sy.err, 1024, sy.opts);
     ln1024_body<F16, 1, 0, 8>(ln, 0);
   }
@@ -2595,8 +2599,8 @@ __global__ __launch_bounds__(256, RWKVTTS_ATT_WPC) void k_att_persist(LnMixArgs 
   int b = blockIdx.x;
   tl_begin(ln.tl);
   sync_stamp(sy, 0);
-  if (b == 0 && threadIdx.x < sy.n_prev) sy.cnt_prev[threadIdx.x * kSyncStride] = 0;
-  if (b < sy.n_ln_blocks) {
+  if (b < sy.n_ln_blocks) {  // (zeroing: as in k_ffn_persist)
+    if (b == 0 && threadIdx.x < sy.n_prev) sy.cnt_prev[threadIdx.x * kSyncStride] = 0;
     if (b < sy.ln_rows) {
       if constexpr (EMB) ln1024_body<F16, 1, 6, 0, true>(ln, b);
       else ln1024_body<F16, 1, 6, 16>(ln, b);
@@ -2611,6 +2615,7 @@ __global__ __launch_bounds__(256, RWKVTTS_ATT_WPC) void k_att_persist(LnMixArgs 
   } else if ((b -= sy.n_wkv) < 16 * go.k_split || !FUSED) {
     gemm2_body<2, 4, kXPlanes, F16, 1, 0, false, 4>(go, b, 0, sy);
   } else if constexpr (FUSED && !EMB) {  // the shift writer
+    if (threadIdx.x < sy.n_prev) sy.cnt_prev[threadIdx.x * kSyncStride] = 0;
     sync_wait(sy.cnt + kSyncStride * kAttRkvDone, sy.n_key, sy.err, 2048, sy.opts);
     ln1024_body<F16, 1, 0, 16>(ln, 0);
   }
