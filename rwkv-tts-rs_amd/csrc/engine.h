@@ -173,6 +173,11 @@ class Engine {
   // one-row decode steps: the row-fused persistent form (each GEMM workgroup computes the row's
   // LayerNorm itself; lm_kernels.h launch_att_persist). RWKVTTS_FUSE_LN1=0 turns it off.
   bool fuse_ln1_ = true;
+  // one-row FFN form: the key -> value hand-off as data-tagged granules (FfnSync::gran; d_epoch_ is
+  // bumped by each pass's layer-0 attention launch). RWKVTTS_GRAN=0 turns it off.
+  bool gran_ = true;
+  uint64_t* d_gran_ = nullptr;
+  int* d_epoch_ = nullptr;
   int ffn_persist_ = 5;     // RWKVTTS_FFN_PERSIST: decode steps' FFN half as one launch (k_ffn_persist);
                             // 0 off, else 1 + 2 x launch options (5: long poll sleep, the measured best)
   int* ffn_sync_ = nullptr; // its hand-off counters: [L][kFfnSyncInts] (give-up code: d_ctrl_[S_])

@@ -165,6 +165,7 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
   if (const char* ap = getenv("RWKVTTS_ATT_PERSIST")) att_persist_ = atoi(ap);
   if (const char* pm = getenv("RWKVTTS_PERSIST_MIN_ROWS")) persist_min_rows_ = atoi(pm);
   if (const char* fl = getenv("RWKVTTS_FUSE_LN1")) fuse_ln1_ = atoi(fl) != 0;
+  if (const char* gr = getenv("RWKVTTS_GRAN")) gran_ = atoi(gr) != 0;
   if ((ffn_persist_ || att_persist_) && !claim_persistent(desc.device, this, &lock_fd_)) ffn_persist_ = att_persist_ = 0;
   if (const char* gp = getenv("RWKVTTS_GEMM_STAMPS")) {
     dbg_gstamp_path_ = gp;
@@ -370,6 +371,15 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
   RT_HIP(hipMemset(d_ctrl_ + S_, 0, sizeof(SlotCtrl)));
   RT_OK(alloc(&d_sem_, (size_t)S_ * RWKVTTS_SEMANTIC_LIMIT));
   RT_HIP(hipHostMalloc((void**)&h_ctrl_, sizeof(SlotCtrl) * 2 * (S_ + 1), hipHostMallocDefault));  // 2 snapshots
+  // granule hand-off of the one-row FFN form (FfnSync::gran): four key splits x F granules, and the
+  // pass counter that tags them (starts at 1: a zeroed granule never carries a live tag)
+  if (gran_) {
+    RT_OK(alloc(&d_gran_, (size_t)ffn_gran_count(4, dims.n_ffn)));
+    RT_OK(alloc(&d_epoch_, 64));
+    const int one = 1;
+    RT_HIP(hipMemcpy(d_epoch_, &one, sizeof(int), hipMemcpyHostToDevice));
+    sync_bufs_.push_back({(int*)d_gran_, (size_t)ffn_gran_count(4, dims.n_ffn) * sizeof(uint64_t)});
+  }
 
   RT_HIP(hipDeviceSynchronize());
   return RWKVTTS_OK;
@@ -552,6 +562,10 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
   bool use_att = att_persist_ && inplace && big && !dbg_exp_ && Lc >= 2 && !dbg_stamps_ && !dbg_gstamps_ &&
                  !any_quant && emb_fused;
   bool use_ffn = ffn_persist_ && inplace && big && !dbg_exp_ && Lc >= 2 && !dbg_gstamps_ && !any_quant;
+  // one-row passes: the FFN key -> value hand-off as granules, live once the layer-0 attention
+  // launch (which bumps the pass epoch) has been issued
+  const bool gran_pass = gran_ && d_gran_ && fuse_ln1_ && R == 1 && use_att && use_ffn;
+  bool gran_live = false;
   if (!emb_fused) {
     prof_begin(&ev);
     launch_embed(d_tok_, d_rows_, &d_ctrl_[0].next_token, (int)(sizeof(SlotCtrl) / 4), emb_,
@@ -704,9 +718,10 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
       att_persisted = launch_att_persist(m, g, k, go, att_sync_ + (size_t)l * kAttSyncInts,
                                          att_sync_ + (size_t)((l + Lc - 1) % Lc) * kAttSyncInts,
                                          (int*)(d_ctrl_ + S_), R, H_, stream_, l == 5 ? dbg_astamps2_ : nullptr,
-                                         att_persist_ >> 1, d_drop_, fuse_ln1_);
+                                         att_persist_ >> 1, d_drop_, fuse_ln1_, l == 0 && gran_pass ? d_epoch_ : nullptr);
       if (att_persisted) {
         prof_end("att_persist", ev);
+        if (l == 0 && gran_pass) gran_live = true;  // this pass's epoch is bumped
       } else {
         RT_CHECK(l == 0, RWKVTTS_EHIP, "persistent attention launch: a layer after layer 0 fell back");
         use_att = false;  // not covered: the separate launches for this whole forward
@@ -777,7 +792,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
       persisted = launch_ffn_persist(f, gk, gv, ffn_sync_ + (size_t)l * kFfnSyncInts,
                                      ffn_sync_ + (size_t)((l + Lc - 1) % Lc) * kFfnSyncInts,
                                      (int*)(d_ctrl_ + S_), R, stream_, l == 5 ? dbg_fstamps_ : nullptr,
-                                     ffn_persist_ >> 1, fuse_ln1_);
+                                     ffn_persist_ >> 1, fuse_ln1_, gran_live ? d_gran_ : nullptr, d_epoch_);
       if (persisted) {
         prof_end("ffn_persist", ev);
       } else {

@@ -209,6 +209,19 @@ struct FfnSync {     // (both persistent launches)
   // test hook (RWKVTTS_TEST_DROP_ARRIVE, null in production): the first rkv workgroup to find *drop
   // set clears it and skips its head arrival (a hand-off that never completes: the waits time out)
   int* drop;
+
+  // Data-tagged granule hand-off (row-fused FFN form, one decode row; null: partial slabs +
+  // counters). A key workgroup stores each output element of the row as ONE 8-byte {f32 bits, tag}
+  // granule (sc1 store) at gran[split * gran_ld + column]; a value workgroup polls the granules of
+  // its K-slice itself until every tag matches -- no store drain, no counter, no separate payload
+  // load behind a poll (MI355X_MICROARCH.md price list: handoff-1to1 vs handoff-flag).
+  // tag = *epoch * 64 + layer; *epoch is bumped once per forward pass by the layer-0 attention
+  // launch (epoch_bump) and by Engine::reset_persistent, so no granule of an earlier pass matches.
+  uint64_t* gran;
+  const int* epoch;
+  int gran_ld;
+  int layer;
+  int* epoch_bump;  // (attention launch of layer 0) one lane adds 1 to it
 };
 
 // The attention half of a decode step (LN1 + mixes, rkv + LoRA-down, WKV, Wo) as ONE persistent
@@ -221,10 +234,12 @@ constexpr int kAttSyncInts = kAttCounters * kSyncStride;  // counter block per l
 // kFfnKeyDone). Replaces the LayerNorm phase and its hand-off at batch 1.
 bool launch_att_persist(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs& wkv, const GemmArgs& wo, int* cnt,
                         int* cnt_prev, int* err, int R, int H, hipStream_t st, uint64_t* stamps, int opts,
-                        int* drop = nullptr, bool fused_ln = false);
+                        int* drop = nullptr, bool fused_ln = false, int* epoch_bump = nullptr);
 bool launch_ffn_persist(const LnMixArgs& ln, const GemmArgs& key, const GemmArgs& val, int* cnt, int* cnt_prev,
                         int* err, int R, hipStream_t st, uint64_t* stamps = nullptr, int opts = 0,
-                        bool fused_ln = false);
+                        bool fused_ln = false, uint64_t* gran = nullptr, const int* epoch = nullptr);
+// granules the row-fused FFN form's key -> value hand-off needs (FfnSync::gran)
+inline int64_t ffn_gran_count(int key_splits, int F) { return (int64_t)key_splits * F; }
 // Fills a.tw / a.tinfo / a.n_tinfo when the segments' packed weights are contiguous in 64-column
 // tiles and every segment's X is seg[0]'s planes plus a multiple of x_mix_stride; returns whether
 // the table applies (otherwise the kernel looks the segment up).

@@ -657,6 +657,18 @@ __device__ inline void sync_arrive(int* c, int replicas = 1, int* drop = nullptr
   if (threadIdx.x < replicas)
     __hip_atomic_fetch_add((gint_t*)(c + threadIdx.x * kSyncStride), inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// granule hand-off (FfnSync::gran): the tag of this pass and layer, one 8-byte {f32, tag} store
+typedef __attribute__((address_space(1))) uint64_t gu64_t;
+typedef uint64_t u64x2_ __attribute__((ext_vector_type(2)));
+__device__ inline uint32_t gran_tag(const FfnSync& sy) {
+  // (an sc1 vector load: the word changed in an earlier launch, a scalar-cache read can be stale)
+  const int ep = __hip_atomic_load((gint_t*)sy.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return (uint32_t)__builtin_amdgcn_readfirstlane(ep) * 64u + (uint32_t)sy.layer;
+}
+__device__ inline void gran_store(uint64_t* p, float v, uint32_t tag) {
+  __hip_atomic_store((gu64_t*)p, ((uint64_t)tag << 32) | __builtin_bit_cast(uint32_t, v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
 // hold a prefetch back until `ticks` (10 ns) after the launch's first s_memrealtime read here
 __device__ inline void hold_until(int ticks) {
   if (ticks <= 0) return;
@@ -922,6 +934,46 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
       *(uint2*)(xl + (c - kbeg)) = make_uint2(l0, l1);
     }
     sync_stamp(sy, 1);
+  } else if constexpr (ROLE == 7) {
+    // value workgroup of the granule form (one row): weights at dispatch, then wave 0 polls its
+    // K-slice's key granules for row 0 -- lane l: columns kbeg + 4l .. + 3 of the NX key splits,
+    // two 16-byte sc1 loads (4 granules) per split -- until every tag is this pass's; the row's
+    // x chunks go where load_x would have put them (rows past 0 stay zero)
+    static_assert(XMODE == kXRelu2 && NX == 4, "granule value role: the relu^2 X of four key splits");
+    hold_until(sy.d_v);
+    load_w();
+#pragma unroll
+    for (int p = 0; p < NX; ++p)
+#pragma unroll
+      for (int u = 0; u < PERR; ++u) xr[p][u] = (float4_){0.f, 0.f, 0.f, 0.f};
+    if (wave == 0) {
+      const uint32_t tag = gran_tag(sy);
+      const auto rs = wt_rsrc(sy.gran);
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      for (;;) {
+        bool ok = true;
+#pragma unroll
+        for (int p = 0; p < NX; ++p) {
+          // two granules per 16-byte load, taken apart as 64-bit halves {data | tag << 32}
+          // (element-wise extraction of the 32-bit vector was miscompiled here: data elements 0
+          // and 2 came out equal)
+          const u64x2_ q0 = __builtin_bit_cast(u64x2_, ld_sc1_b128(rs, (p * sy.gran_ld + kbeg + 4 * lane) * 8));
+          const u64x2_ q1 = __builtin_bit_cast(u64x2_, ld_sc1_b128(rs, (p * sy.gran_ld + kbeg + 4 * lane + 2) * 8));
+          xr[p][0] = (float4_){__builtin_bit_cast(float, (uint32_t)q0.x), __builtin_bit_cast(float, (uint32_t)q0.y),
+                               __builtin_bit_cast(float, (uint32_t)q1.x), __builtin_bit_cast(float, (uint32_t)q1.y)};
+          ok = ok && (uint32_t)(q0.x >> 32) == tag && (uint32_t)(q0.y >> 32) == tag &&
+               (uint32_t)(q1.x >> 32) == tag && (uint32_t)(q1.y >> 32) == tag;
+        }
+        if (__all(ok)) break;
+        __builtin_amdgcn_s_sleep(1);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 5000000ull) {
+          if (lane == 0) __hip_atomic_fetch_or((gint_t*)sy.err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    sync_stamp(sy, 1);
   } else if constexpr (ROLE == 2) {
     if (sy.opts & 1)  // weights after the LN rows
       sync_wait(sy.cnt + kSyncStride * (blockIdx.x & (kLnReplicas - 1)), sy.ln_rows, sy.err, 4, sy.opts);
@@ -953,9 +1005,12 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
     // of this K-slice is staged as relu^2 * 2^-e_r (e_r >= 0 the smallest power of two that
     // brings the row's maximum under 2^15) and its partial product is scaled back by 2^e_r in
     // the epilogue. Powers of two are exact, so rows in range (e_r = 0) are bit-unchanged.
+    // (ROLE 7, one row: only row 0 is staged -- rows past M hold stale bytes, which no stored
+    // output reads: an MFMA output row depends on its own X row only)
     float4_ y4[PERR];
 #pragma unroll
     for (int u = 0; u < PERR; ++u) {
+      if (ROLE == 7 && xrow0 + x_row(u) >= a.M) continue;
       float4_ x = xr[0][u];
 #pragma unroll
       for (int p = 1; p < NX; ++p) x += xr[p][u];
@@ -968,6 +1023,7 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
 #pragma unroll
       for (int u = 0; u < PERR; ++u) {
         const int r = x_row(u);
+        if (ROLE == 7 && xrow0 + r >= a.M) continue;
         const float m = fmaxf(fmaxf(y4[u][0], y4[u][1]), fmaxf(y4[u][2], y4[u][3]));
         if (m >= 32768.f) atomicMax(&s_rexp[r], as_u32(m));  // non-negative floats order as uints
       }
@@ -976,6 +1032,7 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
 #pragma unroll
     for (int u = 0; u < PERR; ++u) {
       const int r = x_row(u), k4 = x_col(u);
+      if (ROLE == 7 && xrow0 + r >= a.M) continue;
       float y[4] = {y4[u][0], y4[u][1], y4[u][2], y4[u][3]};
       if constexpr (F16) {
         const uint32_t mb = s_rexp[r];
@@ -1085,7 +1142,11 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
     }
     return v;
   };
-  if (a.wt) {
+  if (ROLE == 6 && sy.gran) {
+    // granule form: row 0's 64 columns, one {f32, tag} granule per element (lanes 0..15 of each
+    // wave hold row 0: g == 0, j == 0)
+    if (g == 0 && col < Nn) gran_store(sy.gran + (int64_t)split * sy.gran_ld + col_off + col, result(0, 0), gran_tag(sy));
+  } else if (a.wt) {
     // write-through: the tile is staged in LDS so every lane stores whole 16-byte pieces (a
     // 4-byte sc1 store is one fabric write each)
     constexpr int LDT = 68;
@@ -1127,10 +1188,10 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
   }
   if constexpr (ROLE != 0) sync_stamp(sy, 2);
   if constexpr (ROLE == 1) sync_arrive(sy.cnt + kSyncStride * (kLnReplicas + tile / sy.key_group));
-  if constexpr (ROLE == 6) {  // K-slice counter (replica 0) and key-done (lane 1)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (ROLE == 6) {  // K-slice counter (replica 0; not in the granule form) and key-done (lane 1)
+    if (!sy.gran) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0)
+    if (threadIdx.x == 0 && !sy.gran)
       __hip_atomic_fetch_add((gint_t*)(sy.cnt + kSyncStride * (kLnReplicas + tile / sy.key_group)), 1,
                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (threadIdx.x == 1)
@@ -1214,7 +1275,12 @@ __global__ __launch_bounds__(256, RWKVTTS_FFN_WPC) void k_ffn_persist(LnMixArgs 
     if constexpr (FUSED) gemm2_body<1, 8, kXPlanes, F16, 1, 0, false, 6>(ka, b, 0, sy, &ln);
     else gemm2_body<2, 8, kXPlanes, F16, 1, 0, false, 1>(ka, b, 0, sy);
   } else if ((b -= sy.n_key) < sy.n_val || !FUSED) {
-    gemm2_body<2, 8, kXRelu2, F16, 4, 0, false, 2>(va, b, 0, sy);
+    if constexpr (FUSED) {
+      if (sy.gran) gemm2_body<1, 8, kXRelu2, F16, 4, 0, false, 7>(va, b, 0, sy);  // (one row: 16-row tile)
+      else gemm2_body<2, 8, kXRelu2, F16, 4, 0, false, 2>(va, b, 0, sy);
+    } else {
+      gemm2_body<2, 8, kXRelu2, F16, 4, 0, false, 2>(va, b, 0, sy);
+    }
   } else if constexpr (FUSED) {  // the shift writer
     if (threadIdx.x < sy.n_prev) sy.cnt_prev[threadIdx.x * kSyncStride] = 0;
     sync_wait(sy.cnt + kSyncStride * kFfnKeyDone, sy.n_key, sy.err, 1024, sy.opts);
@@ -1645,7 +1711,8 @@ static bool prep_ffn_persist(const LnMixArgs& ln, const GemmArgs& key, const Gem
 }
 
 bool launch_ffn_persist(const LnMixArgs& ln, const GemmArgs& key, const GemmArgs& val, int* cnt, int* cnt_prev,
-                        int* err, int R, hipStream_t st, uint64_t* stamps, int opts, bool fused_ln) {
+                        int* err, int R, hipStream_t st, uint64_t* stamps, int opts, bool fused_ln, uint64_t* gran,
+                        const int* epoch) {
   FfnPrep P;
   if (!prep_ffn_persist(ln, key, val, cnt, cnt_prev, err, R, stamps, opts, P)) return false;
   const bool fused = fused_ln && R == 1 && ln.inplace;
@@ -1655,6 +1722,13 @@ bool launch_ffn_persist(const LnMixArgs& ln, const GemmArgs& key, const GemmArgs
     P.sy.d_k = 0;
     P.sy.opts &= ~1;  // (no LayerNorm rows for the value workgroups to wait for)
     n_fix = 1;
+    // the granule key -> value hand-off: four key splits (the value role's NX), one segment
+    if (gran && epoch && key.k_split == 4 && key.nseg == 1 && ln.layer < 64) {
+      P.sy.gran = gran;
+      P.sy.epoch = epoch;
+      P.sy.gran_ld = key.seg[0].N;
+      P.sy.layer = ln.layer;
+    }
   }
   LnMixArgs& l = P.l;
   GemmArgs& ka = P.ka;
@@ -2601,6 +2675,8 @@ __global__ __launch_bounds__(256, RWKVTTS_ATT_WPC) void k_att_persist(LnMixArgs 
   sync_stamp(sy, 0);
   if (b < sy.n_ln_blocks) {  // (zeroing: as in k_ffn_persist)
     if (b == 0 && threadIdx.x < sy.n_prev) sy.cnt_prev[threadIdx.x * kSyncStride] = 0;
+    if (b == 0 && threadIdx.x == 64 && sy.epoch_bump)  // a new pass for the granule hand-offs
+      __hip_atomic_fetch_add((gint_t*)sy.epoch_bump, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (b < sy.ln_rows) {
       if constexpr (EMB) ln1024_body<F16, 1, 6, 0, true>(ln, b);
       else ln1024_body<F16, 1, 6, 16>(ln, b);
@@ -2616,6 +2692,8 @@ __global__ __launch_bounds__(256, RWKVTTS_ATT_WPC) void k_att_persist(LnMixArgs 
     gemm2_body<2, 4, kXPlanes, F16, 1, 0, false, 4>(go, b, 0, sy);
   } else if constexpr (FUSED && !EMB) {  // the shift writer
     if (threadIdx.x < sy.n_prev) sy.cnt_prev[threadIdx.x * kSyncStride] = 0;
+    if (threadIdx.x == 64 && sy.epoch_bump)
+      __hip_atomic_fetch_add((gint_t*)sy.epoch_bump, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     sync_wait(sy.cnt + kSyncStride * kAttRkvDone, sy.n_key, sy.err, 2048, sy.opts);
     ln1024_body<F16, 1, 0, 16>(ln, 0);
   }
@@ -2679,10 +2757,11 @@ static bool prep_att_persist(const LnMixArgs& ln, const GemmArgs& rkv, const Wkv
 
 bool launch_att_persist(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs& wkv, const GemmArgs& wo, int* cnt,
                         int* cnt_prev, int* err, int R, int H, hipStream_t st, uint64_t* stamps, int opts,
-                        int* drop, bool fused_ln) {
+                        int* drop, bool fused_ln, int* epoch_bump) {
   AttPrep P;
   if (!prep_att_persist(ln, rkv, wkv, wo, cnt, cnt_prev, err, R, H, stamps, opts, P)) return false;
   P.sy.drop = drop;
+  P.sy.epoch_bump = epoch_bump;
   const bool fused = fused_ln && R == 1 && ln.emb == nullptr && ln.inplace;
   int n_fix = 0;  // the row-fused form's shift writer
   if (fused) {

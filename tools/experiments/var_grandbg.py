@@ -1,0 +1,53 @@
+# debug variant: the key role stores its row both as granules and as the partial slab (with the
+# counters); the granule value role also waits for the slabs and compares: a mismatching element
+# ORs 4096 into the give-up word (its index into err[1]) and the slab value is used
+s = open("lm_kernels.hip").read()
+a = """  if (ROLE == 6 && sy.gran) {
+    // granule form: row 0's 64 columns, one {f32, tag} granule per element (lanes 0..15 of each
+    // wave hold row 0: g == 0, j == 0)
+    if (g == 0 && col < Nn) gran_store(sy.gran + (int64_t)split * sy.gran_ld + col_off + col, result(0, 0), gran_tag(sy));
+  } else if (a.wt) {"""
+b = """  if (ROLE == 6 && sy.gran) {
+    if (g == 0 && col < Nn) gran_store(sy.gran + (int64_t)split * sy.gran_ld + col_off + col, result(0, 0), gran_tag(sy));
+  }
+  if (a.wt) {"""
+assert a in s; s = s.replace(a, b)
+a = """    if (!sy.gran) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0 && !sy.gran)"""
+b = """    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)"""
+assert a in s; s = s.replace(a, b)
+a = """#pragma unroll
+      for (int p = 0; p < NX; ++p)
+        xr[p][0] = (float4_){__builtin_bit_cast(float, q[p][0][0]), __builtin_bit_cast(float, q[p][0][2]),
+                             __builtin_bit_cast(float, q[p][1][0]), __builtin_bit_cast(float, q[p][1][2])};
+    }
+    __syncthreads();"""
+b = """#pragma unroll
+      for (int p = 0; p < NX; ++p)
+        xr[p][0] = (float4_){__builtin_bit_cast(float, q[p][0][0]), __builtin_bit_cast(float, q[p][0][2]),
+                             __builtin_bit_cast(float, q[p][1][0]), __builtin_bit_cast(float, q[p][1][2])};
+    }
+    float4_ g0[NX];
+#pragma unroll
+    for (int p = 0; p < NX; ++p) g0[p] = xr[p][0];
+    sync_wait(sy.cnt + kSyncStride * (kLnReplicas + split), sy.key_per_slice, sy.err, 2, sy.opts);
+    load_x();
+    if (wave == 0) {
+#pragma unroll
+      for (int p = 0; p < NX; ++p)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (__builtin_bit_cast(uint32_t, g0[p][e]) != __builtin_bit_cast(uint32_t, xr[p][0][e])) {
+            const int n = __hip_atomic_fetch_add((gint_t*)(sy.err + 1), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (n < 12)
+              printf("GRANDBG layer %d plane %d col %d gran %08x slab %08x tag %u q1 %u\\n", sy.layer, p,
+                     kbeg + 4 * lane + e, __builtin_bit_cast(uint32_t, g0[p][e]),
+                     __builtin_bit_cast(uint32_t, xr[p][0][e]), gran_tag(sy), 0u);
+          }
+    }
+    __syncthreads();"""
+assert a in s; s = s.replace(a, b)
+open("lm_kernels.hip", "w").write(s)

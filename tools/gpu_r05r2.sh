@@ -1,0 +1,7 @@
+set -o pipefail
+O=gpurun_out/r05r2
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_gpu_ffn_persist.py -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1; tail -3 $O/tests.log
+grep -q " passed" $O/tests.log && ! grep -q -E "FAILED|ERROR" $O/tests.log || exit 1
+T=rwkv-tts-rs_amd/rwkvtts/librwkvtts.so
+TAG=r05r2 BS="1" VARIANTS="ab_libs/head4/librwkvtts.so ab_libs/gran1/librwkvtts.so $T" STAMP_BS=1 bash tools/gpu_r05_ab.sh
