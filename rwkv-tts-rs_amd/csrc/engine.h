@@ -177,6 +177,7 @@ class Engine {
   // bumped by each pass's layer-0 attention launch). RWKVTTS_GRAN=0 turns it off.
   bool gran_ = true;
   uint64_t* d_gran_ = nullptr;
+  uint64_t* d_gran_att_ = nullptr;  // the attention form's (rkv -> WKV, WKV -> Wo)
   int* d_epoch_ = nullptr;
   int ffn_persist_ = 5;     // RWKVTTS_FFN_PERSIST: decode steps' FFN half as one launch (k_ffn_persist);
                             // 0 off, else 1 + 2 x launch options (5: long poll sleep, the measured best)

@@ -379,6 +379,9 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
     const int one = 1;
     RT_HIP(hipMemcpy(d_epoch_, &one, sizeof(int), hipMemcpyHostToDevice));
     sync_bufs_.push_back({(int*)d_gran_, (size_t)ffn_gran_count(4, dims.n_ffn) * sizeof(uint64_t)});
+    const int64_t ng = att_gran_count(4, ldA_, (int)dims.n_embd);
+    RT_OK(alloc(&d_gran_att_, (size_t)ng));
+    sync_bufs_.push_back({(int*)d_gran_att_, (size_t)ng * sizeof(uint64_t)});
   }
 
   RT_HIP(hipDeviceSynchronize());
@@ -718,7 +721,8 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
       att_persisted = launch_att_persist(m, g, k, go, att_sync_ + (size_t)l * kAttSyncInts,
                                          att_sync_ + (size_t)((l + Lc - 1) % Lc) * kAttSyncInts,
                                          (int*)(d_ctrl_ + S_), R, H_, stream_, l == 5 ? dbg_astamps2_ : nullptr,
-                                         att_persist_ >> 1, d_drop_, fuse_ln1_, l == 0 && gran_pass ? d_epoch_ : nullptr);
+                                         att_persist_ >> 1, d_drop_, fuse_ln1_, l == 0 && gran_pass ? d_epoch_ : nullptr,
+                                         gran_live ? d_gran_att_ : nullptr, d_epoch_);
       if (att_persisted) {
         prof_end("att_persist", ev);
         if (l == 0 && gran_pass) gran_live = true;  // this pass's epoch is bumped

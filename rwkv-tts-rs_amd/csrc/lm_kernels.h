@@ -221,6 +221,9 @@ struct FfnSync {     // (both persistent launches)
   const int* epoch;
   int gran_ld;
   int layer;
+  // attention (one row): rkv -> WKV granules at gran[split * gran_ld + column] (gran_ld = the rkv
+  // output width), WKV -> Wo granules at zgran[channel] (the z split hi | lo << 16)
+  uint64_t* zgran;
   int* epoch_bump;  // (attention launch of layer 0) one lane adds 1 to it
 };
 
@@ -234,7 +237,10 @@ constexpr int kAttSyncInts = kAttCounters * kSyncStride;  // counter block per l
 // kFfnKeyDone). Replaces the LayerNorm phase and its hand-off at batch 1.
 bool launch_att_persist(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs& wkv, const GemmArgs& wo, int* cnt,
                         int* cnt_prev, int* err, int R, int H, hipStream_t st, uint64_t* stamps, int opts,
-                        int* drop = nullptr, bool fused_ln = false, int* epoch_bump = nullptr);
+                        int* drop = nullptr, bool fused_ln = false, int* epoch_bump = nullptr,
+                        uint64_t* gran = nullptr, const int* epoch = nullptr);
+// granules of the one-row attention form's rkv -> WKV and WKV -> Wo hand-offs
+inline int64_t att_gran_count(int rkv_splits, int ldp, int C) { return (int64_t)rkv_splits * ldp + C; }
 bool launch_ffn_persist(const LnMixArgs& ln, const GemmArgs& key, const GemmArgs& val, int* cnt, int* cnt_prev,
                         int* err, int R, hipStream_t st, uint64_t* stamps = nullptr, int opts = 0,
                         bool fused_ln = false, uint64_t* gran = nullptr, const int* epoch = nullptr);

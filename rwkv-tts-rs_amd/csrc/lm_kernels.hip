@@ -665,9 +665,11 @@ __device__ inline uint32_t gran_tag(const FfnSync& sy) {
   const int ep = __hip_atomic_load((gint_t*)sy.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return (uint32_t)__builtin_amdgcn_readfirstlane(ep) * 64u + (uint32_t)sy.layer;
 }
+__device__ inline void gran_store_bits(uint64_t* p, uint32_t bits, uint32_t tag) {
+  __hip_atomic_store((gu64_t*)p, ((uint64_t)tag << 32) | bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 __device__ inline void gran_store(uint64_t* p, float v, uint32_t tag) {
-  __hip_atomic_store((gu64_t*)p, ((uint64_t)tag << 32) | __builtin_bit_cast(uint32_t, v), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
+  gran_store_bits(p, __builtin_bit_cast(uint32_t, v), tag);
 }
 // hold a prefetch back until `ticks` (10 ns) after the launch's first s_memrealtime read here
 __device__ inline void hold_until(int ticks) {
@@ -896,6 +898,34 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
     for (int hh = h0; hh < h0 + (KS >> 6); ++hh) sync_wait(sy.cnt + kSyncStride * (kAttWkv + hh), sy.ln_rows, sy.err, 8, sy.opts);
     sync_stamp(sy, 1);
     load_x();
+  } else if constexpr (ROLE == 8) {
+    // Wo workgroup of the granule form (one row): weights at dispatch, then wave 0 polls the z
+    // granules of its K-slice (row 0; each granule = the WKV's bf16 / f16 hi | lo << 16 split of one
+    // channel, so no re-split) and writes them as row 0 of the X image; rows past 0 are not staged
+    static_assert(MT == 1 && XMODE == kXPlanes && KS == 128, "granule Wo role: one row, a 128-channel K-slice");
+    hold_until(sy.d_late);
+    load_w();
+    if (threadIdx.x < 64) {
+      const uint32_t tag = gran_tag(sy);
+      const auto rs = wt_rsrc(sy.zgran);
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      u64x2_ q;
+      for (;;) {
+        q = __builtin_bit_cast(u64x2_, ld_sc1_b128(rs, (kbeg + 2 * lane) * 8));
+        const bool ok = (uint32_t)(q.x >> 32) == tag && (uint32_t)(q.y >> 32) == tag;
+        if (__all(ok)) break;
+        __builtin_amdgcn_s_sleep(1);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 5000000ull) {
+          if (lane == 0) __hip_atomic_fetch_or((gint_t*)sy.err, 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+      const uint32_t g0 = (uint32_t)q.x, g1 = (uint32_t)q.y;  // {hi | lo << 16} of channels 2l, 2l + 1
+      *(uint32_t*)(xh + 2 * lane) = (g0 & 0xFFFFu) | (g1 << 16);
+      *(uint32_t*)(xl + 2 * lane) = (g0 >> 16) | (g1 & 0xFFFF0000u);
+    }
+    __syncthreads();
+    sync_stamp(sy, 1);
   } else if constexpr (ROLE == 5 || ROLE == 6) {
     static_assert(MT == 1 && XMODE == kXPlanes, "row-fused LayerNorm: one row, planes");
     // the row's LayerNorm (all 256 threads: thread t owns columns [4t, 4t + 4)), then this
@@ -990,8 +1020,8 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
   // 3) X -> LDS (rows past M: zeros in the persistent roles (never fetched), a copy of row M-1 in the
   // plain launches; an MFMA output row depends on its own X row only, and those rows' outputs are not
   // stored)
-  if constexpr (ROLE == 5 || ROLE == 6) {
-    // (staged by the row-fused LayerNorm above)
+  if constexpr (ROLE == 5 || ROLE == 6 || ROLE == 8) {
+    // (staged by the row-fused LayerNorm / the granule sweep above)
   } else if constexpr (XMODE == kXPlanes) {
 #pragma unroll
     for (int u = 0; u < PERP; ++u) {
@@ -2413,7 +2443,7 @@ __device__ __attribute__((always_inline)) void wkv6_body(const WkvArgs& a, const
   float rp[NP], kp[NP], vp[NP], vf = 0.f;
   auto load_parts = [&](int row) {
     const float* prow = a.part + (int64_t)row * a.ldp;
-    if constexpr (ROLE == 1) {  // handed-off partial slabs: sc1 loads only
+    if constexpr (ROLE >= 1) {  // handed-off partial slabs: sc1 loads only
 #pragma unroll
       for (int p = 0; p < NP; ++p) {
         const auto rs = wt_rsrc(prow + p * a.part_stride);
@@ -2432,7 +2462,7 @@ __device__ __attribute__((always_inline)) void wkv6_body(const WkvArgs& a, const
       vp[p] = pp[2 * C + c];
     }
     }
-    if constexpr (ROLE == 1)
+    if constexpr (ROLE >= 1)
       vf = a.layer > 0 ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
                                                      wt_rsrc(a.v_first + (int64_t)row * a.ldv), c * 4, 0, 16))
                        : 0.f;
@@ -2444,7 +2474,7 @@ __device__ __attribute__((always_inline)) void wkv6_body(const WkvArgs& a, const
   uint4 lw[9];  // 8 bf16 per entry: w 0..1 | a 2..3 | v 4 | g 5..8
   const uint4* pl = (const uint4*)(a.lup + (int64_t)h * 9 * 256 * 8);
   int slot, r_begin, n_rows;
-  if constexpr (ROLE == 1) {
+  if constexpr (ROLE >= 1) {
     // LoRA-up rows and the state first (they do not depend on this layer's rkv workgroups), then
     // wait for the head's r / k / v tiles and the LoRA-down tiles, then their partials
     slot = sg.x; r_begin = sg.y; n_rows = sg.z;
@@ -2529,7 +2559,7 @@ __device__ __attribute__((always_inline)) void wkv6_body(const WkvArgs& a, const
     k = k * (1.0f + (av - 1.0f) * kac);
     if (a.layer == 0) {
       if (qq == 0) {
-        if constexpr (ROLE == 1) store_wt(wt_rsrc(a.v_first + (int64_t)row * a.ldv), c * 4, v);
+        if constexpr (ROLE >= 1) store_wt(wt_rsrc(a.v_first + (int64_t)row * a.ldv), c * 4, v);
         else a.v_first[(int64_t)row * a.ldv + c] = v;
       }
     } else {
@@ -2598,7 +2628,17 @@ __device__ __attribute__((always_inline)) void wkv6_body(const WkvArgs& a, const
     const float mean = ((s_red[2][0] + s_red[2][1]) + (s_red[2][2] + s_red[2][3])) * (1.0f / N);
     const float var =
         fmaxf(((s_red[3][0] + s_red[3][1]) + (s_red[3][2] + s_red[3][3])) * (1.0f / N) - mean * mean, 0.f);
-    if constexpr (ROLE == 1) {
+    if constexpr (ROLE == 2) {
+      // granule form: the channel's split as ONE granule {hi | lo << 16, tag} (same expression
+      // and threads as below, so the same bits) -- the Wo workgroups poll these directly
+      if (qq == 0) {
+        const float gn = (y - mean) * __builtin_amdgcn_rsqf(var + 64e-5f) * lnw + lnb;
+        const float zx = (gn + bonus * v) * lo3;
+        const uint16_t hb = f32_to_w16(zx, F16);
+        const uint16_t lb = f32_to_w16(zx - w16_to_f32(hb, F16), F16);
+        gran_store_bits(sy.zgran + c, (uint32_t)hb | ((uint32_t)lb << 16), gran_tag(sy));
+      }
+    } else if constexpr (ROLE == 1) {
       // the row's 64 z values split by the same threads and expression as split_store (the
       // compiler fuses the product into the 16-bit conversion, so the split must stay here to
       // keep the bits), the planes through LDS; wave 0's lanes 0..15 store 4 channels each as one
@@ -2626,9 +2666,9 @@ __device__ __attribute__((always_inline)) void wkv6_body(const WkvArgs& a, const
     if (rr + 1 < n_rows) __syncthreads();
   }
   if (stp) { stp[6] = __builtin_amdgcn_s_memtime(); stp[7] = __builtin_amdgcn_s_memrealtime(); }
-  if constexpr (ROLE == 1) {
+  if constexpr (ROLE >= 1) {
     sync_stamp(sy, 2);
-    sync_arrive(sy.cnt + kSyncStride * (kAttWkv + h));
+    if constexpr (ROLE == 1) sync_arrive(sy.cnt + kSyncStride * (kAttWkv + h));
     // the final state (read by the next step's launch only) goes out after the hand-off, so its
     // write-through drain is not on the Wo workgroups' path
     const auto rs = wt_rsrc(a.state + (int64_t)slot * a.slot_stride + a.layer_off + (int64_t)h * N * N);
@@ -2687,9 +2727,19 @@ __global__ __launch_bounds__(256, RWKVTTS_ATT_WPC) void k_att_persist(LnMixArgs 
     if constexpr (FUSED) gemm2_body<1, 8, kXPlanes, F16, 1, 2, false, 5>(ga, b % sy.rkv_tiles, b / sy.rkv_tiles, sy, &ln);
     else gemm2_body<2, 8, kXPlanes, F16, 1, 2, false, 3>(ga, b % sy.rkv_tiles, b / sy.rkv_tiles, sy);
   } else if ((b -= sy.n_key) < sy.n_wkv) {
-    wkv6_body<F16, 1>(wa, b, 0, sy);
+    if constexpr (FUSED && !EMB) {
+      if (sy.gran) wkv6_body<F16, 2>(wa, b, 0, sy);
+      else wkv6_body<F16, 1>(wa, b, 0, sy);
+    } else {
+      wkv6_body<F16, 1>(wa, b, 0, sy);
+    }
   } else if ((b -= sy.n_wkv) < 16 * go.k_split || !FUSED) {
-    gemm2_body<2, 4, kXPlanes, F16, 1, 0, false, 4>(go, b, 0, sy);
+    if constexpr (FUSED && !EMB) {
+      if (sy.gran) gemm2_body<1, 4, kXPlanes, F16, 1, 0, false, 8>(go, b, 0, sy);
+      else gemm2_body<2, 4, kXPlanes, F16, 1, 0, false, 4>(go, b, 0, sy);
+    } else {
+      gemm2_body<2, 4, kXPlanes, F16, 1, 0, false, 4>(go, b, 0, sy);
+    }
   } else if constexpr (FUSED && !EMB) {  // the shift writer
     if (threadIdx.x < sy.n_prev) sy.cnt_prev[threadIdx.x * kSyncStride] = 0;
     if (threadIdx.x == 64 && sy.epoch_bump)
@@ -2757,7 +2807,7 @@ static bool prep_att_persist(const LnMixArgs& ln, const GemmArgs& rkv, const Wkv
 
 bool launch_att_persist(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs& wkv, const GemmArgs& wo, int* cnt,
                         int* cnt_prev, int* err, int R, int H, hipStream_t st, uint64_t* stamps, int opts,
-                        int* drop, bool fused_ln, int* epoch_bump) {
+                        int* drop, bool fused_ln, int* epoch_bump, uint64_t* gran, const int* epoch) {
   AttPrep P;
   if (!prep_att_persist(ln, rkv, wkv, wo, cnt, cnt_prev, err, R, H, stamps, opts, P)) return false;
   P.sy.drop = drop;
@@ -2768,6 +2818,16 @@ bool launch_att_persist(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs&
     P.sy.n_ln_blocks = 0;
     P.sy.d_w = 0;  // (the hold only kept the weight streams off the LayerNorm rows' loads)
     n_fix = 1;
+    // the granule hand-offs (rkv -> WKV, WKV -> Wo): four rkv splits (the WKV's NP), 64-channel
+    // heads, 128-channel Wo K-slices (its granule role's KS)
+    if (gran && epoch && rkv.k_split == 4 && wkv.C == 16 * 64 && wo.k_split == 8 && ln.layer < 64 &&
+        wkv.ldp >= 3 * wkv.C + 288) {
+      P.sy.gran = gran;
+      P.sy.zgran = gran + (int64_t)4 * wkv.ldp;
+      P.sy.gran_ld = wkv.ldp;
+      P.sy.epoch = epoch;
+      P.sy.layer = ln.layer;
+    }
   }
   const bool emb = ln.emb != nullptr;
   LnMixArgs& l = P.l;
