@@ -1672,6 +1672,20 @@ void launch_relu2_planes(const float* part, int nx, int64_t pstride, int ld, int
 struct PfHolds {
   int h[5];
 };
+// The row-fused (one-row) forms hold the Wo and the FFN value weight streams instead (the rkv /
+// key ones feed the first GEMM there): 4 / 1 us (same-box B = 1 A/B: 525 -> 513-517 us per step,
+// round 5). RWKVTTS_PF_HOLD1="wo,value" overrides.
+struct PfHolds1 {
+  int wo, val;
+};
+static const PfHolds1& prefetch_holds1() {
+  static const PfHolds1 ph = [] {
+    PfHolds1 p{400, 100};
+    if (const char* e = getenv("RWKVTTS_PF_HOLD1")) sscanf(e, "%d,%d", &p.wo, &p.val);
+    return p;
+  }();
+  return ph;
+}
 static void prefetch_holds(FfnSync& sy) {
   // parsed once, by a thread-safe static initialiser (engines on several devices may launch from
   // their owner threads at the same time)
@@ -1751,6 +1765,7 @@ bool launch_ffn_persist(const LnMixArgs& ln, const GemmArgs& key, const GemmArgs
     P.sy.n_ln_blocks = 0;
     P.sy.d_k = 0;
     P.sy.opts &= ~1;  // (no LayerNorm rows for the value workgroups to wait for)
+    P.sy.d_v = prefetch_holds1().val;
     n_fix = 1;
     // the granule key -> value hand-off: four key splits (the value role's NX), one segment
     if (gran && epoch && key.k_split == 4 && key.nseg == 1 && ln.layer < 64) {
@@ -2817,6 +2832,7 @@ bool launch_att_persist(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs&
   if (fused) {
     P.sy.n_ln_blocks = 0;
     P.sy.d_w = 0;  // (the hold only kept the weight streams off the LayerNorm rows' loads)
+    P.sy.d_late = prefetch_holds1().wo;
     n_fix = 1;
     // the granule hand-offs (rkv -> WKV, WKV -> Wo): four rkv splits (the WKV's NP), 64-channel
     // heads, 128-channel Wo K-slices (its granule role's KS)
