@@ -178,6 +178,10 @@ class Engine {
   bool gran_ = true;
   uint64_t* d_gran_ = nullptr;
   uint64_t* d_gran_att_ = nullptr;  // the attention form's (rkv -> WKV, WKV -> Wo)
+  // one-row passes, layers > 0: the two halves as one launch (launch_layer1_persist). Measured
+  // slower than two launches (B = 1: 525-529 vs 515-519 us per step, profiles/r05w_layer1_ab.txt):
+  // off by default, RWKVTTS_LAYER1=1 turns it on.
+  bool layer1_ = false;
   int* d_epoch_ = nullptr;
   int ffn_persist_ = 5;     // RWKVTTS_FFN_PERSIST: decode steps' FFN half as one launch (k_ffn_persist);
                             // 0 off, else 1 + 2 x launch options (5: long poll sleep, the measured best)

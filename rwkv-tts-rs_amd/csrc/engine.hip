@@ -166,6 +166,7 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
   if (const char* pm = getenv("RWKVTTS_PERSIST_MIN_ROWS")) persist_min_rows_ = atoi(pm);
   if (const char* fl = getenv("RWKVTTS_FUSE_LN1")) fuse_ln1_ = atoi(fl) != 0;
   if (const char* gr = getenv("RWKVTTS_GRAN")) gran_ = atoi(gr) != 0;
+  if (const char* l1 = getenv("RWKVTTS_LAYER1")) layer1_ = atoi(l1) != 0;
   if ((ffn_persist_ || att_persist_) && !claim_persistent(desc.device, this, &lock_fd_)) ffn_persist_ = att_persist_ = 0;
   if (const char* gp = getenv("RWKVTTS_GEMM_STAMPS")) {
     dbg_gstamp_path_ = gp;
@@ -715,14 +716,20 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     // decode steps: the attention half as ONE persistent launch (k_att_persist: LN1 + mixes, rkv +
     // LoRA-down, WKV, Wo with in-launch hand-offs; bit-identical outputs) where the shapes allow it
     bool att_persisted = false;
-    if (use_att) {
+    // one-row passes, layers > 0: both halves as ONE launch (launch_layer1_persist, below at the
+    // FFN half) -- the attention half is launched here only if that form does not apply
+    const bool layer1 = layer1_ && gran_live && l > 0 && use_att && use_ffn && R == 1 && fuse_ln1_;
+    if (layer1) att_persisted = true;  // (issued with the FFN half)
+    auto launch_att = [&]() -> bool {
+      return launch_att_persist(m, g, k, go, att_sync_ + (size_t)l * kAttSyncInts,
+                                att_sync_ + (size_t)((l + Lc - 1) % Lc) * kAttSyncInts, (int*)(d_ctrl_ + S_), R, H_,
+                                stream_, l == 5 ? dbg_astamps2_ : nullptr, att_persist_ >> 1, d_drop_, fuse_ln1_,
+                                l == 0 && gran_pass ? d_epoch_ : nullptr, gran_live ? d_gran_att_ : nullptr, d_epoch_);
+    };
+    if (use_att && !layer1) {
       m.tl = g.tl = k.tl = go.tl = tl_next("att_persist");
       prof_begin(&ev);
-      att_persisted = launch_att_persist(m, g, k, go, att_sync_ + (size_t)l * kAttSyncInts,
-                                         att_sync_ + (size_t)((l + Lc - 1) % Lc) * kAttSyncInts,
-                                         (int*)(d_ctrl_ + S_), R, H_, stream_, l == 5 ? dbg_astamps2_ : nullptr,
-                                         att_persist_ >> 1, d_drop_, fuse_ln1_, l == 0 && gran_pass ? d_epoch_ : nullptr,
-                                         gran_live ? d_gran_att_ : nullptr, d_epoch_);
+      att_persisted = launch_att();
       if (att_persisted) {
         prof_end("att_persist", ev);
         if (l == 0 && gran_pass) gran_live = true;  // this pass's epoch is bumped
@@ -790,7 +797,28 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     // decode steps: the whole FFN half as ONE persistent launch (k_ffn_persist, in-launch
     // hand-offs; bit-identical outputs) where the shapes allow it
     bool persisted = false;
-    if (use_ffn) {
+    if (layer1) {
+      m.tl = g.tl = k.tl = go.tl = f.tl = gk.tl = gv.tl = tl_next("layer1_persist");
+      prof_begin(&ev);
+      persisted = launch_layer1_persist(m, g, k, go, f, gk, gv, att_sync_ + (size_t)l * kAttSyncInts,
+                                        att_sync_ + (size_t)((l + Lc - 1) % Lc) * kAttSyncInts,
+                                        ffn_sync_ + (size_t)l * kFfnSyncInts,
+                                        ffn_sync_ + (size_t)((l + Lc - 1) % Lc) * kFfnSyncInts, (int*)(d_ctrl_ + S_),
+                                        H_, stream_, att_persist_ >> 1, ffn_persist_ >> 1, d_gran_att_, d_gran_, d_epoch_);
+      if (persisted) {
+        prof_end("layer1_persist", ev);
+      } else {  // not covered: the two launches
+        if (tl_base() && tl_n_ > 0) {
+          --tl_n_;
+          if ((int)tl_names_.size() > tl_n_) tl_names_.resize(tl_n_);
+        }
+        m.tl = g.tl = k.tl = go.tl = tl_next("att_persist");
+        prof_begin(&ev);
+        RT_CHECK(launch_att(), RWKVTTS_EHIP, "persistent attention launch: a layer after layer 0 fell back");
+        prof_end("att_persist", ev);
+      }
+    }
+    if (use_ffn && !persisted) {
       f.tl = gk.tl = gv.tl = tl_next("ffn_persist");
       prof_begin(&ev);
       persisted = launch_ffn_persist(f, gk, gv, ffn_sync_ + (size_t)l * kFfnSyncInts,

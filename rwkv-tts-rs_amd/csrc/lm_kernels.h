@@ -119,6 +119,17 @@ struct GemmArgsT {
   uint32_t tinfo[NTINFO_];
 };
 using GemmArgs = GemmArgsT<8, 128>;
+// a single-segment launch's arguments without the segment / descriptor tables (the roles of the
+// one-launch-per-layer form, whose kernel arguments must stay under 4 KB)
+using GemmArgs1 = GemmArgsT<1, 1>;
+inline GemmArgs1 gemm_args1(const GemmArgs& a) {
+  GemmArgs1 b;
+  static_assert(offsetof(GemmArgs, seg) == offsetof(GemmArgs1, seg), "shared scalar layout");
+  memcpy((void*)&b, (const void*)&a, offsetof(GemmArgs, seg));
+  b.seg[0] = a.seg[0];
+  b.tinfo[0] = 0;
+  return b;
+}
 
 struct WkvArgs {
   const float* part;   // [n_part][R][ldp]
@@ -224,6 +235,12 @@ struct FfnSync {     // (both persistent launches)
   // attention (one row): rkv -> WKV granules at gran[split * gran_ld + column] (gran_ld = the rkv
   // output width), WKV -> Wo granules at zgran[channel] (the z split hi | lo << 16)
   uint64_t* zgran;
+  // one launch per layer (k_layer1_persist): the attention half's Wo workgroups and its shift
+  // writer count into wo_done (kLnReplicas replicas, after draining); the FFN key workgroups wait
+  // on dep (replica blockIdx % 8) for dep_target before their LayerNorm
+  int* wo_done;
+  const int* dep;
+  int dep_target;
   int* epoch_bump;  // (attention launch of layer 0) one lane adds 1 to it
 };
 
@@ -244,6 +261,13 @@ inline int64_t att_gran_count(int rkv_splits, int ldp, int C) { return (int64_t)
 bool launch_ffn_persist(const LnMixArgs& ln, const GemmArgs& key, const GemmArgs& val, int* cnt, int* cnt_prev,
                         int* err, int R, hipStream_t st, uint64_t* stamps = nullptr, int opts = 0,
                         bool fused_ln = false, uint64_t* gran = nullptr, const int* epoch = nullptr);
+// One decode row, layers > 0: the attention half and the FFN half (both row-fused, both granule
+// hand-offs) as ONE launch (k_layer1_persist); false if the shapes / options are not covered (the
+// caller then runs launch_att_persist and launch_ffn_persist).
+bool launch_layer1_persist(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs& wkv, const GemmArgs& wo,
+                           const LnMixArgs& lf, const GemmArgs& key, const GemmArgs& val, int* acnt, int* acnt_prev,
+                           int* fcnt, int* fcnt_prev, int* err, int H, hipStream_t st, int aopts, int fopts,
+                           uint64_t* agran, uint64_t* fgran, const int* epoch);
 // granules the row-fused FFN form's key -> value hand-off needs (FfnSync::gran)
 inline int64_t ffn_gran_count(int key_splits, int F) { return (int64_t)key_splits * F; }
 // Fills a.tw / a.tinfo / a.n_tinfo when the segments' packed weights are contiguous in 64-column

@@ -926,8 +926,16 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
     }
     __syncthreads();
     sync_stamp(sy, 1);
-  } else if constexpr (ROLE == 5 || ROLE == 6) {
+  } else if constexpr (ROLE == 5 || ROLE == 6 || ROLE == 9) {
     static_assert(MT == 1 && XMODE == kXPlanes, "row-fused LayerNorm: one row, planes");
+    // ROLE 9 (the FFN key role of the one-launch-per-layer form): weights at dispatch, then wait
+    // until the attention half's Wo workgroups and shift writer have published (its residual and
+    // partial slabs are this launch's: sc1 loads below)
+    if constexpr (ROLE == 9) {
+      hold_until(sy.d_k);
+      load_w();
+      sync_wait(sy.dep + kSyncStride * (blockIdx.x & (kLnReplicas - 1)), sy.dep_target, sy.err, 4096, sy.opts);
+    }
     // the row's LayerNorm (all 256 threads: thread t owns columns [4t, 4t + 4)), then this
     // K-slice's mix split into row 0 of the X image (rows 1..15 are never stored). The LayerNorm
     // inputs (L2 / MALL hits, written by the previous launch) are requested BEFORE the weight stream
@@ -942,12 +950,19 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
       for (int m = 1; m < 6; ++m)
         if (tile_mix == m) mup = L.mu[m];
     }
-    float4_ v = ld4(L.h_in + c);
-    float4_ tp[NPL];
+    float4_ v, tp[NPL];
+    if constexpr (ROLE == 9) {
+      v = __builtin_bit_cast(float4_, ld_sc1_b128(wt_rsrc(L.h_in), c * 4));
 #pragma unroll
-    for (int p = 0; p < NPL; ++p) tp[p] = ld4(L.part + p * L.part_stride + c);
+      for (int p = 0; p < NPL; ++p)
+        tp[p] = __builtin_bit_cast(float4_, ld_sc1_b128(wt_rsrc(L.part + p * L.part_stride), c * 4));
+    } else {
+      v = ld4(L.h_in + c);
+#pragma unroll
+      for (int p = 0; p < NPL; ++p) tp[p] = ld4(L.part + p * L.part_stride + c);
+    }
     const float4_ lw = ld4(L.ln_w + c), lb = ld4(L.ln_b + c);
-    load_w();
+    if constexpr (ROLE != 9) load_w();
     // (after the weights: the token-shift row's address waits for the row descriptor)
     const int4 info = L.rows[0];
     const float4_ mu = ld4(mup + c);
@@ -1020,7 +1035,7 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
   // 3) X -> LDS (rows past M: zeros in the persistent roles (never fetched), a copy of row M-1 in the
   // plain launches; an MFMA output row depends on its own X row only, and those rows' outputs are not
   // stored)
-  if constexpr (ROLE == 5 || ROLE == 6 || ROLE == 8) {
+  if constexpr (ROLE == 5 || ROLE == 6 || ROLE == 8 || ROLE == 9) {
     // (staged by the row-fused LayerNorm / the granule sweep above)
   } else if constexpr (XMODE == kXPlanes) {
 #pragma unroll
@@ -1172,7 +1187,7 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
     }
     return v;
   };
-  if (ROLE == 6 && sy.gran) {
+  if ((ROLE == 6 || ROLE == 9) && sy.gran) {
     // granule form: row 0's 64 columns, one {f32, tag} granule per element (lanes 0..15 of each
     // wave hold row 0: g == 0, j == 0)
     if (g == 0 && col < Nn) gran_store(sy.gran + (int64_t)split * sy.gran_ld + col_off + col, result(0, 0), gran_tag(sy));
@@ -1218,7 +1233,10 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
   }
   if constexpr (ROLE != 0) sync_stamp(sy, 2);
   if constexpr (ROLE == 1) sync_arrive(sy.cnt + kSyncStride * (kLnReplicas + tile / sy.key_group));
-  if constexpr (ROLE == 6) {  // K-slice counter (replica 0; not in the granule form) and key-done (lane 1)
+  if constexpr (ROLE == 8) {  // (one launch per layer) the FFN key workgroups wait for the Wo slabs
+    if (sy.wo_done) sync_arrive(sy.wo_done, kLnReplicas);
+  }
+  if constexpr (ROLE == 6 || ROLE == 9) {  // K-slice counter (replica 0; not in the granule form) and key-done (lane 1)
     if (!sy.gran) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0 && !sy.gran)
@@ -1754,13 +1772,14 @@ static bool prep_ffn_persist(const LnMixArgs& ln, const GemmArgs& key, const Gem
   return true;
 }
 
-bool launch_ffn_persist(const LnMixArgs& ln, const GemmArgs& key, const GemmArgs& val, int* cnt, int* cnt_prev,
-                        int* err, int R, hipStream_t st, uint64_t* stamps, int opts, bool fused_ln, uint64_t* gran,
-                        const int* epoch) {
-  FfnPrep P;
+// the FFN half's arguments, its row-fused form (n_fix = 1: the trailing shift writer) and the
+// granule hand-off where they apply
+static bool ffn_setup(const LnMixArgs& ln, const GemmArgs& key, const GemmArgs& val, int* cnt, int* cnt_prev, int* err,
+                      int R, uint64_t* stamps, int opts, bool fused_ln, uint64_t* gran, const int* epoch, FfnPrep& P,
+                      int& n_fix) {
   if (!prep_ffn_persist(ln, key, val, cnt, cnt_prev, err, R, stamps, opts, P)) return false;
   const bool fused = fused_ln && R == 1 && ln.inplace;
-  int n_fix = 0;
+  n_fix = 0;
   if (fused) {
     P.sy.n_ln_blocks = 0;
     P.sy.d_k = 0;
@@ -1775,6 +1794,16 @@ bool launch_ffn_persist(const LnMixArgs& ln, const GemmArgs& key, const GemmArgs
       P.sy.layer = ln.layer;
     }
   }
+  return true;
+}
+
+bool launch_ffn_persist(const LnMixArgs& ln, const GemmArgs& key, const GemmArgs& val, int* cnt, int* cnt_prev,
+                        int* err, int R, hipStream_t st, uint64_t* stamps, int opts, bool fused_ln, uint64_t* gran,
+                        const int* epoch) {
+  FfnPrep P;
+  int n_fix = 0;
+  if (!ffn_setup(ln, key, val, cnt, cnt_prev, err, R, stamps, opts, fused_ln, gran, epoch, P, n_fix)) return false;
+  const bool fused = n_fix == 1;
   LnMixArgs& l = P.l;
   GemmArgs& ka = P.ka;
   GemmArgs& va = P.va;
@@ -2820,15 +2849,16 @@ static bool prep_att_persist(const LnMixArgs& ln, const GemmArgs& rkv, const Wkv
   return true;
 }
 
-bool launch_att_persist(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs& wkv, const GemmArgs& wo, int* cnt,
-                        int* cnt_prev, int* err, int R, int H, hipStream_t st, uint64_t* stamps, int opts,
-                        int* drop, bool fused_ln, int* epoch_bump, uint64_t* gran, const int* epoch) {
-  AttPrep P;
+// the attention half's arguments, its row-fused form (n_fix = 1: the trailing shift writer) and
+// the granule hand-offs where they apply
+static bool att_setup(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs& wkv, const GemmArgs& wo, int* cnt,
+                      int* cnt_prev, int* err, int R, int H, uint64_t* stamps, int opts, int* drop, bool fused_ln,
+                      int* epoch_bump, uint64_t* gran, const int* epoch, AttPrep& P, int& n_fix) {
   if (!prep_att_persist(ln, rkv, wkv, wo, cnt, cnt_prev, err, R, H, stamps, opts, P)) return false;
   P.sy.drop = drop;
   P.sy.epoch_bump = epoch_bump;
   const bool fused = fused_ln && R == 1 && ln.emb == nullptr && ln.inplace;
-  int n_fix = 0;  // the row-fused form's shift writer
+  n_fix = 0;
   if (fused) {
     P.sy.n_ln_blocks = 0;
     P.sy.d_w = 0;  // (the hold only kept the weight streams off the LayerNorm rows' loads)
@@ -2845,6 +2875,18 @@ bool launch_att_persist(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs&
       P.sy.layer = ln.layer;
     }
   }
+  return true;
+}
+
+bool launch_att_persist(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs& wkv, const GemmArgs& wo, int* cnt,
+                        int* cnt_prev, int* err, int R, int H, hipStream_t st, uint64_t* stamps, int opts,
+                        int* drop, bool fused_ln, int* epoch_bump, uint64_t* gran, const int* epoch) {
+  AttPrep P;
+  int n_fix = 0;  // the row-fused form's shift writer
+  if (!att_setup(ln, rkv, wkv, wo, cnt, cnt_prev, err, R, H, stamps, opts, drop, fused_ln, epoch_bump, gran, epoch, P,
+                 n_fix))
+    return false;
+  const bool fused = n_fix == 1;
   const bool emb = ln.emb != nullptr;
   LnMixArgs& l = P.l;
   GemmArgs& ga = P.ga;
@@ -2863,6 +2905,88 @@ bool launch_att_persist(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs&
     else if (fused) RT_LAUNCH((k_att_persist<false, false, true>), grid, dim3(256), lds, st, l, ga, wa, gw, sy);
     else RT_LAUNCH((k_att_persist<false, false, false>), grid, dim3(256), lds, st, l, ga, wa, gw, sy);
   }
+  return true;
+}
+
+// ------------------------------------------------------------------------------------
+// layer1_persist: one decode row, layers > 0 -- the row-fused, granule-hand-off attention half and
+// FFN half of a layer as ONE launch:
+//   [0, n_rkv)            rkv + LoRA-down (ROLE 5: own LayerNorm 1)
+//   [+, +n_wkv)           WKV (z granules out)
+//   [+, +n_wo)            Wo (ROLE 8: z granules in), then count into wo_done (8 replicas)
+//   +1                    attention shift writer (residual h1 + token shift), counts into wo_done
+//   [+, +n_key)           FFN key (ROLE 9: weights at dispatch, waits for wo_done, own LayerNorm 2
+//                         from this launch's h1 and Wo slabs by sc1 loads, granules out)
+//   [+, +n_val)           FFN value (ROLE 7: key granules in)
+//   +1                    FFN shift writer (residual h0 + token shift, sc1 loads)
+// The FFN workgroups are dispatched as attention workgroups retire, so their weight streams run
+// beside the attention chain's tail instead of after a launch boundary. Every dependency points to
+// a lower block index. Outputs: the two launches', bit for bit.
+template <bool F16>
+__global__ __launch_bounds__(256, RWKVTTS_ATT_WPC) void k_layer1_persist(LnMixArgs ln, GemmArgs ga, WkvArgs wa,
+                                                                          GemmArgs1 go, LnMixArgs lf, GemmArgs1 ka,
+                                                                          GemmArgs1 va, FfnSync sy, FfnSync sf) {
+  int b = blockIdx.x;
+  tl_begin(ln.tl);
+  const int n_att = sy.n_key + sy.n_wkv + 16 * go.k_split + 1;
+  if (b < n_att) {
+    if (b < sy.n_key) {
+      gemm2_body<1, 8, kXPlanes, F16, 1, 2, false, 5>(ga, b % sy.rkv_tiles, b / sy.rkv_tiles, sy, &ln);
+    } else if ((b -= sy.n_key) < sy.n_wkv) {
+      wkv6_body<F16, 2>(wa, b, 0, sy);
+    } else if ((b -= sy.n_wkv) < 16 * go.k_split) {
+      gemm2_body<1, 4, kXPlanes, F16, 1, 0, false, 8>(go, b, 0, sy);
+    } else {  // attention shift writer
+      if (threadIdx.x < sy.n_prev) sy.cnt_prev[threadIdx.x * kSyncStride] = 0;
+      sync_wait(sy.cnt + kSyncStride * kAttRkvDone, sy.n_key, sy.err, 2048, sy.opts);
+      ln1024_body<F16, 1, 0, 16>(ln, 0);
+      sync_arrive(sy.wo_done, kLnReplicas);
+    }
+  } else if ((b -= n_att) < sf.n_key) {
+    gemm2_body<1, 8, kXPlanes, F16, 1, 0, false, 9>(ka, b, 0, sf, &lf);
+  } else if ((b -= sf.n_key) < sf.n_val) {
+    gemm2_body<1, 8, kXRelu2, F16, 4, 0, false, 7>(va, b, 0, sf);
+  } else {  // FFN shift writer (its residual and slabs are this launch's: sc1 loads)
+    if (threadIdx.x < sf.n_prev) sf.cnt_prev[threadIdx.x * kSyncStride] = 0;
+    sync_wait(sf.cnt + kSyncStride * kFfnKeyDone, sf.n_key, sf.err, 1024, sf.opts);
+    ln1024_body<F16, 1, 0, 8, false, true>(lf, 0);
+  }
+  tl_end(ln.tl);
+}
+
+bool launch_layer1_persist(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs& wkv, const GemmArgs& wo,
+                           const LnMixArgs& lf, const GemmArgs& key, const GemmArgs& val, int* acnt, int* acnt_prev,
+                           int* fcnt, int* fcnt_prev, int* err, int H, hipStream_t st, int aopts, int fopts,
+                           uint64_t* agran, uint64_t* fgran, const int* epoch) {
+  AttPrep A;
+  FfnPrep F;
+  int na = 0, nf = 0;
+  if (!att_setup(ln, rkv, wkv, wo, acnt, acnt_prev, err, 1, H, nullptr, aopts, nullptr, true, nullptr, agran, epoch,
+                 A, na) ||
+      !ffn_setup(lf, key, val, fcnt, fcnt_prev, err, 1, nullptr, fopts, true, fgran, epoch, F, nf))
+    return false;
+  // both halves in their one-row form with the granule hand-offs; the FFN K-slice counters are then
+  // unused and carry the attention half's "published" count (8 replicas)
+  if (na != 1 || nf != 1 || !A.sy.gran || !F.sy.gran || ln.emb != nullptr || wo.nseg != 1 || key.nseg != 1 ||
+      val.nseg != 1)
+    return false;
+  int* wo_done = fcnt + kSyncStride * kLnReplicas;
+  A.sy.wo_done = wo_done;
+  // (RWKVTTS_L1_KHOLD: hold the FFN key weight streams of the workgroups resident at dispatch;
+  // 4 / 7 / 10 us measured slower, 526 -> 540 / 554 / 592 us per step at B = 1)
+  static const int khold = getenv("RWKVTTS_L1_KHOLD") ? atoi(getenv("RWKVTTS_L1_KHOLD")) : 0;
+  F.sy.d_k = khold;
+  F.sy.dep = wo_done;
+  F.sy.dep_target = 16 * wo.k_split + 1;
+  static_assert(kFfnSlices >= kLnReplicas, "the Wo-done replicas live in the K-slice counters");
+  const GemmArgs1 go1 = gemm_args1(A.gw), ka1 = gemm_args1(F.ka), va1 = gemm_args1(F.va);
+  static_assert(sizeof(LnMixArgs) * 2 + sizeof(GemmArgs) + sizeof(WkvArgs) + 3 * sizeof(GemmArgs1) +
+                        2 * sizeof(FfnSync) <= 4096, "k_layer1_persist's arguments must fit 4 KB");
+  const int n_att = A.sy.n_key + A.sy.n_wkv + 16 * wo.k_split + 1;
+  const dim3 grid(n_att + F.sy.n_key + F.nv + 1);
+  const size_t lds = (size_t)2 * 16 * (8 * 32 + 8) * 2 * 2;
+  if (ln.f16) RT_LAUNCH((k_layer1_persist<true>), grid, dim3(256), lds, st, A.l, A.ga, A.wa, go1, F.l, ka1, va1, A.sy, F.sy);
+  else RT_LAUNCH((k_layer1_persist<false>), grid, dim3(256), lds, st, A.l, A.ga, A.wa, go1, F.l, ka1, va1, A.sy, F.sy);
   return true;
 }
 
