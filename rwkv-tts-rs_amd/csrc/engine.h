@@ -182,6 +182,8 @@ class Engine {
   // slower than two launches (B = 1: 525-529 vs 515-519 us per step, profiles/r05w_layer1_ab.txt):
   // off by default, RWKVTTS_LAYER1=1 turns it on.
   bool layer1_ = false;
+  // one-row steps: ln_out folded into the head GEMM (launch_gemm_lnrow). RWKVTTS_FUSE_LNOUT=0 off.
+  bool lnrow_ = true;
   int* d_epoch_ = nullptr;
   int ffn_persist_ = 5;     // RWKVTTS_FFN_PERSIST: decode steps' FFN half as one launch (k_ffn_persist);
                             // 0 off, else 1 + 2 x launch options (5: long poll sleep, the measured best)

@@ -167,6 +167,7 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
   if (const char* fl = getenv("RWKVTTS_FUSE_LN1")) fuse_ln1_ = atoi(fl) != 0;
   if (const char* gr = getenv("RWKVTTS_GRAN")) gran_ = atoi(gr) != 0;
   if (const char* l1 = getenv("RWKVTTS_LAYER1")) layer1_ = atoi(l1) != 0;
+  if (const char* lr = getenv("RWKVTTS_FUSE_LNOUT")) lnrow_ = atoi(lr) != 0;
   if ((ffn_persist_ || att_persist_) && !claim_persistent(desc.device, this, &lock_fd_)) ffn_persist_ = att_persist_ = 0;
   if (const char* gp = getenv("RWKVTTS_GEMM_STAMPS")) {
     dbg_gstamp_path_ = gp;
@@ -854,10 +855,14 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
   }
   if (n_lg > 0) {
     LnMixArgs o = ln_out_args();
-    o.tl = tl_next("ln_out");
-    prof_begin(&ev);
-    launch_ln_mix(o, n_lg, stream_);
-    prof_end("ln_out", ev);
+    // one-row steps: ln_out folded into the head GEMM (launch_gemm_lnrow) where covered
+    const bool lnrow = lnrow_ && n_lg == 1 && R == 1 && !dbg_exp_;
+    if (!lnrow) {
+      o.tl = tl_next("ln_out");
+      prof_begin(&ev);
+      launch_ln_mix(o, n_lg, stream_);
+      prof_end("ln_out", ev);
+    }
     GemmArgs gh{};
     gh.f16 = f16_;
     gh.nseg = 1;
@@ -869,7 +874,20 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     prof_begin(&ev);
     gh.exp = dbg_exp_ >> 8;
     gh.tl = tl_next("gemm_head");
-    if (!(dbg_exp_ & 0x40000)) launch_gemm(gh, stream_);
+    bool headed = false;
+    if (lnrow) {
+      o.n_rows = 1;
+      headed = launch_gemm_lnrow(gh, o, stream_);
+      if (!headed) {  // not covered: the two launches
+        prof_end("gemm_head", ev);
+        o.tl = tl_next("ln_out");
+        prof_begin(&ev);
+        launch_ln_mix(o, n_lg, stream_);
+        prof_end("ln_out", ev);
+        prof_begin(&ev);
+      }
+    }
+    if (!headed && !(dbg_exp_ & 0x40000)) launch_gemm(gh, stream_);
     prof_end("gemm_head", ev);
     if (advance) {
       AdvanceArgs a{};

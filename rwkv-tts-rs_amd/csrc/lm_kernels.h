@@ -170,6 +170,8 @@ void launch_embed(const uint32_t* tokens, const int4* rows, const int* ctrl_tok,
 // Launchers return the workgroup count of the launch.
 int launch_ln_mix(const LnMixArgs& a, int n_out_rows, hipStream_t st);
 int launch_gemm(const GemmArgs& a, hipStream_t st);
+// a one-row step's head GEMM with ln_out folded in (k_gemm2_lnrow); false if not covered
+bool launch_gemm_lnrow(const GemmArgs& a, const LnMixArgs& lo, hipStream_t st);
 // The FFN half of a decode step (LN2 + mix, key GEMM, relu^2, value GEMM) as ONE persistent launch
 // with in-launch hand-offs (k_ffn_persist); false if the shapes are not covered.
 constexpr int kFfnSyncInts = 24 * 64;  // counter block per layer: (8 LN replicas + 16 K-slices) x 256 B

@@ -926,6 +926,31 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
     }
     __syncthreads();
     sync_stamp(sy, 1);
+  } else if constexpr (ROLE == 10) {
+    // the head GEMM of a one-row step with ln_out fused (a plain launch): weights requested after
+    // the row's inputs, the row's LayerNorm computed here (ln1024_body MODE 0's arithmetic: residual
+    // + NP10 partial slabs in order, ln1024_apply) and this K-slice staged as row 0 of the X image
+    static_assert(MT == 1 && XMODE == kXPlanes, "ln_out-fused head: one row, planes");
+    constexpr int C = 1024, NP10 = 16;
+    __shared__ float s_lnred10[16];
+    const LnMixArgs& L = *lr;
+    const int c = 4 * (int)threadIdx.x;
+    float4_ v = ld4(L.h_in + c), tp[NP10];
+#pragma unroll
+    for (int p = 0; p < NP10; ++p) tp[p] = ld4(L.part + p * L.part_stride + c);
+    const float4_ lw = ld4(L.ln_w + c), lb = ld4(L.ln_b + c);
+    load_w();
+#pragma unroll
+    for (int p = 0; p < NP10; ++p) v += tp[p];
+    ln1024_apply(v, lw, lb, s_lnred10, 0);
+    if (c >= kbeg && c < kbeg + KS) {
+      uint32_t h0, l0, h1, l1;
+      split2<F16>(v[0], v[1], h0, l0);
+      split2<F16>(v[2], v[3], h1, l1);
+      *(uint2*)(xh + (c - kbeg)) = make_uint2(h0, h1);
+      *(uint2*)(xl + (c - kbeg)) = make_uint2(l0, l1);
+    }
+    static_assert(C == 1024, "");
   } else if constexpr (ROLE == 5 || ROLE == 6 || ROLE == 9) {
     static_assert(MT == 1 && XMODE == kXPlanes, "row-fused LayerNorm: one row, planes");
     // ROLE 9 (the FFN key role of the one-launch-per-layer form): weights at dispatch, then wait
@@ -1035,7 +1060,7 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
   // 3) X -> LDS (rows past M: zeros in the persistent roles (never fetched), a copy of row M-1 in the
   // plain launches; an MFMA output row depends on its own X row only, and those rows' outputs are not
   // stored)
-  if constexpr (ROLE == 5 || ROLE == 6 || ROLE == 8 || ROLE == 9) {
+  if constexpr (ROLE == 5 || ROLE == 6 || ROLE == 8 || ROLE == 9 || ROLE == 10) {
     // (staged by the row-fused LayerNorm / the granule sweep above)
   } else if constexpr (XMODE == kXPlanes) {
 #pragma unroll
@@ -1274,6 +1299,31 @@ __global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
   tl_begin(a.tl);
   gemm2_body<MT, KSTEPS, XMODE, F16, NX, MS, QW, 0>(a, blockIdx.x, blockIdx.y, FfnSync{});
   tl_end(a.tl);
+}
+
+// the head GEMM of a one-row step with ln_out folded in (gemm2_body ROLE 10): one launch and one
+// launch boundary fewer per step; logits bit for bit those of ln_out + k_gemm2
+template <bool F16>
+__global__ __launch_bounds__(256) void k_gemm2_lnrow(GemmArgs a, LnMixArgs lo) {
+  tl_begin(a.tl);
+  gemm2_body<1, 16, kXPlanes, F16, 1, 0, false, 10>(a, blockIdx.x, blockIdx.y, FfnSync{}, &lo);
+  tl_end(a.tl);
+}
+
+bool launch_gemm_lnrow(const GemmArgs& a, const LnMixArgs& lo, hipStream_t st) {
+  // one row, the head's shape: one segment of 16-bit planes, 512-wide K-slices, no XCD remap;
+  // ln_out's: C = 1024, 16 partial slabs, no row remap beyond row 0
+  if (a.M != 1 || a.nseg != 1 || a.kslice != 512 || a.xmode != kXPlanes || a.q_fmt || a.stamps || a.exp ||
+      a.allow_xmap || a.xalign > 0 || lo.C != 1024 || lo.n_part != 16 || lo.n_mix != 1 || lo.h_out != nullptr ||
+      a.f16 != lo.f16)
+    return false;
+  const int tiles = (a.seg[0].N + 63) / 64;
+  GemmArgs b = a;
+  b.xmap = 0;
+  const size_t lds = (size_t)16 * (16 * 32 + 8) * 2 * 2;
+  if (a.f16) RT_LAUNCH((k_gemm2_lnrow<true>), dim3(tiles, a.k_split, 1), dim3(256), lds, st, b, lo);
+  else RT_LAUNCH((k_gemm2_lnrow<false>), dim3(tiles, a.k_split, 1), dim3(256), lds, st, b, lo);
+  return true;
 }
 
 // ------------------------------------------------------------------------------------

@@ -32,7 +32,9 @@ MODES = {"off": dict(_M, RWKVTTS_FFN_PERSIST="0", RWKVTTS_ATT_PERSIST="0"),
          # instead of data-tagged granules
          "both_slabs": dict(_M, RWKVTTS_FFN_PERSIST="5", RWKVTTS_ATT_PERSIST="5", RWKVTTS_GRAN="0"),
          # the one-row form as one launch per layer (off by default: measured slower)
-         "both_layer1": dict(_M, RWKVTTS_FFN_PERSIST="5", RWKVTTS_ATT_PERSIST="5", RWKVTTS_LAYER1="1")}
+         "both_layer1": dict(_M, RWKVTTS_FFN_PERSIST="5", RWKVTTS_ATT_PERSIST="5", RWKVTTS_LAYER1="1"),
+         # separate launches with ln_out as its own launch (not folded into the one-row head GEMM)
+         "off_lnout": dict(_M, RWKVTTS_FFN_PERSIST="0", RWKVTTS_ATT_PERSIST="0", RWKVTTS_FUSE_LNOUT="0")}
 
 
 class _env:
@@ -116,13 +118,14 @@ def test_persist_one_row_fused_layernorm_bitwise(dtype):
     """One decode row (a lone request): the persistent halves run their row-fused form (no LayerNorm
     workgroups: every rkv / key workgroup computes the row's LayerNorm itself, a trailing workgroup
     stores the residual and the token-shift row; the FFN key -> value hand-off as data-tagged
-    granules). Bitwise the separate launches', the LayerNorm-row form's, the slab hand-off's and the
-    one-launch-per-layer form's tokens and recurrent state, graph replay and eager."""
+    granules; ln_out folded into the head GEMM). Bitwise the separate launches' (ln_out as its own
+    launch, and folded), the LayerNorm-row form's, the slab hand-off's and the one-launch-per-layer
+    form's tokens and recurrent state, graph replay and eager."""
     dt = rwkvtts._ffi.DTYPE_F16 if dtype == "f16" else rwkvtts._ffi.DTYPE_BF16
     blob = W.synth_blob(W.DIMS_04B, seed=11, dtype=dt)
     reqs = [make_request(synth_text(500), seed=5, fixed=40)]
     for graphs in (True, False):
-        outs, _ = _both(blob, reqs, modes=("off", "both", "both_rows", "both_slabs", "both_layer1"), max_slots=4,
+        outs, _ = _both(blob, reqs, modes=("off_lnout", "off", "both", "both_rows", "both_slabs", "both_layer1"), max_slots=4,
                         token_chunk_size=512, use_graphs=graphs)
         assert all(o == outs[0] for o in outs[1:]), graphs
 
