@@ -237,6 +237,7 @@ struct FfnSync {     // (both persistent launches)
   // attention (one row): rkv -> WKV granules at gran[split * gran_ld + column] (gran_ld = the rkv
   // output width), WKV -> Wo granules at zgran[channel] (the z split hi | lo << 16)
   uint64_t* zgran;
+  int rkv_gran;  // (attention, one row) the rkv workgroups hand their row to the WKV ones as granules
   // one launch per layer (k_layer1_persist): the attention half's Wo workgroups and its shift
   // writer count into wo_done (kLnReplicas replicas, after draining); the FFN key workgroups wait
   // on dep (replica blockIdx % 8) for dep_target before their LayerNorm

@@ -1212,7 +1212,7 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
     }
     return v;
   };
-  if ((ROLE == 6 || ROLE == 9) && sy.gran) {
+  if (((ROLE == 6 || ROLE == 9) && sy.gran) || (ROLE == 5 && sy.rkv_gran)) {
     // granule form: row 0's 64 columns, one {f32, tag} granule per element (lanes 0..15 of each
     // wave hold row 0: g == 0, j == 0)
     if (g == 0 && col < Nn) gran_store(sy.gran + (int64_t)split * sy.gran_ld + col_off + col, result(0, 0), gran_tag(sy));
@@ -1276,11 +1276,12 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
     if (c0 < 3 * sy.C) sync_arrive(sy.cnt + kSyncStride * (kAttHead + ((c0 % sy.C) >> 6)), 1, sy.drop);
     else sync_arrive(sy.cnt + kSyncStride * kAttLora, kLnReplicas);
   }
-  if constexpr (ROLE == 5) {  // as ROLE 3, plus rkv-done (lane 8) for the shift writer
+  if constexpr (ROLE == 5) {  // as ROLE 3 (not with the rkv granules), plus rkv-done (lane 8) for the shift writer
     const int c0 = col_off + (tile - tstart) * 64;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!sy.rkv_gran) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (c0 < 3 * sy.C) {
+    if (sy.rkv_gran) {
+    } else if (c0 < 3 * sy.C) {
       if (threadIdx.x == 0)
         __hip_atomic_fetch_add((gint_t*)(sy.cnt + kSyncStride * (kAttHead + ((c0 % sy.C) >> 6))), 1,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2579,11 +2580,80 @@ __device__ __attribute__((always_inline)) void wkv6_body(const WkvArgs& a, const
 #pragma unroll
     for (int u = 0; u < 9; ++u) lw[u] = pl[u * 256 + t];
     load_state(slot);
+    if constexpr (ROLE == 3) {
+      // rkv -> WKV granules (one row): each thread polls a few of the granules the workgroup needs
+      // -- the r / k / v of its channel in split qq, and two-granule pieces of the LoRA hidden
+      // columns -- until every wave sees this pass's tag (votes through LDS, two slots), then the
+      // values go through LDS into load_parts' register layout (the same numbers, the same sums)
+      __shared__ float s_rkv[NP][3][N];
+      __shared__ float s_hidp[NP][DALL];
+      __shared__ int s_ok[2][4];
+      constexpr int NHL = NP * DALL / 2;  // 16-byte hidden loads (two granules each)
+      const uint32_t tag = gran_tag(sy);
+      const auto rs = wt_rsrc(sy.gran);
+      const int ld = sy.gran_ld;
+      float gr_v[3], gh_v[3][2];
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      for (int round = 0;; round ^= 1) {
+        bool ok = true;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          const uint64_t g = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(
+                                                              rs, (qq * ld + q * C + c) * 8, 0, 16));
+          gr_v[q] = __builtin_bit_cast(float, (uint32_t)g);
+          ok = ok && (uint32_t)(g >> 32) == tag;
+        }
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+          const int j = t + 256 * u;
+          if (j < NHL) {
+            const int p = j / (DALL / 2), col = 3 * C + 2 * (j % (DALL / 2));
+            const u64x2_ g = __builtin_bit_cast(u64x2_, ld_sc1_b128(rs, (p * ld + col) * 8));
+            gh_v[u][0] = __builtin_bit_cast(float, (uint32_t)g.x);
+            gh_v[u][1] = __builtin_bit_cast(float, (uint32_t)g.y);
+            ok = ok && (uint32_t)(g.x >> 32) == tag && (uint32_t)(g.y >> 32) == tag;
+          }
+        }
+        const bool wok = __all(ok);
+        if (lane == 0) s_ok[round][wave] = wok ? 1 : 0;
+        __syncthreads();
+        if (s_ok[round][0] && s_ok[round][1] && s_ok[round][2] && s_ok[round][3]) break;
+        __builtin_amdgcn_s_sleep(1);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 5000000ull) {
+          if (t == 0) __hip_atomic_fetch_or((gint_t*)sy.err, 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 3; ++q) s_rkv[qq][q][i] = gr_v[q];
+#pragma unroll
+      for (int u = 0; u < 3; ++u) {
+        const int j = t + 256 * u;
+        if (j < NHL) {
+          const int p = j / (DALL / 2), hc = 2 * (j % (DALL / 2));
+          s_hidp[p][hc] = gh_v[u][0];
+          s_hidp[p][hc + 1] = gh_v[u][1];
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+        rp[p] = s_rkv[p][0][i];
+        kp[p] = s_rkv[p][1][i];
+        vp[p] = s_rkv[p][2][i];
+        hp[p] = *(const float4_*)&s_hidp[p][hid_thread ? 4 * t : 0];
+      }
+      sync_stamp(sy, 1);
+      vf = a.layer > 0 ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                     wt_rsrc(a.v_first + (int64_t)r_begin * a.ldv), c * 4, 0, 16))
+                       : 0.f;
+    } else {
     sync_wait(sy.cnt + kSyncStride * (kAttHead + h), sy.head_target, sy.err, 16, sy.opts);
     sync_wait(sy.cnt + kSyncStride * (kAttLora + (blockIdx.x & (kLnReplicas - 1))), sy.lora_target, sy.err, 32,
               sy.opts);
     sync_stamp(sy, 1);
     load_parts(r_begin);
+    }
   } else {
   load_parts(spec);
 #pragma unroll
@@ -2722,7 +2792,7 @@ __device__ __attribute__((always_inline)) void wkv6_body(const WkvArgs& a, const
     const float mean = ((s_red[2][0] + s_red[2][1]) + (s_red[2][2] + s_red[2][3])) * (1.0f / N);
     const float var =
         fmaxf(((s_red[3][0] + s_red[3][1]) + (s_red[3][2] + s_red[3][3])) * (1.0f / N) - mean * mean, 0.f);
-    if constexpr (ROLE == 2) {
+    if constexpr (ROLE == 2 || ROLE == 3) {
       // granule form: the channel's split as ONE granule {hi | lo << 16, tag} (same expression
       // and threads as below, so the same bits) -- the Wo workgroups poll these directly
       if (qq == 0) {
@@ -2822,7 +2892,8 @@ __global__ __launch_bounds__(256, RWKVTTS_ATT_WPC) void k_att_persist(LnMixArgs 
     else gemm2_body<2, 8, kXPlanes, F16, 1, 2, false, 3>(ga, b % sy.rkv_tiles, b / sy.rkv_tiles, sy);
   } else if ((b -= sy.n_key) < sy.n_wkv) {
     if constexpr (FUSED && !EMB) {
-      if (sy.gran) wkv6_body<F16, 2>(wa, b, 0, sy);
+      if (sy.rkv_gran) wkv6_body<F16, 3>(wa, b, 0, sy);
+      else if (sy.gran) wkv6_body<F16, 2>(wa, b, 0, sy);
       else wkv6_body<F16, 1>(wa, b, 0, sy);
     } else {
       wkv6_body<F16, 1>(wa, b, 0, sy);
@@ -2923,6 +2994,11 @@ static bool att_setup(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs& w
       P.sy.gran_ld = wkv.ldp;
       P.sy.epoch = epoch;
       P.sy.layer = ln.layer;
+      // rkv -> WKV as granules too (RWKVTTS_RKV_GRAN=1; the WKV role's quad-split sweep): measured
+      // slower than the counter hand-off (B = 1: 530-535 vs 513-517 us per step; the WKV workgroups
+      // see the last granule 1.7 us after the last rkv workgroup ends, the counters 0.4 us), off
+      static const int rkv_gran = getenv("RWKVTTS_RKV_GRAN") ? atoi(getenv("RWKVTTS_RKV_GRAN")) : 0;
+      P.sy.rkv_gran = rkv_gran != 0;
     }
   }
   return true;
@@ -2983,7 +3059,8 @@ __global__ __launch_bounds__(256, RWKVTTS_ATT_WPC) void k_layer1_persist(LnMixAr
     if (b < sy.n_key) {
       gemm2_body<1, 8, kXPlanes, F16, 1, 2, false, 5>(ga, b % sy.rkv_tiles, b / sy.rkv_tiles, sy, &ln);
     } else if ((b -= sy.n_key) < sy.n_wkv) {
-      wkv6_body<F16, 2>(wa, b, 0, sy);
+      if (sy.rkv_gran) wkv6_body<F16, 3>(wa, b, 0, sy);
+      else wkv6_body<F16, 2>(wa, b, 0, sy);
     } else if ((b -= sy.n_wkv) < 16 * go.k_split) {
       gemm2_body<1, 4, kXPlanes, F16, 1, 0, false, 8>(go, b, 0, sy);
     } else {  // attention shift writer

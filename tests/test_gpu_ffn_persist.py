@@ -33,6 +33,8 @@ MODES = {"off": dict(_M, RWKVTTS_FFN_PERSIST="0", RWKVTTS_ATT_PERSIST="0"),
          "both_slabs": dict(_M, RWKVTTS_FFN_PERSIST="5", RWKVTTS_ATT_PERSIST="5", RWKVTTS_GRAN="0"),
          # the one-row form as one launch per layer (off by default: measured slower)
          "both_layer1": dict(_M, RWKVTTS_FFN_PERSIST="5", RWKVTTS_ATT_PERSIST="5", RWKVTTS_LAYER1="1"),
+         # the rkv -> WKV hand-off as granules as well (off by default: measured slower)
+         "both_rkvgran": dict(_M, RWKVTTS_FFN_PERSIST="5", RWKVTTS_ATT_PERSIST="5", RWKVTTS_RKV_GRAN="1"),
          # separate launches with ln_out as its own launch (not folded into the one-row head GEMM)
          "off_lnout": dict(_M, RWKVTTS_FFN_PERSIST="0", RWKVTTS_ATT_PERSIST="0", RWKVTTS_FUSE_LNOUT="0")}
 
@@ -125,7 +127,7 @@ def test_persist_one_row_fused_layernorm_bitwise(dtype):
     blob = W.synth_blob(W.DIMS_04B, seed=11, dtype=dt)
     reqs = [make_request(synth_text(500), seed=5, fixed=40)]
     for graphs in (True, False):
-        outs, _ = _both(blob, reqs, modes=("off_lnout", "off", "both", "both_rows", "both_slabs", "both_layer1"), max_slots=4,
+        outs, _ = _both(blob, reqs, modes=("off_lnout", "off", "both", "both_rows", "both_slabs", "both_rkvgran", "both_layer1"), max_slots=4,
                         token_chunk_size=512, use_graphs=graphs)
         assert all(o == outs[0] for o in outs[1:]), graphs
 

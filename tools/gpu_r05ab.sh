@@ -1,0 +1,7 @@
+set -o pipefail
+O=gpurun_out/r05ab
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_gpu_ffn_persist.py tests/test_gpu_persist_recovery.py -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1; tail -3 $O/tests.log
+grep -q " passed" $O/tests.log && ! grep -q -E "FAILED|ERROR" $O/tests.log || exit 1
+T=rwkv-tts-rs_amd/rwkvtts/librwkvtts.so
+TAG=r05ab BS="1 32" VARIANTS="ab_libs/head8/librwkvtts.so $T" STAMP_BS=none bash tools/gpu_r05_ab.sh
