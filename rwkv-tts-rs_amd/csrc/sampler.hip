@@ -1760,18 +1760,29 @@ __device__ __attribute__((always_inline)) void advance_prep(const float* raw, co
     for (int w = 1; w < NW; ++w) L = fminf(L, sm.fred[8 + w]);
   }
   if (L > 0.0f) {
+    // the wave's candidates counted first (ballots only), ONE LDS atomic per wave reserves their
+    // slots, then they are written in the same k-major order (the list's order across waves was
+    // the atomics' order before as well; its consumers do not depend on it)
     const float T = L * (1.0f - 0x1p-19f);
+    uint64_t bms[PT];
+    int tot = 0;
 #pragma unroll
     for (int k = 0; k < PT; ++k) {
       const int i = tid + k * NT;
-      const bool c = i < n && v[k] >= T;
-      const uint64_t bm = __ballot(c);
-      if (bm) {
-        int base = 0;
-        if (lane == 0) base = atomicAdd(&sm.ired[31], __popcll(bm));
-        base = __builtin_amdgcn_readfirstlane(base);
-        const int off = base + __popcll(bm & ((1ull << lane) - 1ull));
-        if (c && off < kFastCap) sm.keys[off] = ((uint64_t)__builtin_bit_cast(uint32_t, v[k]) << 32) | (uint32_t)i;
+      bms[k] = __ballot(i < n && v[k] >= T);
+      tot += __popcll(bms[k]);
+    }
+    if (tot) {
+      int base = 0;
+      if (lane == 0) base = atomicAdd(&sm.ired[31], tot);
+      base = __builtin_amdgcn_readfirstlane(base);
+#pragma unroll
+      for (int k = 0; k < PT; ++k) {
+        const int i = tid + k * NT;
+        const int off = base + __popcll(bms[k] & ((1ull << lane) - 1ull));
+        if (((bms[k] >> lane) & 1ull) && off < kFastCap)
+          sm.keys[off] = ((uint64_t)__builtin_bit_cast(uint32_t, v[k]) << 32) | (uint32_t)i;
+        base += __popcll(bms[k]);
       }
     }
   }
@@ -1782,6 +1793,7 @@ __device__ __attribute__((always_inline)) void advance_prep(const float* raw, co
   // crude bound, so |S - E| <= B = sum_i 2^(floor(log2(P_i (1 + eps0))) - 24) (the f32 half-ulp at
   // that binade, >= 2^-150); B is typically ~5x below n 2^-23 E. Threads take contiguous chunks of
   // p; the index list region (unused on this path) holds the f64 partials.
+  STAMP(14);
   double E = sm.dscan[0];
 #pragma unroll
   for (int w = 1; w < NW; ++w) E += sm.dscan[w];
