@@ -1282,7 +1282,9 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
     __syncthreads();
     if (sy.rkv_gran) {
     } else if (c0 < 3 * sy.C) {
-      if (threadIdx.x == 0)
+      // (test hook as in sync_arrive: the first workgroup to find *drop set skips its arrival)
+      if (threadIdx.x == 0 &&
+          !(sy.drop && __hip_atomic_exchange((gint_t*)sy.drop, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0))
         __hip_atomic_fetch_add((gint_t*)(sy.cnt + kSyncStride * (kAttHead + ((c0 % sy.C) >> 6))), 1,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else if (threadIdx.x < kLnReplicas) {

@@ -73,6 +73,29 @@ def test_engine_recovers_after_a_timed_out_handoff(mid):
         rt.close()
 
 
+def test_one_row_form_recovers_after_a_timed_out_handoff():
+    """The same at one decode row (the row-fused form with the granule hand-offs, 0.4B widths):
+    the dropped rkv arrival times out a WKV workgroup, the request fails, and the next one -- after
+    the counters and granule buffers are reset -- is token-exact vs the engine without the hook."""
+    blob = W.synth_blob(W.DIMS_04B, seed=13)
+    req = make_request(synth_text(77), seed=77, fixed=6)
+    ref_rt = rwkvtts.SharedRwkvRuntime(blob, device=0, max_slots=2, token_chunk_size=512, use_graphs=True)
+    try:
+        ref = ref_rt.generate_batch([req])
+    finally:
+        ref_rt.close()
+    with _env(RWKVTTS_TEST_DROP_ARRIVE=1):
+        rt = rwkvtts.SharedRwkvRuntime(blob, device=0, max_slots=2, token_chunk_size=512, use_graphs=True)
+    try:
+        with pytest.raises(rwkvtts._ffi.RwkvTtsError) as ei:
+            rt.generate_batch([req])
+        assert ei.value.code == rwkvtts._ffi.EHIP, ei.value
+        assert rt.generate_batch([req]) == ref
+        assert rt.generate_batch([req]) == ref
+    finally:
+        rt.close()
+
+
 def test_manager_fails_the_unit_and_keeps_serving(mid):
     """Through the manager: the requests of the failed unit resolve with EHIP, every other ticket
     resolves, the engine is not marked dead, and later requests are token-exact."""
