@@ -117,10 +117,14 @@ __device__ inline void glds16(const void* g, void* l) {
 // runs this decoder in fp32 on ORT) are staged as hi + lo planes too, and every product takes a
 // third MFMA x_hi * w_lo: weights enter at ~2^-16 relative, as the activations do. With w_lo = 0
 // the third MFMA adds exact zeros, so a WLO launch on bf16-exact weights is bit-identical.
-template <int TN, int KT, bool WLO = false, int NWV = conv_waves(KT), bool FUSE = false>
-__global__ __launch_bounds__(64 * NWV, NWV == 8 ? 1 : 2) void k_conv(ConvArgs a) {
+// SB (single-buffered, two workgroups per CU): one chunk buffer per workgroup and the epilogue
+// staged in two 16-row passes, so two workgroups share a CU (2 x 64-70 KB of LDS, <= 128 VGPRs) and
+// one's chunk fills, MFMAs and epilogue overlap the other's instead of a double buffer within one.
+template <int TN, int KT, bool WLO = false, int NWV = conv_waves(KT), bool FUSE = false, bool SB = false>
+__global__ __launch_bounds__(64 * NWV, (NWV == 8 && !SB) ? 1 : 2) void k_conv(ConvArgs a) {
   constexpr int TM = 32 * NWV, NT = TN / 16;
   static_assert(!FUSE || (TN == 96 && !WLO), "fused residual unit: 96 channels, bf16-exact weights");
+  static_assert(!SB || (!FUSE && TN != 96), "single-buffered tiles: plain convs, no early residual loads");
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int req = blockIdx.z;
   const int Tin = a.ntok[req] * a.tin_mul;
@@ -211,11 +215,7 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? 1 : 2) void k_conv(ConvArgs a)
 #pragma unroll
     for (int n = 0; n < NT; ++n) acc[m][n] = (float4_){0.f, 0.f, 0.f, 0.f};
 
-  issue(0, lds);
-  for (int ck = 0; ck < nck; ++ck) {
-    __syncthreads();  // chunk ck has landed; every wave is done with the other buffer
-    uint8_t* cur = lds + (ck & 1) * buf_bytes;
-    if (ck + 1 < nck) issue(ck + 1, lds + ((ck + 1) & 1) * buf_bytes);
+  auto mma_chunk = [&](const uint8_t* cur) {
     const uint8_t* sA = cur;
     const uint8_t* sW = cur + nAblk * 1024;
     const uint8_t* sWl = sW + nWblk * 1024;
@@ -245,6 +245,22 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? 1 : 2) void k_conv(ConvArgs a)
                                                                 __builtin_bit_cast(cbf16x8, bwl[n]), acc[m][n], 0, 0, 0);
         }
       }
+    }
+  };
+  if constexpr (SB) {
+    for (int ck = 0; ck < nck; ++ck) {
+      if (ck) __syncthreads();  // every wave is done with chunk ck - 1
+      issue(ck, lds);
+      __syncthreads();          // chunk ck has landed
+      mma_chunk(lds);
+    }
+  } else {
+    issue(0, lds);
+    for (int ck = 0; ck < nck; ++ck) {
+      __syncthreads();  // chunk ck has landed; every wave is done with the other buffer
+      uint8_t* cur = lds + (ck & 1) * buf_bytes;
+      if (ck + 1 < nck) issue(ck + 1, lds + ((ck + 1) & 1) * buf_bytes);
+      mma_chunk(cur);
     }
   }
   if constexpr (FUSE) {
@@ -344,25 +360,44 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? 1 : 2) void k_conv(ConvArgs a)
   }
   __syncthreads();  // every wave is done with the chunk buffers
   constexpr int LDE = TN + 4;
-  float* sE = (float*)lds + wave * 32 * LDE;
+  constexpr int NH = SB ? 2 : 1, RH = 32 / NH;  // epilogue passes, rows per pass
+  float* sE = (float*)lds + wave * RH * LDE;
+  // When 64 is a multiple of TN / 4 (TN 32, 64) every readback iteration of a lane covers the same
+  // four channels: their Snake alphas and 1 / (alpha + 1e-9) are taken once (the stores below may
+  // alias y_alpha as far as the compiler knows, so it would reload and divide per element). The
+  // planes' hi / lo split is the hardware RNE convert (split2: the bits of f32_to_bf16).
+  constexpr bool kC4Inv = (64 % (TN / 4)) == 0;
+  float ya[4] = {0.f, 0.f, 0.f, 0.f}, yi[4] = {0.f, 0.f, 0.f, 0.f};
+  if (kC4Inv && a.y_alpha) {
+    const int c4 = (lane % (TN / 4)) * 4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      ya[e] = a.y_alpha[co0 + c4 + e];
+      yi[e] = 1.0f / (ya[e] + 1e-9f);
+    }
+  }
+#pragma unroll
+  for (int hh = 0; hh < NH; ++hh) {
 #pragma unroll
   for (int n = 0; n < NT; ++n) {
     const int co = co0 + n * 16 + li;
     const float b = (FUSE ? a.bias1 : a.bias)[co] + (a.rbias ? a.rbias[req * a.rb_bs + co] : 0.0f);
     const float gm = a.gamma ? a.gamma[co] : 1.0f;
 #pragma unroll
-    for (int m = 0; m < 2; ++m)
+    for (int m = 0; m < 2; ++m) {
+      if (NH == 2 && m != hh) continue;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         float v = acc[m][n][j] + b;
         if (a.act == 1) v = 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
-        sE[(m * 16 + 4 * g + j) * LDE + n * 16 + li] = v * gm;
+        sE[((NH == 2 ? 0 : m * 16) + 4 * g + j) * LDE + n * 16 + li] = v * gm;
       }
+    }
   }
 #pragma unroll
-  for (int it = 0; it < NIT; ++it) {
+  for (int it = 0; it < NIT / NH; ++it) {
     const int idx = lane + 64 * it, r = idx / (TN / 4), c4 = (idx % (TN / 4)) * 4;
-    const int q = q0 + wave * 32 + r;
+    const int q = q0 + wave * 32 + hh * RH + r;
     if (q >= Tin) continue;
     float4_ v = *(const float4_*)(sE + r * LDE + c4);
     const int64_t o = yoff + (int64_t)(q * ostr + phase) * a.Co + co0 + c4;
@@ -373,16 +408,24 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? 1 : 2) void k_conv(ConvArgs a)
     if (a.y) *(float4_*)(a.y + o) = v;
     if (a.yh) {
       const int64_t op = a.y_cs ? yoff + ((co0 + c4) >> 5) * a.y_cs + (int64_t)(q * ostr + phase) * 32 + ((co0 + c4) & 31) : o;
-      uint16_t h[4], l[4];
+      float pv[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float pv = a.y_alpha ? snake_fast(v[e], a.y_alpha[co0 + c4 + e]) : v[e];
-        h[e] = f32_to_bf16(pv);
-        l[e] = f32_to_bf16(pv - bf16_to_f32(h[e]));
+        pv[e] = v[e];
+        if (a.y_alpha) {
+          const float al = kC4Inv ? ya[e] : a.y_alpha[co0 + c4 + e];
+          const float inv = kC4Inv ? yi[e] : 1.0f / (al + 1e-9f);
+          const float s = __sinf(al * v[e]);
+          pv[e] = v[e] + inv * (s * s);
+        }
       }
-      *(uint2*)(a.yh + op) = make_uint2(h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16));
-      *(uint2*)(a.yl + op) = make_uint2(l[0] | ((uint32_t)l[1] << 16), l[2] | ((uint32_t)l[3] << 16));
+      uint32_t h01, l01, h23, l23;
+      split2<false>(pv[0], pv[1], h01, l01);
+      split2<false>(pv[2], pv[3], h23, l23);
+      *(uint2*)(a.yh + op) = make_uint2(h01, h23);
+      *(uint2*)(a.yl + op) = make_uint2(l01, l23);
     }
+  }
   }
 }
 
@@ -659,6 +702,7 @@ class Codec {
     RT_HIP(hipFuncSetAttribute((const void*)k_conv<TN_, KT_, WLO_, NWV_, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     RT_CONV_FUSED(RT_CONV_ATTR_F)
 #undef RT_CONV_ATTR_F
+    RT_HIP(hipFuncSetAttribute((const void*)k_conv<64, 7, false, 8, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024));
     RT_HIP(hipFuncSetAttribute((const void*)k_conv_out, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     // zero page: out-of-range window rows read zeros at channel offsets up to the largest Ci
     RT_HIP(hipMalloc(&zeros, 16384));
@@ -830,7 +874,11 @@ class Codec {
       nwv = bw;
     }
     const int TM = 32 * nwv;
-    const size_t shm = shm_of(TN, nwv);
+    // single-buffered 7-tap tiles, two workgroups per CU (k_conv SB): A/B switch while measured
+    static const bool sb_on = getenv("RWKVTTS_CONV_SB") && atoi(getenv("RWKVTTS_CONV_SB")) != 0;
+    const bool sb = sb_on && KT == 7 && TN == 64 && nwv == 8 && !wlo && mode == 0;
+    const size_t shm = sb ? std::max((size_t)chunk_rows(TN, nwv) * 64, (size_t)nwv * 16 * (TN + 4) * sizeof(float))
+                          : shm_of(TN, nwv);
     RT_CHECK(fits(TN, nwv) && ntaps_max <= 7 && Ci <= 4096, RWKVTTS_EINVAL, "codec conv: tile window too large");
     ConvArgs a{};
     a.xh = x.h; a.xl = x.l; a.x_bs = bs; a.Ci = Ci; a.tin_mul = tin_mul; a.w = w; a.wl = wlb ? wlb + (w - wb) : nullptr; a.K = K; a.Co = Co;
@@ -855,6 +903,10 @@ class Codec {
     pbeg();
     const int nthr = 64 * nwv;
     bool launched = false;
+    if (sb) {
+      k_conv<64, 7, false, 8, false, true><<<grid, nthr, shm, stream>>>(a);
+      launched = true;
+    }
 #define RT_CONV_LAUNCH(TN_, KT_, WLO_, NWV_)                                          \
     if (!launched && TN == TN_ && KT == KT_ && wlo == WLO_ && nwv == NWV_) {          \
       k_conv<TN_, KT_, WLO_, NWV_><<<grid, nthr, shm, stream>>>(a);                   \

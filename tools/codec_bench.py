@@ -18,7 +18,13 @@ d = codec.CODEC_DIMS_FULL
 c = codec.BiCodecDetokenizer(codec.synth_codec_blob(d), d)
 rs = np.random.default_rng(0)
 items = [(rs.integers(0, 4096, 32), rs.integers(0, 8192, T)) for _ in range(B)]
-c.decode_audio_batch(items)
+pcm = c.decode_audio_batch(items)
+if os.environ.get("CODEC_DIGEST"):
+    import hashlib
+    h = hashlib.sha256()
+    for x in pcm:
+        h.update(np.ascontiguousarray(x, dtype=np.float32).tobytes())
+    print("pcm digest", h.hexdigest()[:16])
 t0 = time.perf_counter()
 for _ in range(3):
     c.decode_audio_batch(items)
