@@ -215,13 +215,11 @@ __global__ __launch_bounds__(64 * NWV, (NWV == 8 && !SB) ? 1 : 2) void k_conv(Co
 #pragma unroll
     for (int n = 0; n < NT; ++n) acc[m][n] = (float4_){0.f, 0.f, 0.f, 0.f};
 
-  auto mma_chunk = [&](const uint8_t* cur) {
+  auto mma_tap = [&](const uint8_t* cur, int j) {
     const uint8_t* sA = cur;
     const uint8_t* sW = cur + nAblk * 1024;
     const uint8_t* sWl = sW + nWblk * 1024;
-#pragma unroll
-    for (int j = 0; j < KT; ++j) {
-      if (j >= ntaps) break;
+    {
       short8 bw[NT], bwl[WLO ? NT : 1];
 #pragma unroll
       for (int n = 0; n < NT; ++n) bw[n] = *(const short8*)(sW + j * TN * 64 + swz(n * 16 + li, g));
@@ -245,6 +243,15 @@ __global__ __launch_bounds__(64 * NWV, (NWV == 8 && !SB) ? 1 : 2) void k_conv(Co
                                                                 __builtin_bit_cast(cbf16x8, bwl[n]), acc[m][n], 0, 0, 0);
         }
       }
+    }
+  };
+  // (a hand-pipelined form -- tap j + 1's fragments requested before tap j's MFMAs, two register
+  // sets, scheduling barriers -- measured 1-3 % slower per 7-tap launch: not the bound)
+  auto mma_chunk = [&](const uint8_t* cur) {
+#pragma unroll
+    for (int j = 0; j < KT; ++j) {
+      if (j >= ntaps) break;
+      mma_tap(cur, j);
     }
   };
   if constexpr (SB) {
@@ -362,18 +369,21 @@ __global__ __launch_bounds__(64 * NWV, (NWV == 8 && !SB) ? 1 : 2) void k_conv(Co
   constexpr int LDE = TN + 4;
   constexpr int NH = SB ? 2 : 1, RH = 32 / NH;  // epilogue passes, rows per pass
   float* sE = (float*)lds + wave * RH * LDE;
-  // When 64 is a multiple of TN / 4 (TN 32, 64) every readback iteration of a lane covers the same
-  // four channels: their Snake alphas and 1 / (alpha + 1e-9) are taken once (the stores below may
-  // alias y_alpha as far as the compiler knows, so it would reload and divide per element). The
-  // planes' hi / lo split is the hardware RNE convert (split2: the bits of f32_to_bf16).
-  constexpr bool kC4Inv = (64 % (TN / 4)) == 0;
-  float ya[4] = {0.f, 0.f, 0.f, 0.f}, yi[4] = {0.f, 0.f, 0.f, 0.f};
-  if (kC4Inv && a.y_alpha) {
-    const int c4 = (lane % (TN / 4)) * 4;
+  // A lane's readback channels repeat with period kCP over the iterations (1 for TN 32 / 64, 3 for
+  // TN 48 / 96 / 192): their Snake alphas and 1 / (alpha + 1e-9) are taken once (the stores below
+  // may alias y_alpha as far as the compiler knows, so it would reload and divide per element).
+  // The planes' hi / lo split is the hardware RNE convert (split2: the bits of f32_to_bf16).
+  constexpr int kGcd = (TN / 4) % 16 == 0 ? 16 : ((TN / 4) % 8 == 0 ? 8 : 4);  // gcd(64, TN / 4)
+  constexpr int kCP = (TN / 4) / kGcd;
+  static_assert(kCP <= 3 && NIT % kCP == 0, "readback channel period");
+  float ya[kCP][4], yi[kCP][4];
+#pragma unroll
+  for (int p = 0; p < kCP; ++p) {
+    const int c4 = ((lane + 64 * p) % (TN / 4)) * 4;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      ya[e] = a.y_alpha[co0 + c4 + e];
-      yi[e] = 1.0f / (ya[e] + 1e-9f);
+      ya[p][e] = a.y_alpha ? a.y_alpha[co0 + c4 + e] : 0.f;
+      yi[p][e] = 1.0f / (ya[p][e] + 1e-9f);
     }
   }
 #pragma unroll
@@ -413,8 +423,7 @@ __global__ __launch_bounds__(64 * NWV, (NWV == 8 && !SB) ? 1 : 2) void k_conv(Co
       for (int e = 0; e < 4; ++e) {
         pv[e] = v[e];
         if (a.y_alpha) {
-          const float al = kC4Inv ? ya[e] : a.y_alpha[co0 + c4 + e];
-          const float inv = kC4Inv ? yi[e] : 1.0f / (al + 1e-9f);
+          const float al = ya[it % kCP][e], inv = yi[it % kCP][e];
           const float s = __sinf(al * v[e]);
           pv[e] = v[e] + inv * (s * s);
         }
