@@ -288,20 +288,32 @@ __global__ __launch_bounds__(64 * NWV, (NWV == 8 && !SB) ? 1 : 2) void k_conv(Co
         for (int j = 0; j < 4; ++j) sE0[(m * 16 + 4 * g + j) * LDE0 + n * 16 + li] = acc[m][n][j] + b;
     }
     constexpr int NIT0 = TN / 8;
+    // a lane's channels repeat with period 3 over the iterations (TN = 96): alphas and reciprocals
+    // taken once; hi / lo by the hardware RNE convert (the bits of f32_to_bf16)
+    float ma[3][4], mi[3][4];
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        ma[p][e] = a.mid_alpha[co0 + ((lane + 64 * p) % (TN / 4)) * 4 + e];
+        mi[p][e] = 1.0f / (ma[p][e] + 1e-9f);
+      }
     uint2 ph[NIT0], pl[NIT0];
 #pragma unroll
     for (int it = 0; it < NIT0; ++it) {
       const int idx = lane + 64 * it, r = idx / (TN / 4), c4 = (idx % (TN / 4)) * 4;
       const float4_ v = *(const float4_*)(sE0 + r * LDE0 + c4);
-      uint16_t h[4], l[4];
+      float pv[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float pv = snake_fast(v[e], a.mid_alpha[co0 + c4 + e]);
-        h[e] = f32_to_bf16(pv);
-        l[e] = f32_to_bf16(pv - bf16_to_f32(h[e]));
+        const float s = __sinf(ma[it % 3][e] * v[e]);
+        pv[e] = v[e] + mi[it % 3][e] * (s * s);
       }
-      ph[it] = make_uint2(h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16));
-      pl[it] = make_uint2(l[0] | ((uint32_t)l[1] << 16), l[2] | ((uint32_t)l[3] << 16));
+      uint32_t h01, l01, h23, l23;
+      split2<false>(pv[0], pv[1], h01, l01);
+      split2<false>(pv[2], pv[3], h23, l23);
+      ph[it] = make_uint2(h01, h23);
+      pl[it] = make_uint2(l01, l23);
     }
     __syncthreads();  // every wave has read its sE0 tile: the image may overwrite it
     uint8_t* img = lds;                              // [NCH][2 planes][TM rows][64 B]
