@@ -5,6 +5,8 @@
 //   mode 1: global_load_dwordx4 into VGPRs, ds_write_b128, barrier per chunk
 //   mode 2: LDS-DMA, every chunk issued up front, one wait (raw DMA throughput)
 //   mode 3: VGPR loads, every chunk issued up front (raw load throughput)
+//   mode 4: mode 0 + k_conv's per-chunk MFMA work (7 taps x 2 x 4 x hi/lo, fragments from LDS)
+//   mode 5: the MFMA work alone (no staging: every chunk computes on buffer 0)
 // Build: hipcc --offload-arch=gfx950 -O3 -o tools/experiments/stage_bench.bin tools/experiments/stage_bench.hip
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -102,6 +104,49 @@ __global__ __launch_bounds__(512, 1) void k_stage(Args a) {
     }
   };
   float acc = 0.f;
+  typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+  typedef short sh8 __attribute__((ext_vector_type(8)));
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  f4 macc[2][4];
+  for (int m = 0; m < 2; ++m)
+    for (int n = 0; n < 4; ++n) macc[m][n] = (f4){0.f, 0.f, 0.f, 0.f};
+  const int li = lane & 15, g = lane >> 4;
+  auto compute = [&](const uint8_t* cur) {
+    const uint8_t* sW = cur + nAblk * 1024;
+#pragma unroll
+    for (int j = 0; j < 7; ++j) {
+      sh8 bw[4];
+#pragma unroll
+      for (int n = 0; n < 4; ++n) bw[n] = *(const sh8*)(sW + j * TN * 64 + swz(n * 16 + li, g));
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        const int wr = wave * 32 + m * 16 + li + j;
+        const sh8 ah = *(const sh8*)(cur + swz(wr, g));
+        const sh8 al = *(const sh8*)(cur + WRp * 64 + swz(wr, g));
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+          macc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf8, ah), __builtin_bit_cast(bf8, bw[n]), macc[m][n], 0, 0, 0);
+          macc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf8, al), __builtin_bit_cast(bf8, bw[n]), macc[m][n], 0, 0, 0);
+        }
+      }
+    }
+  };
+  if (MODE == 4) {
+    issue_dma(0, lds);
+    for (int ck = 0; ck < a.nck; ++ck) {
+      __syncthreads();
+      const uint8_t* cur = lds + (ck & 1) * buf_bytes;
+      if (ck + 1 < a.nck) issue_dma(ck + 1, lds + ((ck + 1) & 1) * buf_bytes);
+      compute(cur);
+    }
+  } else if (MODE == 5) {
+    for (int ck = 0; ck < a.nck; ++ck) {
+      __syncthreads();
+      compute(lds);
+    }
+  }
+  for (int m = 0; m < 2; ++m)
+    for (int n = 0; n < 4; ++n) acc += macc[m][n][0] + macc[m][n][3];
   if (MODE == 0) {
     issue_dma(0, lds);
     for (int ck = 0; ck < a.nck; ++ck) {
@@ -124,7 +169,7 @@ __global__ __launch_bounds__(512, 1) void k_stage(Args a) {
     for (int ck = 0; ck < a.nck; ++ck) issue_dma(ck, lds + (ck & 1) * buf_bytes);
     __syncthreads();
     acc += *(const float*)(lds + swz(tid & 255, lane & 3));
-  } else {
+  } else if (MODE == 3) {
     for (int ck = 0; ck < a.nck; ++ck) {
       u32x4 r[MAXB];
       load_regs(ck, r);
@@ -158,9 +203,10 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  void (*kern[4])(Args) = {k_stage<0>, k_stage<1>, k_stage<2>, k_stage<3>};
-  const char* names[4] = {"dma double-buffered", "vgpr double-buffered", "dma all-up-front", "vgpr loads only"};
-  for (int m = 0; m < 4; ++m) {
+  void (*kern[6])(Args) = {k_stage<0>, k_stage<1>, k_stage<2>, k_stage<3>, k_stage<4>, k_stage<5>};
+  const char* names[6] = {"dma double-buffered", "vgpr double-buffered", "dma all-up-front", "vgpr loads only",
+                          "dma + mfma", "mfma only"};
+  for (int m = 0; m < 6; ++m) {
     CK(hipFuncSetAttribute((const void*)kern[m], hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes));
     for (int rep = 0; rep < 2; ++rep) hipLaunchKernelGGL(kern[m], dim3(grid), dim3(512), lds_bytes, 0, a);
     CK(hipDeviceSynchronize());
