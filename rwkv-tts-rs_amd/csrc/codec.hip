@@ -557,12 +557,14 @@ __global__ __launch_bounds__(128) void k_dw_ln(const float* x, float* y, bf16_t*
   }
 }
 
-// final conv7 (C -> 1) over the snake-activated planes -> tanh. 256 samples per workgroup of 256
-// threads: the input window (262 rows) is staged once into LDS as f32 (hi + lo) with 16-byte
-// global loads (8 channels per load and plane; C % 8 == 0) at row stride C + 1 (conflict-free
-// walks); each thread then walks its 7 x C window against the weights (scalar operands).
-constexpr int kOutT = 256;
-__global__ __launch_bounds__(256) void k_conv_out(const bf16_t* xh, const bf16_t* xl, int64_t x_bs, int64_t x_cs,
+// final conv7 (C -> 1) over the snake-activated planes -> tanh. kOutT samples per workgroup of
+// kOutT threads: the input window (kOutT + 6 rows) is staged once into LDS as f32 (hi + lo) with
+// 16-byte global loads (8 channels per load and plane; C % 8 == 0) at row stride C + 1
+// (conflict-free walks); each thread then walks its 7 x C window against the weights (scalar
+// operands). 128 samples: 52 KB of LDS at 96 channels, three workgroups per CU (256 samples took
+// 101 KB, one per CU, and the walks of one workgroup left the CU's memory path idle).
+constexpr int kOutT = 128;
+__global__ __launch_bounds__(kOutT) void k_conv_out(const bf16_t* xh, const bf16_t* xl, int64_t x_bs, int64_t x_cs,
                                                   int C, int tin_mul, const int* ntok, const float* w,
                                                   const float* b, float* pcm, int64_t p_bs) {
   extern __shared__ float s_x[];
@@ -574,11 +576,11 @@ __global__ __launch_bounds__(256) void k_conv_out(const bf16_t* xh, const bf16_t
   // first conversion, so the window's memory latency is paid once per batch, not once per piece
   constexpr int kBatch = 8;
   const int total = rows * c8n;
-  for (int i0 = threadIdx.x; i0 < total; i0 += 256 * kBatch) {
+  for (int i0 = threadIdx.x; i0 < total; i0 += kOutT * kBatch) {
     uint4 h[kBatch], l[kBatch];
 #pragma unroll
     for (int j = 0; j < kBatch; ++j) {
-      const int i = i0 + 256 * j;
+      const int i = i0 + kOutT * j;
       const int r = i / c8n, c8 = (i - r * c8n) * 8, p = t0 - 3 + r;
       h[j] = l[j] = make_uint4(0u, 0u, 0u, 0u);
       if (i < total && p >= 0 && p < T) {
@@ -589,7 +591,7 @@ __global__ __launch_bounds__(256) void k_conv_out(const bf16_t* xh, const bf16_t
     }
 #pragma unroll
     for (int j = 0; j < kBatch; ++j) {
-      const int i = i0 + 256 * j;
+      const int i = i0 + kOutT * j;
       if (i >= total) break;
       const int r = i / c8n, c8 = (i - r * c8n) * 8;
       float* dst = s_x + r * LDX + c8;
@@ -1172,7 +1174,7 @@ class Codec {
     }
     pbeg();
     const size_t shm = (size_t)(kOutT + 6) * (C + 1) * sizeof(float);
-    k_conv_out<<<dim3((unsigned)((Tmax * (int64_t)mul + kOutT - 1) / kOutT), n), 256, shm, stream>>>(
+    k_conv_out<<<dim3((unsigned)((Tmax * (int64_t)mul + kOutT - 1) / kOutT), n), kOutT, shm, stream>>>(
         pp[cur].h, pp[cur].l, bs, PB(cur, mul).cs, C, mul, d_ntok, F(0, 0, CD_COUT_W), F(0, 0, CD_COUT_B), pcm,
         (int64_t)Tmax * RWKVTTS_HOP);
     RT_HIP(hipGetLastError());
