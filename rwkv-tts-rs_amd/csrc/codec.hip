@@ -496,6 +496,27 @@ __global__ __launch_bounds__(256) void k_gemv(const float* w, const float* b, in
   if (lane == 0) out[req * o_bs + r] = acc + b[r];
 }
 
+// the AdaLN scale / shift projections of every prenet layer in one launch (blockIdx.z = job; each
+// job is k_gemv's arithmetic on its own weights and output)
+constexpr int kMaxGemvJobs = 32;
+struct GemvJobs {
+  const float* w[kMaxGemvJobs];
+  const float* b[kMaxGemvJobs];
+  float* out[kMaxGemvJobs];
+};
+__global__ __launch_bounds__(256) void k_gemv_jobs(GemvJobs jb, int rows, int cols, const float* v, int64_t v_bs,
+                                                   int64_t o_bs) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63, req = blockIdx.y, job = blockIdx.z;
+  if (r >= rows) return;
+  const float* wr = jb.w[job] + (int64_t)r * cols;
+  const float* vr = v + req * v_bs;
+  float acc = 0.0f;
+  for (int i = lane; i < cols; i += 64) acc += wr[i] * vr[i];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  if (lane == 0) jb.out[job][req * o_bs + r] = acc + jb.b[job][r];
+}
+
 // [optional depthwise conv k7 pad 3] -> LayerNorm (eps 1e-6) -> * scale + shift
 // scale/shift: [n][P] (AdaLN, stride P) or [P] (plain LN affine, stride 0).
 // Output: f32 y (nullable) and/or planes yh/yl (nullable).
@@ -1038,13 +1059,23 @@ class Codec {
     k_fsq<<<n, 256, 0, stream>>>(d_glob, G, d.fsq_levels, d.fsq_dims, F(0, 0, CD_FSQ_W), F(0, 0, CD_FSQ_B), Q, hs);
     k_gemv<<<dim3((S + 3) / 4, n), 256, 0, stream>>>(F(0, 0, CD_SPK_W), F(0, 0, CD_SPK_B), S, Q * G, hs,
                                                      (int64_t)Q * G, dvec, S);
-    for (int l = -1; l < d.prenet_layers; ++l) {
-      const float* sw = l < 0 ? F(0, 0, CD_N0_SW) : F(1, l, CB_SW);
-      const float* sb = l < 0 ? F(0, 0, CD_N0_SB) : F(1, l, CB_SB);
-      const float* hw = l < 0 ? F(0, 0, CD_N0_HW) : F(1, l, CB_HW);
-      const float* hb = l < 0 ? F(0, 0, CD_N0_HB) : F(1, l, CB_HB);
-      k_gemv<<<dim3((P + 3) / 4, n), 256, 0, stream>>>(sw, sb, P, S, dvec, S, cond + 2 * (l + 1) * P, cstr);
-      k_gemv<<<dim3((P + 3) / 4, n), 256, 0, stream>>>(hw, hb, P, S, dvec, S, cond + (2 * (l + 1) + 1) * P, cstr);
+    {
+      GemvJobs jb{};
+      int nj = 0;
+      auto flush = [&]() {
+        if (nj) k_gemv_jobs<<<dim3((P + 3) / 4, n, nj), 256, 0, stream>>>(jb, P, S, dvec, S, cstr);
+        nj = 0;
+      };
+      for (int l = -1; l < d.prenet_layers; ++l) {
+        if (nj + 2 > kMaxGemvJobs) flush();
+        jb.w[nj] = l < 0 ? F(0, 0, CD_N0_SW) : F(1, l, CB_SW);
+        jb.b[nj] = l < 0 ? F(0, 0, CD_N0_SB) : F(1, l, CB_SB);
+        jb.out[nj++] = cond + 2 * (l + 1) * P;
+        jb.w[nj] = l < 0 ? F(0, 0, CD_N0_HW) : F(1, l, CB_HW);
+        jb.b[nj] = l < 0 ? F(0, 0, CD_N0_HB) : F(1, l, CB_HB);
+        jb.out[nj++] = cond + (2 * (l + 1) + 1) * P;
+      }
+      flush();
     }
     k_fvq<<<dim3(Tmax, n), 256, 0, stream>>>(d_tok, Tmax, d_ntok, F(0, 0, CD_CODEBOOK), d.codebook_dim,
                                             F(0, 0, CD_OUTP_W), F(0, 0, CD_OUTP_B), L, zp.h, zp.l);
