@@ -162,7 +162,20 @@ typedef struct {
    * (the LoRA matrices, embedding and head stay 16-bit). RWKVTTS_QUANT_NONE when 0 layers. */
   int32_t quant_layers;
   int32_t quant_type;       /* RWKVTTS_QUANT_* */
+  /* Decode-step forms. 0 (the default) = the shipping forms. Each RWKVTTS_FORM_* bit switches one
+   * fused form back to the launches it replaces; tokens and the recurrent state are bitwise equal
+   * either way (tests/test_gpu_ffn_persist.py, test_gpu_emb_fusion.py). For verification and A/B
+   * timing: no bit makes the engine faster. No reference counterpart (web-rwkv has one form). */
+  uint32_t forms;
 } rwkvtts_engine_desc;
+
+#define RWKVTTS_FORM_SEPARATE_ATT 1u   /* attention half: LN1 / rkv / WKV / Wo launches, not k_att_persist */
+#define RWKVTTS_FORM_SEPARATE_FFN 2u   /* FFN half: LN2 / key / value launches, not k_ffn_persist */
+#define RWKVTTS_FORM_LN_ROWS 4u        /* one-row steps: LayerNorm workgroups, not the row-fused LayerNorm */
+#define RWKVTTS_FORM_SLAB_HANDOFF 8u   /* one-row steps: partial slabs + counters, not data-tagged granules */
+#define RWKVTTS_FORM_SEPARATE_LNOUT 16u /* one-row steps: ln_out launch, not folded into the head GEMM */
+#define RWKVTTS_FORM_SEPARATE_EMBED 32u /* decode steps: k_embed launch, not folded into layer 0's LayerNorm */
+#define RWKVTTS_FORM_EXACT_SAMPLER 64u /* k_advance: always the exact sequential-sum walk (no certificate) */
 
 #define RWKVTTS_QUANT_NONE 0
 #define RWKVTTS_QUANT_INT8 1 /* 128-element blocks along K: f16 (min, max), u8 q; w = min + q (max - min)/255 */
@@ -393,6 +406,16 @@ int64_t rwkvtts_codec_blob_bytes(const rwkvtts_codec_dims* d);
 int rwkvtts_codec_synth_weights(const rwkvtts_codec_dims* d, uint64_t seed, float* out);
 int rwkvtts_codec_create(int device, const rwkvtts_codec_dims* d, const float* weights,
                          rwkvtts_codec** out);
+/* As rwkvtts_codec_create with the conv weight path chosen by the caller:
+ * RWKVTTS_CODEC_WEIGHTS_AUTO (what rwkvtts_codec_create does): the weight hi + lo planes (three
+ * MFMAs per product) iff some conv weight is not bf16-exact, so f32 checkpoints keep ~2^-16
+ * relative weights; _BF16: bf16 weights (two MFMAs; faster, the weights rounded to bf16);
+ * _HILO: hi + lo planes always (on bf16-exact weights bitwise the _BF16 PCM, tested). */
+#define RWKVTTS_CODEC_WEIGHTS_AUTO 0
+#define RWKVTTS_CODEC_WEIGHTS_BF16 1
+#define RWKVTTS_CODEC_WEIGHTS_HILO 2
+int rwkvtts_codec_create_ex(int device, const rwkvtts_codec_dims* d, const float* weights, int weight_path,
+                            rwkvtts_codec** out);
 int rwkvtts_codec_destroy(rwkvtts_codec* c);
 /* semantic [T] i64, global [n_global] i64 -> pcm [T * 320] f32 (output "wav_rec"). */
 int rwkvtts_codec_decode(rwkvtts_codec* c, const int64_t* semantic, int T, const int64_t* global,
@@ -400,6 +423,11 @@ int rwkvtts_codec_decode(rwkvtts_codec* c, const int64_t* semantic, int T, const
 /* decode_audio_batch (lightweight_tts_pipeline.rs:625-703): n utterances in one pass. */
 int rwkvtts_codec_decode_batch(rwkvtts_codec* c, const int64_t* const* semantic, const int* T,
                                const int64_t* const* global, int n, float* const* pcm);
+/* Verification forms of later decode calls (0 = shipping); the PCM is bitwise equal either way
+ * (tests/test_gpu_codec.py). No reference counterpart (ORT runs one graph). */
+#define RWKVTTS_CODEC_FORM_SEPARATE_RESUNIT 1u /* 96-channel residual units as conv7 + conv1 launches */
+#define RWKVTTS_CODEC_FORM_CHANNEL_LAST 2u     /* WaveGenerator planes [t][c] instead of [c / 32][t][32] */
+int rwkvtts_codec_set_forms(rwkvtts_codec* c, uint32_t forms);
 /* Per-stage HIP-event timing of later decode calls (profiling on): name, launches, total ms. */
 int rwkvtts_codec_set_profiling(rwkvtts_codec* c, int on);
 int rwkvtts_codec_profile_count(rwkvtts_codec* c);

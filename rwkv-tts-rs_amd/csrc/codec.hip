@@ -117,14 +117,12 @@ __device__ inline void glds16(const void* g, void* l) {
 // runs this decoder in fp32 on ORT) are staged as hi + lo planes too, and every product takes a
 // third MFMA x_hi * w_lo: weights enter at ~2^-16 relative, as the activations do. With w_lo = 0
 // the third MFMA adds exact zeros, so a WLO launch on bf16-exact weights is bit-identical.
-// SB (single-buffered, two workgroups per CU): one chunk buffer per workgroup and the epilogue
-// staged in two 16-row passes, so two workgroups share a CU (2 x 64-70 KB of LDS, <= 128 VGPRs) and
-// one's chunk fills, MFMAs and epilogue overlap the other's instead of a double buffer within one.
-template <int TN, int KT, bool WLO = false, int NWV = conv_waves(KT), bool FUSE = false, bool SB = false>
-__global__ __launch_bounds__(64 * NWV, (NWV == 8 && !SB) ? 1 : 2) void k_conv(ConvArgs a) {
+// (A single-buffered variant at two workgroups per CU measured the vocoder alone 2 ms faster but
+// left no LDS for a decode workgroup beside it, and the bench equal or lower: DESIGN.md §14.)
+template <int TN, int KT, bool WLO = false, int NWV = conv_waves(KT), bool FUSE = false>
+__global__ __launch_bounds__(64 * NWV, NWV == 8 ? 1 : 2) void k_conv(ConvArgs a) {
   constexpr int TM = 32 * NWV, NT = TN / 16;
   static_assert(!FUSE || (TN == 96 && !WLO), "fused residual unit: 96 channels, bf16-exact weights");
-  static_assert(!SB || (!FUSE && TN != 96), "single-buffered tiles: plain convs, no early residual loads");
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int req = blockIdx.z;
   const int Tin = a.ntok[req] * a.tin_mul;
@@ -254,21 +252,12 @@ __global__ __launch_bounds__(64 * NWV, (NWV == 8 && !SB) ? 1 : 2) void k_conv(Co
       mma_tap(cur, j);
     }
   };
-  if constexpr (SB) {
-    for (int ck = 0; ck < nck; ++ck) {
-      if (ck) __syncthreads();  // every wave is done with chunk ck - 1
-      issue(ck, lds);
-      __syncthreads();          // chunk ck has landed
-      mma_chunk(lds);
-    }
-  } else {
-    issue(0, lds);
-    for (int ck = 0; ck < nck; ++ck) {
-      __syncthreads();  // chunk ck has landed; every wave is done with the other buffer
-      uint8_t* cur = lds + (ck & 1) * buf_bytes;
-      if (ck + 1 < nck) issue(ck + 1, lds + ((ck + 1) & 1) * buf_bytes);
-      mma_chunk(cur);
-    }
+  issue(0, lds);
+  for (int ck = 0; ck < nck; ++ck) {
+    __syncthreads();  // chunk ck has landed; every wave is done with the other buffer
+    uint8_t* cur = lds + (ck & 1) * buf_bytes;
+    if (ck + 1 < nck) issue(ck + 1, lds + ((ck + 1) & 1) * buf_bytes);
+    mma_chunk(cur);
   }
   if constexpr (FUSE) {
     // ---- residual unit, second half: v = conv7 + bias -> Snake(mid_alpha) -> hi + lo planes in an
@@ -379,7 +368,7 @@ __global__ __launch_bounds__(64 * NWV, (NWV == 8 && !SB) ? 1 : 2) void k_conv(Co
   }
   __syncthreads();  // every wave is done with the chunk buffers
   constexpr int LDE = TN + 4;
-  constexpr int NH = SB ? 2 : 1, RH = 32 / NH;  // epilogue passes, rows per pass
+  constexpr int NH = 1, RH = 32 / NH;  // epilogue passes, rows per pass
   float* sE = (float*)lds + wave * RH * LDE;
   // A lane's readback channels repeat with period kCP over the iterations (1 for TN 32 / 64, 3 for
   // TN 48 / 96 / 192): their Snake alphas and 1 / (alpha + 1e-9) are taken once (the stores below
@@ -664,6 +653,7 @@ class Codec {
   bf16_t* wb = nullptr;  // bf16 mirror (same element offsets) for MFMA operands: hi part
   bf16_t* wlb = nullptr; // lo part (f32 - hi), read by the WLO conv kernels
   bool wlo = false;      // some conv weight is not bf16-exact: three MFMAs per product
+  uint32_t forms = 0;    // RWKVTTS_CODEC_FORM_* of later decode calls (rwkvtts_codec_set_forms)
   int cap_n = 0, cap_T = 0;
   int *d_tok = nullptr, *d_glob = nullptr, *d_ntok = nullptr;
   // prenet: x f32 residual stream [n][T][P]; zp/up/hp planes [n][T][L|P|I]
@@ -705,7 +695,7 @@ class Codec {
   const float* F(int g, int i, int t) const { return wf + rwkvtts_codec_offset(&d, g, i, t); }
   const bf16_t* B(int g, int i, int t) const { return wb + rwkvtts_codec_offset(&d, g, i, t); }
 
-  int init(int dev, const rwkvtts_codec_dims& dims, const float* host_w) {
+  int init(int dev, const rwkvtts_codec_dims& dims, const float* host_w, int weight_path) {
     d = dims;
     device = dev;
     RT_CHECK(d.n_up >= 1 && d.n_up <= 4 && d.latent_dim == d.spk_dim && d.prenet_dim <= 512 &&
@@ -722,21 +712,9 @@ class Codec {
     {  // lowest queue priority: the LM decode chain (engine.hip) goes first when both share the GPU
       int least = 0, greatest = 0;
       RT_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
-      if (getenv("RWKVTTS_NO_PRIO")) least = 0;
-      const char* cus = getenv("RWKVTTS_CODEC_CUS");  // experiment: confine the vocoder to N CUs
-      if (cus && atoi(cus) > 0) {
-        hipDeviceProp_t prop;
-        RT_HIP(hipGetDeviceProperties(&prop, device));
-        const int ncu = prop.multiProcessorCount, want = std::min(atoi(cus), ncu);
-        std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
-        for (int i = 0; i < want; ++i) {
-          const int cu = (int)((int64_t)i * ncu / want);
-          mask[cu / 32] |= 1u << (cu % 32);
-        }
-        RT_HIP(hipExtStreamCreateWithCUMask(&stream, (uint32_t)mask.size(), mask.data()));
-      } else {
-        RT_HIP(hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, least));
-      }
+      // (a CU-masked stream confining the vocoder to 32 / 128 CUs measured no gain beside the
+      // decode)
+      RT_HIP(hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, least));
     }
 #define RT_CONV_ATTR(TN_, KT_, WLO_, NWV_) \
     RT_HIP(hipFuncSetAttribute((const void*)k_conv<TN_, KT_, WLO_, NWV_>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -746,7 +724,6 @@ class Codec {
     RT_HIP(hipFuncSetAttribute((const void*)k_conv<TN_, KT_, WLO_, NWV_, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     RT_CONV_FUSED(RT_CONV_ATTR_F)
 #undef RT_CONV_ATTR_F
-    RT_HIP(hipFuncSetAttribute((const void*)k_conv<64, 7, false, 8, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024));
     RT_HIP(hipFuncSetAttribute((const void*)k_conv_out, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     // zero page: out-of-range window rows read zeros at channel offsets up to the largest Ci
     RT_HIP(hipMalloc(&zeros, 16384));
@@ -755,9 +732,11 @@ class Codec {
     RT_HIP(hipMalloc(&wf, n * sizeof(float)));
     RT_HIP(hipMalloc(&wb, n * sizeof(bf16_t)));
     // the MFMA convs take the three-product path when any of their weights is not bf16-exact
-    // (RWKVTTS_CODEC_WLO=0 / 1 forces the choice: A/B timing); the lo plane exists only then
-    wlo = !conv_weights_bf16_exact(host_w);
-    if (const char* e = getenv("RWKVTTS_CODEC_WLO")) wlo = atoi(e) != 0;
+    // (weight_path RWKVTTS_CODEC_WEIGHTS_BF16 / _HILO forces the choice); the lo plane exists only then
+    RT_CHECK(weight_path >= RWKVTTS_CODEC_WEIGHTS_AUTO && weight_path <= RWKVTTS_CODEC_WEIGHTS_HILO, RWKVTTS_EINVAL,
+             "codec: unknown weight_path");
+    wlo = weight_path == RWKVTTS_CODEC_WEIGHTS_AUTO ? !conv_weights_bf16_exact(host_w)
+                                                    : weight_path == RWKVTTS_CODEC_WEIGHTS_HILO;
     if (wlo) RT_HIP(hipMalloc(&wlb, n * sizeof(bf16_t)));
     RT_HIP(hipMemcpy(wf, host_w, n * sizeof(float), hipMemcpyHostToDevice));
     k_f32_split_bf16<<<2048, 256, 0, stream>>>(wf, wb, wlb, n);
@@ -865,8 +844,7 @@ class Codec {
     // pointwise (memory-bound) convs: 96-wide column tiles read the input window fewer times
     // (conv1 @ 192 / 384 / 768: 6.9 / 4.1 / 2.2 -> 5.3 / 3.5 / 2.0 ms per batch with the XCD-aware
     // order below; 192-wide tiles halve the occupancy and are slower)
-    static const int tn1 = getenv("RWKVTTS_CONV1_TN") ? atoi(getenv("RWKVTTS_CONV1_TN")) : 96;  // A/B switch
-    if (K == 1 && tn1 > 0 && Co % tn1 == 0 && (tn1 == 64 || tn1 == 96 || tn1 == 192)) TN = tn1;
+    if (K == 1 && Co % 96 == 0) TN = 96;
     const int ntaps_max = mode == 1 ? (K + s - 1) / s : K;
     const int span = (ntaps_max - 1) * (mode == 1 ? 1 : dil);
     const int KT = ntaps_max <= 1 ? 1 : (ntaps_max <= 3 ? 3 : 7);
@@ -879,19 +857,13 @@ class Codec {
        // samples/s (same-box A/B x2, tools/bench_ab.sh) for +1 ms of vocoder time. Tests
        // bit-identical either way: the per-element accumulation order does not depend on TN.
       // Round 4: the decode step's persistent workgroups (k_att_persist / k_ffn_persist) take
-      // 36.6 KB of LDS, which fits beside a 64-wide tile at dilation 1 only. 48-wide tiles
-      // (RWKVTTS_CONV7_TN=48) leave room at every dilation: bench A/Bs (13 alternating pairs over
-      // three boxes, profiles/r04_conv7_tile_ab.txt) +0.1 to +1.2 % samples/s, within the boxes'
-      // run-to-run spread, for +1.5 ms of vocoder time; 64 stays the default.
-      static const int tn7 = getenv("RWKVTTS_CONV7_TN") ? atoi(getenv("RWKVTTS_CONV7_TN")) : 64;  // A/B switch
-      const int wr = (256 + span + 15) & ~15;
-      if (KT == 7 && mode == 0 && tn7 == 96 && Co % 96 == 0 && 2 * (size_t)(2 * wr + ntaps_max * 96) * 64 <= 160 * 1024)
-        TN = 96;
-      if (KT == 7 && mode == 0 && tn7 == 48 && Co % 48 == 0) TN = 48;
+      // 36.6 KB of LDS, which fits beside a 64-wide tile at dilation 1 only. 48-wide tiles leave
+      // room at every dilation: bench A/Bs (13 alternating pairs over three boxes,
+      // profiles/r04_conv7_tile_ab.txt) +0.1 to +1.2 % samples/s, within the boxes' run-to-run
+      // spread, for +1.5 ms of vocoder time; 64 stays.
       // ConvTranspose: 96-wide tiles measured faster at 96 and 384 output channels (2.54 -> 2.14,
       // 2.30 -> 2.10 ms per batch), slower at 192 (2.51 -> 2.62), equal at 768
-      static const int tnT = getenv("RWKVTTS_CONVT_TN") ? atoi(getenv("RWKVTTS_CONVT_TN")) : -1;  // A/B switch
-      if (mode == 1 && KT == 3 && Co % 96 == 0 && (tnT == 96 || (tnT < 0 && (Co == 96 || Co == 384)))) TN = 96;
+      if (mode == 1 && KT == 3 && (Co == 96 || Co == 384)) TN = 96;
     }
     int nwv = conv_waves(KT);
     const int wplanes = wlo ? 2 : 1;  // weight planes staged per chunk
@@ -918,11 +890,7 @@ class Codec {
       nwv = bw;
     }
     const int TM = 32 * nwv;
-    // single-buffered 7-tap tiles, two workgroups per CU (k_conv SB): A/B switch while measured
-    static const bool sb_on = getenv("RWKVTTS_CONV_SB") && atoi(getenv("RWKVTTS_CONV_SB")) != 0;
-    const bool sb = sb_on && KT == 7 && TN == 64 && nwv == 8 && !wlo && mode == 0;
-    const size_t shm = sb ? std::max((size_t)chunk_rows(TN, nwv) * 64, (size_t)nwv * 16 * (TN + 4) * sizeof(float))
-                          : shm_of(TN, nwv);
+    const size_t shm = shm_of(TN, nwv);
     RT_CHECK(fits(TN, nwv) && ntaps_max <= 7 && Ci <= 4096, RWKVTTS_EINVAL, "codec conv: tile window too large");
     ConvArgs a{};
     a.xh = x.h; a.xl = x.l; a.x_bs = bs; a.Ci = Ci; a.tin_mul = tin_mul; a.w = w; a.wl = wlb ? wlb + (w - wb) : nullptr; a.K = K; a.Co = Co;
@@ -935,10 +903,10 @@ class Codec {
     // XCD-aware order for the long-time-axis residual convs (conv7 and conv1 at >= 32 time tiles:
     // a time tile's column tiles share one L2); the short prenet / conv_in / convT launches keep
     // the default order (2x slower remapped)
-    static const int xm = getenv("RWKVTTS_CODEC_XMAP") ? atoi(getenv("RWKVTTS_CODEC_XMAP")) : 3;
+    // (the ConvTranspose launches in this order too: 1-8 % slower, the Infinity Cache serves their
+    // re-reads)
     a.xmap = 0;
-    if (grid.y > 1 && grid.x >= 32 &&
-        ((mode == 0 && (((xm & 1) && K == 7) || ((xm & 2) && K == 1))) || (mode == 1 && (xm & 4)))) {
+    if (grid.y > 1 && grid.x >= 32 && mode == 0 && (K == 7 || K == 1)) {
       a.xmap = 1;
       a.gx = (int)grid.x;
       a.gy = (int)grid.y;
@@ -947,10 +915,6 @@ class Codec {
     pbeg();
     const int nthr = 64 * nwv;
     bool launched = false;
-    if (sb) {
-      k_conv<64, 7, false, 8, false, true><<<grid, nthr, shm, stream>>>(a);
-      launched = true;
-    }
 #define RT_CONV_LAUNCH(TN_, KT_, WLO_, NWV_)                                          \
     if (!launched && TN == TN_ && KT == KT_ && wlo == WLO_ && nwv == NWV_) {          \
       k_conv<TN_, KT_, WLO_, NWV_><<<grid, nthr, shm, stream>>>(a);                   \
@@ -972,12 +936,10 @@ class Codec {
                     const bf16_t* w7, const float* b7, int dil, const float* mid_alpha, const bf16_t* w1,
                     const float* b1, const ConvOut& o, bool* done) {
     *done = false;
-    const bool off = getenv("RWKVTTS_NO_RESFUSE") != nullptr;  // A/B switch (read per call: tests toggle it)
-    if (off || wlo || C != 96) return RWKVTTS_OK;
+    if ((forms & RWKVTTS_CODEC_FORM_SEPARATE_RESUNIT) || wlo || C != 96) return RWKVTTS_OK;
     const int span = 6 * dil;
     int nwv = 0;
-    static const int nw_pref = getenv("RWKVTTS_RESFUSE_NW") ? atoi(getenv("RWKVTTS_RESFUSE_NW")) : 8;  // A/B switch
-    for (int nw : {nw_pref == 4 ? 4 : 8, 4}) {
+    for (int nw : {8, 4}) {  // (4-wave units where 8 do not fit: 8 measured faster)
       const int wr = (32 * nw + span + 15) & ~15;
       const size_t chunk = 2 * (size_t)(2 * wr + 7 * 96) * 64;
       const size_t fused = (size_t)3 * 2 * 32 * nw * 64 + 3 * 96 * 64;
@@ -1135,10 +1097,9 @@ class Codec {
     }
     // WaveGenerator: conv_in -> [snake -> convT -> 3 x residual unit] x n_up -> snake -> conv_out
     // Its planes are channel-blocked ([C / 32][Tmax * mul][32] per utterance) unless
-    // RWKVTTS_CODEC_BLK=0 (A/B switch, read per call; the arithmetic is the same either way)
+    // RWKVTTS_CODEC_FORM_CHANNEL_LAST (the arithmetic is the same either way)
     const int64_t bs = (int64_t)Tmax * big_per_tok;
-    const char* blk_env = getenv("RWKVTTS_CODEC_BLK");
-    const bool blk = !blk_env || atoi(blk_env) != 0;
+    const bool blk = !(forms & RWKVTTS_CODEC_FORM_CHANNEL_LAST);
     auto PB = [&](int i, int m) {  // pp[i] holding a tensor of Tmax * m rows
       Planes q = pp[i];
       q.cs = blk ? (int64_t)Tmax * m * 32 : 0;
@@ -1319,11 +1280,16 @@ int rwkvtts_codec_synth_weights(const rwkvtts_codec_dims* d, uint64_t seed, floa
 }
 
 int rwkvtts_codec_create(int device, const rwkvtts_codec_dims* d, const float* weights, rwkvtts_codec** out) {
+  return rwkvtts_codec_create_ex(device, d, weights, RWKVTTS_CODEC_WEIGHTS_AUTO, out);
+}
+
+int rwkvtts_codec_create_ex(int device, const rwkvtts_codec_dims* d, const float* weights, int weight_path,
+                            rwkvtts_codec** out) {
   RT_CHECK(d && weights && out, RWKVTTS_EINVAL, "codec_create: null argument");
   *out = nullptr;
   try {
     rwkvtts_codec* c = new rwkvtts_codec();
-    const int rc = c->c.init(device, *d, weights);
+    const int rc = c->c.init(device, *d, weights, weight_path);
     if (rc != RWKVTTS_OK) {
       delete c;
       return rc;
@@ -1355,6 +1321,14 @@ int rwkvtts_codec_decode_batch(rwkvtts_codec* c, const int64_t* const* semantic,
     set_error(ex.what());
     return RWKVTTS_ENOMEM;
   }
+}
+
+int rwkvtts_codec_set_forms(rwkvtts_codec* c, uint32_t forms) {
+  RT_CHECK(c, RWKVTTS_EINVAL, "codec_set_forms: null codec");
+  RT_CHECK((forms & ~(RWKVTTS_CODEC_FORM_SEPARATE_RESUNIT | RWKVTTS_CODEC_FORM_CHANNEL_LAST)) == 0, RWKVTTS_EINVAL,
+           "codec_set_forms: unknown forms bits");
+  c->c.forms = forms;
+  return RWKVTTS_OK;
 }
 
 int rwkvtts_codec_set_profiling(rwkvtts_codec* c, int on) {

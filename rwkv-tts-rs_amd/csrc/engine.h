@@ -148,50 +148,56 @@ class Engine {
   // on the engine's stream and wait for it (the jobs of the failed units have already been failed;
   // their slots are reset at their next admission, slot_reset)
   int reset_persistent();
+  // after a second timed-out hand-off within kDegradeWindow units: the separate launches from now on
+  // (persistent forms off, cached graphs dropped, the device's persistent slot released)
+  int degrade_persistent();
+  static constexpr int64_t kDegradeWindow = 1024;
+  int64_t units_ = 0;             // units finished (finish_unit)
+  int64_t last_fault_unit_ = -1;  // units_ at the last timed-out hand-off
   int lock_fd_ = -1;          // the cross-process lock of the persistent slot (claim_persistent)
   int persist_fault_ = 0;     // give-up code of the last failed unit (finish_unit), 0 if none
   bool recovered_ = false;
   std::vector<std::pair<int*, size_t>> sync_bufs_;  // every persistent counter block (reset_persistent)
-  // RWKVTTS_TEST_DROP_ARRIVE=1 at creation (test hook): a device word set to 1; the first rkv
-  // workgroup of a persistent attention launch that finds it set clears it and skips its head
-  // arrival, so that head's WKV workgroups time out once (tests/test_gpu_persist_recovery.py)
+  // RWKVTTS_TEST_DROP_ARRIVE=n at creation (test hook, not a deployment knob): a device word set to
+  // 1; the rkv workgroup of a persistent attention launch that takes it (take_drop) skips its head
+  // arrival, so that head's WKV workgroups time out and the unit fails; the word is re-armed after
+  // each recovery until n units have failed (tests/test_gpu_persist_recovery.py)
   int* d_drop_ = nullptr;
+  int test_drops_left_ = 0;
 
   void state_permute(const float* std_block, float* dev_block);
   void state_unpermute(const float* dev_block, float* std_block);
   int state_perm_ = 0;  // WKV state block layout (wkv_perm_layout; engine.hip perm_index)
   // XCD-aware grids per launch class: bit 0 rkv, 1 Wo, 2 ffn key, 3 ffn value, 4 head, 5 wkv
-  int xmap_mask_ = 0x28;  // measured (timeline A/B): value GEMM and WKV gain, rkv loses
-  // write-through (sc1) output stores per launch class, same bit order as xmap_mask_, plus
+  static constexpr int kXmapMask = 0x28;  // measured (timeline A/B): value GEMM and WKV gain, rkv loses
+  // write-through (sc1) output stores per launch class, same bit order as kXmapMask, plus
   // bit 6 ln_att, bit 7 ln_ffn
-  int wt_mask_ = 0xFF;
-  // RWKVTTS_PERSIST_MIN_ROWS: decode steps with fewer rows take the separate launches. 1 since the
-  // 1-us weight-stream hold: the persistent halves then win at every batch size measured (B = 1:
-  // 637-642 -> 622 us per step, B = 8: 693 -> 677-679, B = 32: 771-782 -> 754-768;
-  // profiles/r04h7_small_batch_ab.txt)
-  int persist_min_rows_ = 1;
+  static constexpr int kWtMask = 0xFF;
+  // GemmArgs::xalign per class: bit 0 rkv (-> WKV heads; within noise, off), bit 2 ffn key (-> value K-slices)
+  static constexpr int kXalignMask = 4;
+  // The decode-step forms (rwkvtts_engine_desc.forms, RWKVTTS_FORM_*; the defaults are the shipping
+  // forms, each measured faster than the launches it replaces):
   // one-row decode steps: the row-fused persistent form (each GEMM workgroup computes the row's
-  // LayerNorm itself; lm_kernels.h launch_att_persist). RWKVTTS_FUSE_LN1=0 turns it off.
+  // LayerNorm itself; lm_kernels.h launch_att_persist). RWKVTTS_FORM_LN_ROWS turns it off.
   bool fuse_ln1_ = true;
-  // one-row FFN form: the key -> value hand-off as data-tagged granules (FfnSync::gran; d_epoch_ is
-  // bumped by each pass's layer-0 attention launch). RWKVTTS_GRAN=0 turns it off.
+  // one-row forms: the FFN key -> value and the WKV -> Wo hand-offs as data-tagged granules
+  // (FfnSync::gran; d_epoch_ is bumped by each pass's layer-0 attention launch and by
+  // reset_persistent). RWKVTTS_FORM_SLAB_HANDOFF turns it off.
   bool gran_ = true;
   uint64_t* d_gran_ = nullptr;
-  uint64_t* d_gran_att_ = nullptr;  // the attention form's (rkv -> WKV, WKV -> Wo)
-  // one-row passes, layers > 0: the two halves as one launch (launch_layer1_persist). Measured
-  // slower than two launches (B = 1: 525-529 vs 515-519 us per step, profiles/r05w_layer1_ab.txt):
-  // off by default, RWKVTTS_LAYER1=1 turns it on.
-  bool layer1_ = false;
-  // one-row steps: ln_out folded into the head GEMM (launch_gemm_lnrow). RWKVTTS_FUSE_LNOUT=0 off.
+  uint64_t* d_gran_att_ = nullptr;  // the attention form's (WKV -> Wo)
+  // one-row steps: ln_out folded into the head GEMM (launch_gemm_lnrow). RWKVTTS_FORM_SEPARATE_LNOUT off.
   bool lnrow_ = true;
+  bool exact_sampler_ = false;  // RWKVTTS_FORM_EXACT_SAMPLER: k_advance without the certified fast path
   int* d_epoch_ = nullptr;
-  int ffn_persist_ = 5;     // RWKVTTS_FFN_PERSIST: decode steps' FFN half as one launch (k_ffn_persist);
-                            // 0 off, else 1 + 2 x launch options (5: long poll sleep, the measured best)
+  // decode steps' FFN / attention half as one persistent launch (k_ffn_persist / k_att_persist):
+  // 0 off (RWKVTTS_FORM_SEPARATE_FFN / _ATT), else 1 + 2 x launch options (opts 2: the longer poll
+  // sleep, the measured best)
+  static constexpr int kPersistOn = 5;
+  int ffn_persist_ = kPersistOn;
   int* ffn_sync_ = nullptr; // its hand-off counters: [L][kFfnSyncInts] (give-up code: d_ctrl_[S_])
-  int att_persist_ = 5;     // RWKVTTS_ATT_PERSIST: decode steps' attention half as one launch (k_att_persist),
-                            // same encoding
+  int att_persist_ = kPersistOn;
   int* att_sync_ = nullptr; // its hand-off counters: [L][kAttSyncInts]
-  int xalign_mask_ = 4;     // GemmArgs::xalign per class: bit 0 rkv (-> WKV heads), bit 2 ffn key (-> value K-slices)
   int device_ = 0;
   int f16_ = 0;  // fp16 matrices (else bf16): MFMA f16 and f16 activation planes
   hipStream_t stream_ = nullptr;
@@ -199,7 +205,7 @@ class Engine {
   int splitA_ = 1, splitO_ = 1, splitK_ = 1, splitF_ = 1, splitH_ = 1;
   bool use_graphs_ = true;
   uint8_t* wblob_ = nullptr;
-  // debug timeline (RWKVTTS_TIMELINE=path): per launch of a decode step, earliest WG start and
+  // debug timeline (RWKVTTS_DEBUG_STAMPS "timeline=path"): per launch of a decode step, earliest WG start and
   // latest WG end (s_memrealtime); accumulated over steps and written at the end of generate()
   unsigned long long* d_tl_ = nullptr;  // [kTlMax][kTlStride]
   unsigned long long* d_gt_ = nullptr;  // in-graph timing slots [kTlMax][kTlStride]
@@ -266,18 +272,18 @@ class Engine {
   std::map<std::pair<int, int>, hipGraphExec_t> graphs_;
   std::vector<std::pair<std::string, hipEvent_t>> pending_prof_;
   std::vector<void*> allocs_;
-  uint64_t* dbg_stamps_ = nullptr;  // RWKVTTS_WKV_STAMPS=<file>: layer-5 WKV phase stamps
+  // debug stamps (RWKVTTS_DEBUG_STAMPS "kind=path", null in production):
+  uint64_t* dbg_stamps_ = nullptr;  // wkv: layer-5 WKV phase stamps
   std::string dbg_stamp_path_;
-  int dbg_exp_ = 0;
-  bool no_emb_fuse_ = false;  // RWKVTTS_NO_EMB_FUSE at creation: decode steps launch k_embed separately
-  uint64_t* dbg_astamps_ = nullptr;  // RWKVTTS_ADV_STAMPS=<file>: k_advance phase stamps, [rows][16]
+  bool no_emb_fuse_ = false;  // RWKVTTS_FORM_SEPARATE_EMBED: decode steps launch k_embed separately
+  uint64_t* dbg_astamps_ = nullptr;  // adv: k_advance phase stamps, [rows][16]
   std::string dbg_astamp_path_;
-  uint64_t* dbg_astamps2_ = nullptr;  // RWKVTTS_ATT_STAMPS=<file>: layer-5 k_att_persist block stamps
+  uint64_t* dbg_astamps2_ = nullptr;  // att: layer-5 k_att_persist block stamps
   std::string dbg_astamp2_path_;
-  uint64_t* dbg_fstamps_ = nullptr;  // RWKVTTS_FFN_STAMPS=<file>: layer-5 k_ffn_persist block stamps
+  uint64_t* dbg_fstamps_ = nullptr;  // ffn: layer-5 k_ffn_persist block stamps
   std::string dbg_fstamp_path_;
-  uint64_t* dbg_gstamps_ = nullptr;  // RWKVTTS_GEMM_STAMPS=<file>: layer-5 rkv / ffn_value GEMM stamps
-  std::string dbg_gstamp_path_;  // RWKVTTS_DEBUG_EXP: timing experiments (wrong numerics), never in production
+  uint64_t* dbg_gstamps_ = nullptr;  // gemm: layer-5 rkv / ffn_value GEMM stamps
+  std::string dbg_gstamp_path_;
   template <typename T>
   int alloc(T** p, size_t count);
 };

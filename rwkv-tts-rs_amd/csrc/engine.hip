@@ -52,8 +52,20 @@ int lock_device_file(int device) {
     if (*c == '/' || *c == ' ') *c = '_';
   const char* dir = getenv("RWKVTTS_LOCK_DIR");
   const std::string path = std::string(dir && dir[0] ? dir : "/tmp") + "/rwkvtts_persist_" + bus + ".lock";
-  const int fd = open(path.c_str(), O_RDONLY | O_CREAT | O_CLOEXEC, 0666);
-  if (fd < 0) return -2;
+  int fd = open(path.c_str(), O_RDONLY | O_CREAT | O_CLOEXEC, 0666);
+  // another user's lock file in a sticky world-writable directory: O_CREAT is refused under
+  // fs.protected_regular (EACCES) although the file itself may be readable -- open it as it is
+  if (fd < 0) fd = open(path.c_str(), O_RDONLY | O_CLOEXEC);
+  if (fd < 0) {
+    if (access(path.c_str(), F_OK) == 0) {  // it exists but cannot be opened: assume it is held
+      fprintf(stderr, "rwkvtts: cannot open the persistent-launch lock %s; running the separate launches\n",
+              path.c_str());
+      return -1;
+    }
+    fprintf(stderr, "rwkvtts: cannot create the persistent-launch lock %s: no cross-process guard "
+            "(set RWKVTTS_LOCK_DIR to a directory every process on this GPU shares)\n", path.c_str());
+    return -2;
+  }
   if (flock(fd, LOCK_EX | LOCK_NB) != 0) {
     close(fd);
     return -1;
@@ -111,7 +123,6 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
      // vocoder sharing the GPU (codec.hip: lowest) fills the CUs it leaves idle
     int least = 0, greatest = 0;
     RT_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
-    if (getenv("RWKVTTS_NO_PRIO")) greatest = 0;
     RT_HIP(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, greatest));
   }
 
@@ -148,51 +159,64 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
     while (ks > 128 && K % ks) ks >>= 1;
     return K / ks;
   };
-  splitA_ = pick(C, getenv("RWKVTTS_RKV_KS") ? atoi(getenv("RWKVTTS_RKV_KS")) : 256);   // r,k,v,LoRA-down: 53 col tiles x 4
-  splitO_ = pick(C, getenv("RWKVTTS_WO_KS") ? atoi(getenv("RWKVTTS_WO_KS")) : 128);   // Wo: 16 col tiles x 8
-  splitK_ = pick(C, getenv("RWKVTTS_KEY_KS") ? atoi(getenv("RWKVTTS_KEY_KS")) : 256);  // ffn key: 64 col tiles x 4
-  splitF_ = pick(F, getenv("RWKVTTS_VAL_KS") ? atoi(getenv("RWKVTTS_VAL_KS")) : 256);   // ffn value: 16 col tiles x 16
-  splitH_ = pick(C, getenv("RWKVTTS_HEAD_KS") ? atoi(getenv("RWKVTTS_HEAD_KS")) : 512);   // head: 129 col tiles x 2
+  // (K-slice depths measured at B = 32 and B = 1: twice or half the slices of any projection are
+  // equal or slower, DESIGN.md §7.0 / §12, profiles/r04b1_splitk_ab.txt)
+  splitA_ = pick(C, 256);  // r,k,v,LoRA-down: 53 col tiles x 4
+  splitO_ = pick(C, 128);  // Wo: 16 col tiles x 8
+  splitK_ = pick(C, 256);  // ffn key: 64 col tiles x 4
+  splitF_ = pick(F, 256);  // ffn value: 16 col tiles x 16
+  splitH_ = pick(C, 512);  // head: 129 col tiles x 2
   RT_CHECK(C % 128 == 0 && F % 128 == 0, RWKVTTS_EUNSUPPORTED, "K dims must be multiples of 128");
   RT_CHECK(splitA_ <= kMaxParts, RWKVTTS_EUNSUPPORTED, "n_embd too large for the WKV partial sum (raise kMaxParts)");
   state_perm_ = wkv_perm_layout(dims.d_decay, dims.d_aaa, dims.d_mv, dims.d_gate, splitA_, S_, desc.wkv_variant);
-  if (const char* ex = getenv("RWKVTTS_DEBUG_EXP")) dbg_exp_ = atoi(ex);
-  no_emb_fuse_ = getenv("RWKVTTS_NO_EMB_FUSE") != nullptr;  // A/B switch (read per engine: tests compare)
-  if (const char* xm = getenv("RWKVTTS_XMAP_MASK")) xmap_mask_ = (int)strtol(xm, nullptr, 0);
-  if (const char* wm = getenv("RWKVTTS_WT_MASK")) wt_mask_ = (int)strtol(wm, nullptr, 0);
-  if (const char* xa = getenv("RWKVTTS_XALIGN_MASK")) xalign_mask_ = (int)strtol(xa, nullptr, 0);
-  if (const char* fp = getenv("RWKVTTS_FFN_PERSIST")) ffn_persist_ = atoi(fp);
-  if (const char* ap = getenv("RWKVTTS_ATT_PERSIST")) att_persist_ = atoi(ap);
-  if (const char* pm = getenv("RWKVTTS_PERSIST_MIN_ROWS")) persist_min_rows_ = atoi(pm);
-  if (const char* fl = getenv("RWKVTTS_FUSE_LN1")) fuse_ln1_ = atoi(fl) != 0;
-  if (const char* gr = getenv("RWKVTTS_GRAN")) gran_ = atoi(gr) != 0;
-  if (const char* l1 = getenv("RWKVTTS_LAYER1")) layer1_ = atoi(l1) != 0;
-  if (const char* lr = getenv("RWKVTTS_FUSE_LNOUT")) lnrow_ = atoi(lr) != 0;
+  // decode-step forms (rwkvtts_engine_desc.forms; 0 = the shipping forms, every bit bitwise-equal)
+  constexpr uint32_t kKnownForms = RWKVTTS_FORM_SEPARATE_ATT | RWKVTTS_FORM_SEPARATE_FFN | RWKVTTS_FORM_LN_ROWS |
+                                   RWKVTTS_FORM_SLAB_HANDOFF | RWKVTTS_FORM_SEPARATE_LNOUT |
+                                   RWKVTTS_FORM_SEPARATE_EMBED | RWKVTTS_FORM_EXACT_SAMPLER;
+  RT_CHECK((desc.forms & ~kKnownForms) == 0, RWKVTTS_EINVAL, "engine desc: unknown forms bits");
+  att_persist_ = (desc.forms & RWKVTTS_FORM_SEPARATE_ATT) ? 0 : kPersistOn;
+  ffn_persist_ = (desc.forms & RWKVTTS_FORM_SEPARATE_FFN) ? 0 : kPersistOn;
+  fuse_ln1_ = !(desc.forms & RWKVTTS_FORM_LN_ROWS);
+  gran_ = !(desc.forms & RWKVTTS_FORM_SLAB_HANDOFF);
+  lnrow_ = !(desc.forms & RWKVTTS_FORM_SEPARATE_LNOUT);
+  no_emb_fuse_ = (desc.forms & RWKVTTS_FORM_SEPARATE_EMBED) != 0;
+  exact_sampler_ = (desc.forms & RWKVTTS_FORM_EXACT_SAMPLER) != 0;
   if ((ffn_persist_ || att_persist_) && !claim_persistent(desc.device, this, &lock_fd_)) ffn_persist_ = att_persist_ = 0;
-  if (const char* gp = getenv("RWKVTTS_GEMM_STAMPS")) {
-    dbg_gstamp_path_ = gp;
-    RT_OK(alloc(&dbg_gstamps_, 2 * 4096 * 4));
-  }
-  if (const char* fs = getenv("RWKVTTS_FFN_STAMPS")) {  // debug: layer-5 k_ffn_persist block stamps
-    dbg_fstamp_path_ = fs;
-    RT_OK(alloc(&dbg_fstamps_, 1024 * 4));
-  }
-  if (const char* as = getenv("RWKVTTS_ATT_STAMPS")) {  // debug: layer-5 k_att_persist block stamps
-    dbg_astamp2_path_ = as;
-    RT_OK(alloc(&dbg_astamps2_, 2048 * 4));
-  }
-  if (const char* tp = getenv("RWKVTTS_TIMELINE")) {
-    tl_path_ = tp;
-    RT_OK(alloc(&d_tl_, (size_t)kTlStride * kTlMax));
-    use_graphs_ = desc.use_graphs != 0;
-  }
-  if (const char* ap = getenv("RWKVTTS_ADV_STAMPS")) {
-    dbg_astamp_path_ = ap;
-    RT_OK(alloc(&dbg_astamps_, 256 * 16));
-  }
-  if (const char* sp = getenv("RWKVTTS_WKV_STAMPS")) {
-    dbg_stamp_path_ = sp;
-    RT_OK(alloc(&dbg_stamps_, 4096 * 8));
+  // debug instrumentation (tools/: stamps of one layer's launches, the launch timeline), off in
+  // production: RWKVTTS_DEBUG_STAMPS="kind=path[;kind=path...]", kind one of gemm (layer-5 rkv /
+  // value GEMM), ffn / att (layer-5 persistent-launch block stamps), timeline (per-launch start /
+  // end of every decode step), adv (k_advance phases), wkv (layer-5 WKV phases)
+  if (const char* ds = getenv("RWKVTTS_DEBUG_STAMPS")) {
+    std::string spec(ds);
+    size_t pos = 0;
+    while (pos < spec.size()) {
+      size_t end = spec.find(';', pos);
+      if (end == std::string::npos) end = spec.size();
+      const std::string item = spec.substr(pos, end - pos);
+      pos = end + 1;
+      const size_t eq = item.find('=');
+      if (eq == std::string::npos) continue;
+      const std::string kind = item.substr(0, eq), path = item.substr(eq + 1);
+      if (kind == "gemm") {
+        dbg_gstamp_path_ = path;
+        RT_OK(alloc(&dbg_gstamps_, 2 * 4096 * 4));
+      } else if (kind == "ffn") {
+        dbg_fstamp_path_ = path;
+        RT_OK(alloc(&dbg_fstamps_, 1024 * 4));
+      } else if (kind == "att") {
+        dbg_astamp2_path_ = path;
+        RT_OK(alloc(&dbg_astamps2_, 2048 * 4));
+      } else if (kind == "timeline") {
+        tl_path_ = path;
+        RT_OK(alloc(&d_tl_, (size_t)kTlStride * kTlMax));
+      } else if (kind == "adv") {
+        dbg_astamp_path_ = path;
+        RT_OK(alloc(&dbg_astamps_, 256 * 16));
+      } else if (kind == "wkv") {
+        dbg_stamp_path_ = path;
+        RT_OK(alloc(&dbg_stamps_, 4096 * 8));
+      }
+    }
   }
 
   // weights
@@ -358,10 +382,11 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
   sync_bufs_ = {{ffn_sync_, (size_t)Lc * kFfnSyncInts * sizeof(int)},
                 {att_sync_, (size_t)Lc * kAttSyncInts * sizeof(int)}};
   for (auto& b : sync_bufs_) RT_HIP(hipMemset(b.first, 0, b.second));
-  if (getenv("RWKVTTS_TEST_DROP_ARRIVE")) {
+  if (const char* dr = getenv("RWKVTTS_TEST_DROP_ARRIVE")) {  // test hook: n units with a dropped arrival
     RT_OK(alloc(&d_drop_, 64));
     const int one = 1;
     RT_HIP(hipMemcpy(d_drop_, &one, sizeof(int), hipMemcpyHostToDevice));
+    test_drops_left_ = std::max(1, atoi(dr)) - 1;  // re-armed after each recovery
   }
   RT_OK(alloc(&vfirst_, RC));
   RT_OK(alloc(&xo_hi_, RC));
@@ -381,7 +406,7 @@ int Engine::init(const rwkvtts_engine_desc& desc, const void* weights, size_t by
     const int one = 1;
     RT_HIP(hipMemcpy(d_epoch_, &one, sizeof(int), hipMemcpyHostToDevice));
     sync_bufs_.push_back({(int*)d_gran_, (size_t)ffn_gran_count(4, dims.n_ffn) * sizeof(uint64_t)});
-    const int64_t ng = att_gran_count(4, ldA_, (int)dims.n_embd);
+    const int64_t ng = att_gran_count((int)dims.n_embd);
     RT_OK(alloc(&d_gran_att_, (size_t)ng));
     sync_bufs_.push_back({(int*)d_gran_att_, (size_t)ng * sizeof(uint64_t)});
   }
@@ -561,12 +586,10 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
   // whole forward falls back.
   bool any_quant = false;
   for (const LayerW& lw : L_) any_quant = any_quant || lw.quant != 0;
-  // Below persist_min_rows_ rows (measured: B = 1 and 8 are 1.4 % slower persistent, B = 32 7 %
-  // faster) the separate launches run.
-  const bool big = R >= persist_min_rows_;
-  bool use_att = att_persist_ && inplace && big && !dbg_exp_ && Lc >= 2 && !dbg_stamps_ && !dbg_gstamps_ &&
-                 !any_quant && emb_fused;
-  bool use_ffn = ffn_persist_ && inplace && big && !dbg_exp_ && Lc >= 2 && !dbg_gstamps_ && !any_quant;
+  // (every row count: with the 1-us weight-stream hold the persistent halves win at B = 1, 8 and 32,
+  // profiles/r04h7_small_batch_ab.txt)
+  bool use_att = att_persist_ && inplace && Lc >= 2 && !dbg_stamps_ && !dbg_gstamps_ && !any_quant && emb_fused;
+  bool use_ffn = ffn_persist_ && inplace && Lc >= 2 && !dbg_gstamps_ && !any_quant;
   // one-row passes: the FFN key -> value hand-off as granules, live once the layer-0 attention
   // launch (which bumps the pass epoch) has been issued
   const bool gran_pass = gran_ && d_gran_ && fuse_ln1_ && R == 1 && use_att && use_ffn;
@@ -605,7 +628,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     m.rows = d_rows_;
     m.row_map = nullptr;
     m.inplace = inplace ? 1 : 0;
-    m.wt = (wt_mask_ >> 6) & 1;
+    m.wt = (kWtMask >> 6) & 1;
     if (l == 0 && emb_fused) {
       m.emb_tok = d_tok_;
       m.emb_ctrl = &d_ctrl_[0].next_token;
@@ -666,11 +689,10 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
       for (int t = 0; t < 3 * C / 64; ++t) g.tinfo[t] |= 1u << 31;
     }
     g.xmode = kXPlanes; g.out = partA_; g.split_stride = (int64_t)Rmax_ * ldA_; g.ldo = ldA_;
-    g.allow_xmap = xmap_mask_ & 1;
-    g.xalign = (xalign_mask_ & 1) ? 1 : 0;  // r / k / v tile h (head h) on the XCD of WKV head h
-    g.wt = wt_mask_ & 1;
+    g.allow_xmap = kXmapMask & 1;
+    g.xalign = (kXalignMask & 1) ? 1 : 0;  // r / k / v tile h (head h) on the XCD of WKV head h
+    g.wt = kWtMask & 1;
     g.stamps = (l == 5 && dbg_gstamps_) ? dbg_gstamps_ : nullptr;
-    g.exp = dbg_exp_ >> 8;
     // ---- WKV + LoRA-up + GroupNorm + bonus + gate
     WkvArgs k{};
     k.f16 = f16_;
@@ -683,11 +705,10 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     k.v_first = vfirst_; k.ldv = C; k.z_hi = z_hi_; k.z_lo = z_lo_; k.ldz = C;
     k.segs = d_segs_; k.layer = l; k.C = C; k.n_slots = S_; k.n_seg = n_seg; k.multi_row = R > n_seg;
     k.perm = state_perm_;
-    k.allow_xmap = (xmap_mask_ >> 5) & 1;
-    k.wt = (wt_mask_ >> 5) & 1;
+    k.allow_xmap = (kXmapMask >> 5) & 1;
+    k.wt = (kWtMask >> 5) & 1;
     k.Dw = dims.d_decay; k.Da = dims.d_aaa; k.Dv = dims.d_mv; k.Dg = dims.d_gate;
     k.stamps = (l == 5) ? dbg_stamps_ : nullptr;
-    k.exp = dbg_exp_;
     // ---- output projection (split-K partials)
     GemmArgs go{};
     go.f16 = f16_;
@@ -695,10 +716,9 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     go.seg[0] = {w.wo, z_hi_, z_lo_, C, C, 0, 0};
     go.K = C; go.M = R; go.k_split = splitO_; go.kslice = C / splitO_;
     go.xmode = kXPlanes; go.out = partO_; go.split_stride = RC; go.ldo = C;
-    go.allow_xmap = (xmap_mask_ >> 1) & 1;
+    go.allow_xmap = (kXmapMask >> 1) & 1;
     if (w.quant) { go.q_fmt = w.quant; go.qw = w.q_o; go.qs = w.s_o; go.q_shift = w.qs_o; }
-    go.wt = (wt_mask_ >> 1) & 1;
-    go.exp = dbg_exp_ >> 8;
+    go.wt = (kWtMask >> 1) & 1;
     // ---- ffn: residual + Wo partials -> LN2 -> mix
     LnMixArgs f = m;
     f.emb = nullptr;  // (layer 0's embedding fusion belongs to the attention LayerNorm only)
@@ -713,24 +733,18 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     f.x_hi = xf_hi_;
     f.x_lo = xf_lo_;
     f.shift = ffn_sh_;
-    f.wt = (wt_mask_ >> 7) & 1;
+    f.wt = (kWtMask >> 7) & 1;
     // decode steps: the attention half as ONE persistent launch (k_att_persist: LN1 + mixes, rkv +
     // LoRA-down, WKV, Wo with in-launch hand-offs; bit-identical outputs) where the shapes allow it
     bool att_persisted = false;
-    // one-row passes, layers > 0: both halves as ONE launch (launch_layer1_persist, below at the
-    // FFN half) -- the attention half is launched here only if that form does not apply
-    const bool layer1 = layer1_ && gran_live && l > 0 && use_att && use_ffn && R == 1 && fuse_ln1_;
-    if (layer1) att_persisted = true;  // (issued with the FFN half)
-    auto launch_att = [&]() -> bool {
-      return launch_att_persist(m, g, k, go, att_sync_ + (size_t)l * kAttSyncInts,
-                                att_sync_ + (size_t)((l + Lc - 1) % Lc) * kAttSyncInts, (int*)(d_ctrl_ + S_), R, H_,
-                                stream_, l == 5 ? dbg_astamps2_ : nullptr, att_persist_ >> 1, d_drop_, fuse_ln1_,
-                                l == 0 && gran_pass ? d_epoch_ : nullptr, gran_live ? d_gran_att_ : nullptr, d_epoch_);
-    };
-    if (use_att && !layer1) {
+    if (use_att) {
       m.tl = g.tl = k.tl = go.tl = tl_next("att_persist");
       prof_begin(&ev);
-      att_persisted = launch_att();
+      att_persisted = launch_att_persist(m, g, k, go, att_sync_ + (size_t)l * kAttSyncInts,
+                                         att_sync_ + (size_t)((l + Lc - 1) % Lc) * kAttSyncInts, (int*)(d_ctrl_ + S_),
+                                         R, H_, stream_, l == 5 ? dbg_astamps2_ : nullptr, att_persist_ >> 1, d_drop_,
+                                         fuse_ln1_, l == 0 && gran_pass ? d_epoch_ : nullptr,
+                                         gran_live ? d_gran_att_ : nullptr, d_epoch_);
       if (att_persisted) {
         prof_end("att_persist", ev);
         if (l == 0 && gran_pass) gran_live = true;  // this pass's epoch is bumped
@@ -746,20 +760,19 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     if (!att_persisted) {
       m.tl = tl_next("ln_att");
       prof_begin(&ev);
-      if (!(dbg_exp_ & 0x10000))
-        RT_CHECK(launch_ln_mix(m, R, stream_) >= 0, RWKVTTS_EUNSUPPORTED, "layer-0 embedding fusion: unsupported shape");
+      RT_CHECK(launch_ln_mix(m, R, stream_) >= 0, RWKVTTS_EUNSUPPORTED, "layer-0 embedding fusion: unsupported shape");
       prof_end("ln_mix_att", ev);
       g.tl = tl_next("gemm_rkv");
       prof_begin(&ev);
-      if (!(dbg_exp_ & 0x40000)) launch_gemm(g, stream_);
+      launch_gemm(g, stream_);
       prof_end("gemm_rkv_lora", ev);
       k.tl = tl_next("wkv");
       prof_begin(&ev);
-      if (!(dbg_exp_ & 0x20000)) launch_wkv(k, n_seg, H_, stream_);
+      launch_wkv(k, n_seg, H_, stream_);
       prof_end("wkv", ev);
       go.tl = tl_next("gemm_wo");
       prof_begin(&ev);
-      if (!(dbg_exp_ & 0x40000)) launch_gemm(go, stream_);
+      launch_gemm(go, stream_);
       prof_end("gemm_wo", ev);
     }
     GemmArgs gk{};
@@ -768,12 +781,11 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     gk.seg[0] = {w.ffn_k, xf_hi_, xf_lo_, C, F, 0, 0};
     gk.K = C; gk.M = R; gk.k_split = splitK_; gk.kslice = C / splitK_;
     gk.xmode = kXPlanes; gk.out = partK_; gk.split_stride = (int64_t)Rmax_ * F; gk.ldo = F;
-    gk.allow_xmap = (xmap_mask_ >> 2) & 1;
+    gk.allow_xmap = (kXmapMask >> 2) & 1;
     if (w.quant) { gk.q_fmt = w.quant; gk.qw = w.q_fk; gk.qs = w.s_fk; gk.q_shift = w.qs_fk; }
     // key tiles of value K-slice s on the XCD that runs slice s (value xmap: split = xcd + 8 j)
-    if ((xalign_mask_ >> 2) & 1) gk.xalign = std::max(1, (F / splitF_) / 64);
-    gk.wt = (wt_mask_ >> 2) & 1;
-    gk.exp = dbg_exp_ >> 8;
+    if ((kXalignMask >> 2) & 1) gk.xalign = std::max(1, (F / splitF_) / 64);
+    gk.wt = (kWtMask >> 2) & 1;
     GemmArgs gv{};
     gv.f16 = f16_;
     gv.nseg = 1;
@@ -781,8 +793,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     gv.K = F; gv.M = R; gv.k_split = splitF_; gv.kslice = F / splitF_;
     gv.xmode = kXRelu2; gv.x_part = partK_; gv.x_nsplit = splitK_; gv.x_ld = F;
     gv.x_part_stride = (int64_t)Rmax_ * F;
-    static const bool no_planes = getenv("RWKVTTS_NO_RELU2_PLANES") != nullptr;  // A/B timing switch
-    const bool planes = xk_hi_ && R > kPlaneRows && !no_planes;
+    const bool planes = xk_hi_ && R > kPlaneRows;
     if (planes) {
       // prefill steps: relu^2 planes once (every value column tile would otherwise re-read the
       // NX f32 key slabs of its K-slice); decode steps keep the fused staging (one launch fewer)
@@ -790,36 +801,14 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
       gv.xmode = kXPlanes;
     }
     gv.out = partF_; gv.split_stride = RC; gv.ldo = C;
-    gv.allow_xmap = (xmap_mask_ >> 3) & 1;
+    gv.allow_xmap = (kXmapMask >> 3) & 1;
     if (w.quant) { gv.q_fmt = w.quant; gv.qw = w.q_fv; gv.qs = w.s_fv; gv.q_shift = w.qs_fv; }
-    gv.wt = (wt_mask_ >> 3) & 1;
+    gv.wt = (kWtMask >> 3) & 1;
     gv.stamps = (l == 5 && dbg_gstamps_) ? dbg_gstamps_ + 4096 * 4 : nullptr;
-    gv.exp = dbg_exp_ >> 8;
     // decode steps: the whole FFN half as ONE persistent launch (k_ffn_persist, in-launch
     // hand-offs; bit-identical outputs) where the shapes allow it
     bool persisted = false;
-    if (layer1) {
-      m.tl = g.tl = k.tl = go.tl = f.tl = gk.tl = gv.tl = tl_next("layer1_persist");
-      prof_begin(&ev);
-      persisted = launch_layer1_persist(m, g, k, go, f, gk, gv, att_sync_ + (size_t)l * kAttSyncInts,
-                                        att_sync_ + (size_t)((l + Lc - 1) % Lc) * kAttSyncInts,
-                                        ffn_sync_ + (size_t)l * kFfnSyncInts,
-                                        ffn_sync_ + (size_t)((l + Lc - 1) % Lc) * kFfnSyncInts, (int*)(d_ctrl_ + S_),
-                                        H_, stream_, att_persist_ >> 1, ffn_persist_ >> 1, d_gran_att_, d_gran_, d_epoch_);
-      if (persisted) {
-        prof_end("layer1_persist", ev);
-      } else {  // not covered: the two launches
-        if (tl_base() && tl_n_ > 0) {
-          --tl_n_;
-          if ((int)tl_names_.size() > tl_n_) tl_names_.resize(tl_n_);
-        }
-        m.tl = g.tl = k.tl = go.tl = tl_next("att_persist");
-        prof_begin(&ev);
-        RT_CHECK(launch_att(), RWKVTTS_EHIP, "persistent attention launch: a layer after layer 0 fell back");
-        prof_end("att_persist", ev);
-      }
-    }
-    if (use_ffn && !persisted) {
+    if (use_ffn) {
       f.tl = gk.tl = gv.tl = tl_next("ffn_persist");
       prof_begin(&ev);
       persisted = launch_ffn_persist(f, gk, gv, ffn_sync_ + (size_t)l * kFfnSyncInts,
@@ -840,23 +829,23 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     if (!persisted) {
       f.tl = tl_next("ln_ffn");
       prof_begin(&ev);
-      if (!(dbg_exp_ & 0x10000)) launch_ln_mix(f, R, stream_);
+      launch_ln_mix(f, R, stream_);
       prof_end("ln_mix_ffn", ev);
       prof_begin(&ev);
       gk.tl = tl_next("gemm_key");
-      if (!(dbg_exp_ & 0x40000)) launch_gemm(gk, stream_);
+      launch_gemm(gk, stream_);
       prof_end("gemm_ffn_key", ev);
       if (planes) launch_relu2_planes(partK_, splitK_, (int64_t)Rmax_ * F, F, F, R, xk_hi_, xk_lo_, stream_);
       prof_begin(&ev);
       gv.tl = tl_next("gemm_value");
-      if (!(dbg_exp_ & 0x40000)) launch_gemm(gv, stream_);
+      launch_gemm(gv, stream_);
       prof_end("gemm_ffn_value", ev);
     }
   }
   if (n_lg > 0) {
     LnMixArgs o = ln_out_args();
     // one-row steps: ln_out folded into the head GEMM (launch_gemm_lnrow) where covered
-    const bool lnrow = lnrow_ && n_lg == 1 && R == 1 && !dbg_exp_;
+    const bool lnrow = lnrow_ && n_lg == 1 && R == 1;
     if (!lnrow) {
       o.tl = tl_next("ln_out");
       prof_begin(&ev);
@@ -869,10 +858,9 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
     gh.seg[0] = {head_, xo_hi_, xo_lo_, C, head_rows, 0, 0};
     gh.K = C; gh.M = n_lg; gh.k_split = splitH_; gh.kslice = C / splitH_;
     gh.xmode = kXPlanes; gh.out = logits_; gh.split_stride = (int64_t)Rmax_ * Vpad_; gh.ldo = Vpad_;
-    gh.allow_xmap = (xmap_mask_ >> 4) & 1;
-    gh.wt = (wt_mask_ >> 4) & 1;
+    gh.allow_xmap = (kXmapMask >> 4) & 1;
+    gh.wt = (kWtMask >> 4) & 1;
     prof_begin(&ev);
-    gh.exp = dbg_exp_ >> 8;
     gh.tl = tl_next("gemm_head");
     bool headed = false;
     if (lnrow) {
@@ -887,7 +875,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
         prof_begin(&ev);
       }
     }
-    if (!headed && !(dbg_exp_ & 0x40000)) launch_gemm(gh, stream_);
+    if (!headed) launch_gemm(gh, stream_);
     prof_end("gemm_head", ev);
     if (advance) {
       AdvanceArgs a{};
@@ -902,7 +890,7 @@ int Engine::launch_forward(int R, int n_seg, int n_lg, int head_rows, bool tok_f
       a.tl = tl_next("advance");
       a.stamps = dbg_astamps_;
       prof_begin(&ev);
-      launch_advance(a, stream_);
+      launch_advance(a, stream_, exact_sampler_ ? 0 : 1);
       prof_end("sample_advance", ev);
     }
   }
@@ -959,10 +947,7 @@ int Engine::run_step(const StepPlan& p, bool upload) {
       // one capture at a time per process: engines owned by different threads (the manager's
       // workers) never capture / instantiate concurrently
       static std::mutex capture_mu;
-      // RWKVTTS_CAPTURE_UNSERIALIZED: experiment switch (the round-2 manager hang)
-      static const bool unser = getenv("RWKVTTS_CAPTURE_UNSERIALIZED") != nullptr;
-      std::unique_lock<std::mutex> cap_lock(capture_mu, std::defer_lock);
-      if (!unser) cap_lock.lock();
+      std::unique_lock<std::mutex> cap_lock(capture_mu);
       hipGraph_t graph;
       RT_HIP(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
       int rc = launch_forward(R, n_seg, n_lg, p.head_rows, true, p.advance);
@@ -1324,10 +1309,7 @@ int Engine::generate(const rwkvtts_request* reqs, int n, rwkvtts_result* res) {
 // idle gap), accounts its time, and retires the slots its control-block snapshot shows done.
 int Engine::finish_unit(int b, bool prefill, std::vector<Active>& act, std::vector<int>& free_slots, JobSource& src,
                         hipEvent_t* ev0, hipEvent_t* ev1) {
-  static const bool blocking = getenv("RWKVTTS_SYNC_BLOCKING") != nullptr;  // A/B switch
-  if (blocking) {
-    RT_HIP(hipEventSynchronize(ev1[b]));
-  } else {
+  {
     hipError_t q;
     while ((q = hipEventQuery(ev1[b])) == hipErrorNotReady) __builtin_ia32_pause();
     RT_HIP(q);
@@ -1368,6 +1350,7 @@ int Engine::finish_unit(int b, bool prefill, std::vector<Active>& act, std::vect
     }
     tl_steps_++;
   }
+  ++units_;
   // retire finished slots: every finished slot's tokens copied on the engine's stream (no
   // null-stream sync), one synchronisation, then the jobs are handed back
   const SlotCtrl* snap = h_ctrl_ + (size_t)b * (S_ + 1);
@@ -1378,19 +1361,11 @@ int Engine::finish_unit(int b, bool prefill, std::vector<Active>& act, std::vect
     return RWKVTTS_EHIP;
   }
   bool copied = false;
-  // RWKVTTS_RESULT_COPY_SYNC=1: experiment switch recreating the round-2 result copies
-  // (synchronous null-stream hipMemcpy per finished slot; DESIGN §3, the manager hang)
-  static const bool sync_copy = getenv("RWKVTTS_RESULT_COPY_SYNC") != nullptr;
   for (auto& a : act) {
     const SlotCtrl& c = snap[a.slot];
     if (a.prefilled < (int)a.prompt.size() || c.phase != kPhDone) continue;
     rwkvtts_result& r = *a.job->res;
     if (r.semantic_tokens && c.n_sem > 0) {
-      if (sync_copy) {
-        RT_HIP(hipMemcpy(r.semantic_tokens, d_sem_ + (int64_t)a.slot * RWKVTTS_SEMANTIC_LIMIT,
-                         sizeof(int32_t) * c.n_sem, hipMemcpyDeviceToHost));
-        continue;
-      }
       RT_HIP(hipMemcpyAsync(r.semantic_tokens, d_sem_ + (int64_t)a.slot * RWKVTTS_SEMANTIC_LIMIT,
                             sizeof(int32_t) * c.n_sem, hipMemcpyDeviceToHost, stream_));
       copied = true;
@@ -1651,8 +1626,7 @@ int Engine::serve(JobSource& src) {
       if ((rc = finish_unit(u.buf, u.prefill, act, free_slots, src, ev0, ev1)) != RWKVTTS_OK) break;
       if (act.size() != dp.rows.size()) decode_plan_valid = false;
     }
-    static const bool no_ahead = getenv("RWKVTTS_NO_AHEAD") != nullptr;  // A/B switch
-    bool ahead = !no_ahead && !any_prefill && !uploaded && use_graphs_ && !profiling && !d_tl_ &&
+    bool ahead = !any_prefill && !uploaded && use_graphs_ && !profiling && !d_tl_ &&
                  (!open || free_slots.empty());
     for (auto& a : act) ahead &= a.total - a.advances >= 1;
     if (ahead) {
@@ -1666,9 +1640,21 @@ int Engine::serve(JobSource& src) {
   if (persist_fault_) {  // a timed-out hand-off: the engine recovers and keeps serving
     const int code = persist_fault_;
     persist_fault_ = 0;
-    recovered_ = reset_persistent() == RWKVTTS_OK;
+    // a second timeout within kDegradeWindow units of the last one (e.g. another process
+    // running persistent launches on this GPU without sharing the lock directory, so the deadlock
+    // condition recurs): leave the persistent forms for good -- separate launches never wait on
+    // one another -- instead of failing unit after unit
+    const bool degrade = last_fault_unit_ >= 0 && units_ - last_fault_unit_ <= kDegradeWindow;
+    last_fault_unit_ = units_;
+    recovered_ = reset_persistent() == RWKVTTS_OK && (!degrade || degrade_persistent() == RWKVTTS_OK);
+    if (recovered_ && d_drop_ && test_drops_left_ > 0) {  // (test hook: the next dropped arrival)
+      --test_drops_left_;
+      const int one = 1;
+      recovered_ = hipMemcpy(d_drop_, &one, sizeof(int), hipMemcpyHostToDevice) == hipSuccess;
+    }
     set_error("persistent decode launch: a hand-off wait timed out (code " + std::to_string(code) +
-              "); the unit's requests failed, the engine was reset");
+              "); the unit's requests failed, the engine was reset" +
+              (degrade ? " and now runs the separate launches (second timeout)" : ""));
   }
   for (int i = 0; i < 2; ++i) {
     hipEventDestroy(ev0[i]);
@@ -1689,7 +1675,25 @@ int Engine::reset_persistent() {
   RT_HIP(hipSetDevice(device_));
   RT_HIP(hipMemsetAsync(d_ctrl_ + S_, 0, sizeof(SlotCtrl), stream_));
   for (auto& b : sync_bufs_) RT_HIP(hipMemsetAsync(b.first, 0, b.second, stream_));
+  if (d_epoch_) {  // a new granule pass tag as well (the zeroed granules match no tag anyway)
+    int ep = 0;
+    RT_HIP(hipMemcpyAsync(&ep, d_epoch_, sizeof(int), hipMemcpyDeviceToHost, stream_));
+    RT_HIP(hipStreamSynchronize(stream_));
+    ++ep;
+    RT_HIP(hipMemcpyAsync(d_epoch_, &ep, sizeof(int), hipMemcpyHostToDevice, stream_));
+  }
   RT_HIP(hipStreamSynchronize(stream_));
+  return RWKVTTS_OK;
+}
+
+int Engine::degrade_persistent() {
+  RT_HIP(hipSetDevice(device_));
+  RT_HIP(hipStreamSynchronize(stream_));
+  att_persist_ = ffn_persist_ = 0;
+  for (auto& g : graphs_) hipGraphExecDestroy(g.second);  // they hold persistent launches
+  graphs_.clear();
+  graph_names_.clear();
+  release_persistent(device_, this, &lock_fd_);
   return RWKVTTS_OK;
 }
 

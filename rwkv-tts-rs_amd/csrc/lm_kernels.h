@@ -81,7 +81,6 @@ struct GemmArgsT {
   int ldo;
   uint64_t* stamps;    // debug: 4 s_memtime stamps per workgroup (null in production)
   int f16;             // weights and activation planes in f16 (fp16 model)
-  int exp;             // debug experiment bits (0 in production): 1 skip X loads, 2 skip W loads
   unsigned long long* tl;  // debug timeline slot (null in production)
   // Multi-segment launches whose segments are packed back to back in 64-column tiles (set by
   // gemm_tile_table): tile t's weights at tw + t * 64 * K and one descriptor word per tile,
@@ -157,7 +156,6 @@ struct WkvArgs {
   int wt;              // k_wkv4 / k_wkv6: write-through (sc1) state stores
   int f16;             // fp16 model: LoRA-up rows and the z planes are f16
   uint64_t* stamps;    // debug: 8 s_memtime stamps per workgroup (null in production)
-  int exp;             // debug experiment bits (0 in production)
   int multi_row;       // some segment has > 1 row (prefill / mixed step): a separate kernel
                        // instantiation, so profiles separate decode launches from prefill ones
   unsigned long long* tl;  // debug timeline slot (null in production)
@@ -228,22 +226,17 @@ struct FfnSync {     // (both persistent launches)
   // granule (sc1 store) at gran[split * gran_ld + column]; a value workgroup polls the granules of
   // its K-slice itself until every tag matches -- no store drain, no counter, no separate payload
   // load behind a poll (MI355X_MICROARCH.md price list: handoff-1to1 vs handoff-flag).
-  // tag = *epoch * 64 + layer; *epoch is bumped once per forward pass by the layer-0 attention
-  // launch (epoch_bump) and by Engine::reset_persistent, so no granule of an earlier pass matches.
+  // tag = (*epoch * 64 + layer) with bit 31 set (lm_kernels.hip gran_tag): never 0, so a zeroed
+  // granule never matches. *epoch is bumped once per one-row forward pass by the layer-0 attention
+  // launch (epoch_bump) and once by Engine::reset_persistent (which also zeroes every granule), so
+  // no granule of an earlier pass matches: every one-row pass rewrites all of them, and a pass
+  // that failed part-way is followed by that reset.
   uint64_t* gran;
   const int* epoch;
   int gran_ld;
   int layer;
-  // attention (one row): rkv -> WKV granules at gran[split * gran_ld + column] (gran_ld = the rkv
-  // output width), WKV -> Wo granules at zgran[channel] (the z split hi | lo << 16)
+  // attention (one row): WKV -> Wo granules at zgran[channel] (the z split hi | lo << 16)
   uint64_t* zgran;
-  int rkv_gran;  // (attention, one row) the rkv workgroups hand their row to the WKV ones as granules
-  // one launch per layer (k_layer1_persist): the attention half's Wo workgroups and its shift
-  // writer count into wo_done (kLnReplicas replicas, after draining); the FFN key workgroups wait
-  // on dep (replica blockIdx % 8) for dep_target before their LayerNorm
-  int* wo_done;
-  const int* dep;
-  int dep_target;
   int* epoch_bump;  // (attention launch of layer 0) one lane adds 1 to it
 };
 
@@ -259,18 +252,11 @@ bool launch_att_persist(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs&
                         int* cnt_prev, int* err, int R, int H, hipStream_t st, uint64_t* stamps, int opts,
                         int* drop = nullptr, bool fused_ln = false, int* epoch_bump = nullptr,
                         uint64_t* gran = nullptr, const int* epoch = nullptr);
-// granules of the one-row attention form's rkv -> WKV and WKV -> Wo hand-offs
-inline int64_t att_gran_count(int rkv_splits, int ldp, int C) { return (int64_t)rkv_splits * ldp + C; }
+// granules of the one-row attention form's WKV -> Wo hand-off (one per channel)
+inline int64_t att_gran_count(int C) { return (int64_t)C; }
 bool launch_ffn_persist(const LnMixArgs& ln, const GemmArgs& key, const GemmArgs& val, int* cnt, int* cnt_prev,
                         int* err, int R, hipStream_t st, uint64_t* stamps = nullptr, int opts = 0,
                         bool fused_ln = false, uint64_t* gran = nullptr, const int* epoch = nullptr);
-// One decode row, layers > 0: the attention half and the FFN half (both row-fused, both granule
-// hand-offs) as ONE launch (k_layer1_persist); false if the shapes / options are not covered (the
-// caller then runs launch_att_persist and launch_ffn_persist).
-bool launch_layer1_persist(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs& wkv, const GemmArgs& wo,
-                           const LnMixArgs& lf, const GemmArgs& key, const GemmArgs& val, int* acnt, int* acnt_prev,
-                           int* fcnt, int* fcnt_prev, int* err, int H, hipStream_t st, int aopts, int fopts,
-                           uint64_t* agran, uint64_t* fgran, const int* epoch);
 // granules the row-fused FFN form's key -> value hand-off needs (FfnSync::gran)
 inline int64_t ffn_gran_count(int key_splits, int F) { return (int64_t)key_splits * F; }
 // Fills a.tw / a.tinfo / a.n_tinfo when the segments' packed weights are contiguous in 64-column

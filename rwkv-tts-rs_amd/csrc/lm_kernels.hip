@@ -482,7 +482,7 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
   short8 b[KSTEPS];
 #pragma unroll
   for (int t = 0; t < KSTEPS; ++t)
-    b[t] = (a.exp & 2) ? (short8){0, 0, 0, 0, 0, 0, 0, 0} : __builtin_nontemporal_load((const short8*)(wp + t * 512));
+    b[t] = __builtin_nontemporal_load((const short8*)(wp + t * 512));
   // 2) stage X slice
   constexpr int CH = KS / 8;  // 16-byte chunks per row
   if constexpr (XMODE == kXPlanes) {
@@ -494,7 +494,7 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
       const int r = c / CH, k8 = (c % CH) * 8;
       const int src = row0 + r;
       vh[u] = vl[u] = (short8){0, 0, 0, 0, 0, 0, 0, 0};
-      if (src < a.M && !(a.exp & 1)) {
+      if (src < a.M) {
         const int64_t o = (int64_t)src * sg.ldx + kbeg + k8;
         vh[u] = *(const short8*)(sg.Xhi + o);
         vl[u] = *(const short8*)(sg.Xlo + o);
@@ -521,7 +521,7 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
           const int c = threadIdx.x + u * 256;
           const int r = c / (KS / 4), k4 = (c % (KS / 4)) * 4;
           const int src = row0 + r;
-          t[pp][u] = (src < a.M && p0 + pp < a.x_nsplit && !(a.exp & 1))
+          t[pp][u] = (src < a.M && p0 + pp < a.x_nsplit)
                          ? *(const float4_*)(a.x_part + (p0 + pp) * a.x_part_stride + (int64_t)src * a.x_ld + kbeg + k4)
                          : (float4_){0.f, 0.f, 0.f, 0.f};
         }
@@ -645,15 +645,22 @@ __device__ inline void sync_wait(const int* c, int target, int* err, int code, i
   }
   __syncthreads();
 }
+// test hook (RWKVTTS_TEST_DROP_ARRIVE=n): *drop counts the arrivals still to be dropped; takes one
+__device__ inline bool take_drop(int* drop) {
+  int v = __hip_atomic_load((gint_t*)drop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  while (v > 0)
+    if (__hip_atomic_compare_exchange_strong((gint_t*)drop, &v, v - 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT))
+      return true;
+  return false;
+}
 // publish: every wave's write-through (sc1) stores drained, then ONE lane counts the workgroup in
 // (replicas > 1: lanes 0..replicas-1 of wave 0 add to one replica each, kSyncStride ints apart).
-// drop (test hook, replicas == 1 only): lane 0 skips the add once if it finds *drop set
+// drop (test hook, replicas == 1 only): lane 0 skips the add if it takes a pending drop
 __device__ inline void sync_arrive(int* c, int replicas = 1, int* drop = nullptr, int inc = 1) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (drop && threadIdx.x == 0 &&
-      __hip_atomic_exchange((gint_t*)drop, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
-    return;
+  if (drop && threadIdx.x == 0 && take_drop(drop)) return;
   if (threadIdx.x < replicas)
     __hip_atomic_fetch_add((gint_t*)(c + threadIdx.x * kSyncStride), inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -661,9 +668,18 @@ __device__ inline void sync_arrive(int* c, int replicas = 1, int* drop = nullptr
 typedef __attribute__((address_space(1))) uint64_t gu64_t;
 typedef uint64_t u64x2_ __attribute__((ext_vector_type(2)));
 __device__ inline uint32_t gran_tag(const FfnSync& sy) {
-  // (an sc1 vector load: the word changed in an earlier launch, a scalar-cache read can be stale)
+  // (an sc1 vector load: the word changed in an earlier launch, a scalar-cache read can be stale).
+  // Bit 31 set: a tag is never 0, so a zeroed granule (Engine::reset_persistent) never matches, also
+  // once the 32-bit epoch * 64 has wrapped (every 2^25 one-row passes)
   const int ep = __hip_atomic_load((gint_t*)sy.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return (uint32_t)__builtin_amdgcn_readfirstlane(ep) * 64u + (uint32_t)sy.layer;
+  return (((uint32_t)__builtin_amdgcn_readfirstlane(ep) * 64u + (uint32_t)sy.layer) & 0x7FFFFFFFu) | 0x80000000u;
+}
+// one polled granule: a relaxed agent-scope 64-bit atomic load (global_load_dwordx2 sc1). The poll
+// loops re-read granules with these only: an atomic load is re-issued on every pass (a plain load in
+// a spin loop may legally be merged or hoisted) and is single-copy atomic over its 8 bytes, so the
+// {data, tag} pair is never torn (a 16-byte load's halves carry no such guarantee)
+__device__ inline uint64_t ld_gran(const uint64_t* p) {
+  return __hip_atomic_load((const gu64_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ inline void gran_store_bits(uint64_t* p, uint32_t bits, uint32_t tag) {
   __hip_atomic_store((gu64_t*)p, ((uint64_t)tag << 32) | bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -677,7 +693,8 @@ __device__ inline void hold_until(int ticks) {
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)ticks) __builtin_amdgcn_s_sleep(2);
 }
-// handed-off bytes are read with sc1 (L1-bypassing) buffer loads only
+// handed-off bytes are read with sc1 (L1-bypassing) buffer loads only (after the hand-off's counter
+// wait: never as the polled word itself -- polls are atomic loads, sync_wait / ld_gran)
 __device__ inline u32x4_ ld_sc1_b128(__amdgpu_buffer_rsrc_t r, int off_bytes) {
   return __builtin_amdgcn_raw_buffer_load_b128(r, off_bytes, 0, 16);
 }
@@ -907,12 +924,13 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
     load_w();
     if (threadIdx.x < 64) {
       const uint32_t tag = gran_tag(sy);
-      const auto rs = wt_rsrc(sy.zgran);
+      const uint64_t* zp = sy.zgran + kbeg + 2 * lane;
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      u64x2_ q;
+      uint64_t q0, q1;
       for (;;) {
-        q = __builtin_bit_cast(u64x2_, ld_sc1_b128(rs, (kbeg + 2 * lane) * 8));
-        const bool ok = (uint32_t)(q.x >> 32) == tag && (uint32_t)(q.y >> 32) == tag;
+        q0 = ld_gran(zp);
+        q1 = ld_gran(zp + 1);
+        const bool ok = (uint32_t)(q0 >> 32) == tag && (uint32_t)(q1 >> 32) == tag;
         if (__all(ok)) break;
         __builtin_amdgcn_s_sleep(1);
         if (__builtin_amdgcn_s_memrealtime() - t0 > 5000000ull) {
@@ -920,7 +938,7 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
           break;
         }
       }
-      const uint32_t g0 = (uint32_t)q.x, g1 = (uint32_t)q.y;  // {hi | lo << 16} of channels 2l, 2l + 1
+      const uint32_t g0 = (uint32_t)q0, g1 = (uint32_t)q1;  // {hi | lo << 16} of channels 2l, 2l + 1
       *(uint32_t*)(xh + 2 * lane) = (g0 & 0xFFFFu) | (g1 << 16);
       *(uint32_t*)(xl + 2 * lane) = (g0 >> 16) | (g1 & 0xFFFF0000u);
     }
@@ -951,16 +969,8 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
       *(uint2*)(xl + (c - kbeg)) = make_uint2(l0, l1);
     }
     static_assert(C == 1024, "");
-  } else if constexpr (ROLE == 5 || ROLE == 6 || ROLE == 9) {
+  } else if constexpr (ROLE == 5 || ROLE == 6) {
     static_assert(MT == 1 && XMODE == kXPlanes, "row-fused LayerNorm: one row, planes");
-    // ROLE 9 (the FFN key role of the one-launch-per-layer form): weights at dispatch, then wait
-    // until the attention half's Wo workgroups and shift writer have published (its residual and
-    // partial slabs are this launch's: sc1 loads below)
-    if constexpr (ROLE == 9) {
-      hold_until(sy.d_k);
-      load_w();
-      sync_wait(sy.dep + kSyncStride * (blockIdx.x & (kLnReplicas - 1)), sy.dep_target, sy.err, 4096, sy.opts);
-    }
     // the row's LayerNorm (all 256 threads: thread t owns columns [4t, 4t + 4)), then this
     // K-slice's mix split into row 0 of the X image (rows 1..15 are never stored). The LayerNorm
     // inputs (L2 / MALL hits, written by the previous launch) are requested BEFORE the weight stream
@@ -975,19 +985,11 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
       for (int m = 1; m < 6; ++m)
         if (tile_mix == m) mup = L.mu[m];
     }
-    float4_ v, tp[NPL];
-    if constexpr (ROLE == 9) {
-      v = __builtin_bit_cast(float4_, ld_sc1_b128(wt_rsrc(L.h_in), c * 4));
+    float4_ v = ld4(L.h_in + c), tp[NPL];
 #pragma unroll
-      for (int p = 0; p < NPL; ++p)
-        tp[p] = __builtin_bit_cast(float4_, ld_sc1_b128(wt_rsrc(L.part + p * L.part_stride), c * 4));
-    } else {
-      v = ld4(L.h_in + c);
-#pragma unroll
-      for (int p = 0; p < NPL; ++p) tp[p] = ld4(L.part + p * L.part_stride + c);
-    }
+    for (int p = 0; p < NPL; ++p) tp[p] = ld4(L.part + p * L.part_stride + c);
     const float4_ lw = ld4(L.ln_w + c), lb = ld4(L.ln_b + c);
-    if constexpr (ROLE != 9) load_w();
+    load_w();
     // (after the weights: the token-shift row's address waits for the row descriptor)
     const int4 info = L.rows[0];
     const float4_ mu = ld4(mup + c);
@@ -1018,21 +1020,20 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
       for (int u = 0; u < PERR; ++u) xr[p][u] = (float4_){0.f, 0.f, 0.f, 0.f};
     if (wave == 0) {
       const uint32_t tag = gran_tag(sy);
-      const auto rs = wt_rsrc(sy.gran);
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       for (;;) {
         bool ok = true;
 #pragma unroll
         for (int p = 0; p < NX; ++p) {
-          // two granules per 16-byte load, taken apart as 64-bit halves {data | tag << 32}
-          // (element-wise extraction of the 32-bit vector was miscompiled here: data elements 0
-          // and 2 came out equal)
-          const u64x2_ q0 = __builtin_bit_cast(u64x2_, ld_sc1_b128(rs, (p * sy.gran_ld + kbeg + 4 * lane) * 8));
-          const u64x2_ q1 = __builtin_bit_cast(u64x2_, ld_sc1_b128(rs, (p * sy.gran_ld + kbeg + 4 * lane + 2) * 8));
-          xr[p][0] = (float4_){__builtin_bit_cast(float, (uint32_t)q0.x), __builtin_bit_cast(float, (uint32_t)q0.y),
-                               __builtin_bit_cast(float, (uint32_t)q1.x), __builtin_bit_cast(float, (uint32_t)q1.y)};
-          ok = ok && (uint32_t)(q0.x >> 32) == tag && (uint32_t)(q0.y >> 32) == tag &&
-               (uint32_t)(q1.x >> 32) == tag && (uint32_t)(q1.y >> 32) == tag;
+          // four granules {data | tag << 32} per split, each one atomic 64-bit load (ld_gran)
+          const uint64_t* gp = sy.gran + (int64_t)p * sy.gran_ld + kbeg + 4 * lane;
+          uint64_t q[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) q[e] = ld_gran(gp + e);
+          xr[p][0] = (float4_){__builtin_bit_cast(float, (uint32_t)q[0]), __builtin_bit_cast(float, (uint32_t)q[1]),
+                               __builtin_bit_cast(float, (uint32_t)q[2]), __builtin_bit_cast(float, (uint32_t)q[3])};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) ok = ok && (uint32_t)(q[e] >> 32) == tag;
         }
         if (__all(ok)) break;
         __builtin_amdgcn_s_sleep(1);
@@ -1060,7 +1061,7 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
   // 3) X -> LDS (rows past M: zeros in the persistent roles (never fetched), a copy of row M-1 in the
   // plain launches; an MFMA output row depends on its own X row only, and those rows' outputs are not
   // stored)
-  if constexpr (ROLE == 5 || ROLE == 6 || ROLE == 8 || ROLE == 9 || ROLE == 10) {
+  if constexpr (ROLE == 5 || ROLE == 6 || ROLE == 8 || ROLE == 10) {
     // (staged by the row-fused LayerNorm / the granule sweep above)
   } else if constexpr (XMODE == kXPlanes) {
 #pragma unroll
@@ -1212,7 +1213,7 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
     }
     return v;
   };
-  if (((ROLE == 6 || ROLE == 9) && sy.gran) || (ROLE == 5 && sy.rkv_gran)) {
+  if (ROLE == 6 && sy.gran) {
     // granule form: row 0's 64 columns, one {f32, tag} granule per element (lanes 0..15 of each
     // wave hold row 0: g == 0, j == 0)
     if (g == 0 && col < Nn) gran_store(sy.gran + (int64_t)split * sy.gran_ld + col_off + col, result(0, 0), gran_tag(sy));
@@ -1258,10 +1259,7 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
   }
   if constexpr (ROLE != 0) sync_stamp(sy, 2);
   if constexpr (ROLE == 1) sync_arrive(sy.cnt + kSyncStride * (kLnReplicas + tile / sy.key_group));
-  if constexpr (ROLE == 8) {  // (one launch per layer) the FFN key workgroups wait for the Wo slabs
-    if (sy.wo_done) sync_arrive(sy.wo_done, kLnReplicas);
-  }
-  if constexpr (ROLE == 6 || ROLE == 9) {  // K-slice counter (replica 0; not in the granule form) and key-done (lane 1)
+  if constexpr (ROLE == 6) {  // K-slice counter (replica 0; not in the granule form) and key-done (lane 1)
     if (!sy.gran) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0 && !sy.gran)
@@ -1276,15 +1274,13 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
     if (c0 < 3 * sy.C) sync_arrive(sy.cnt + kSyncStride * (kAttHead + ((c0 % sy.C) >> 6)), 1, sy.drop);
     else sync_arrive(sy.cnt + kSyncStride * kAttLora, kLnReplicas);
   }
-  if constexpr (ROLE == 5) {  // as ROLE 3 (not with the rkv granules), plus rkv-done (lane 8) for the shift writer
+  if constexpr (ROLE == 5) {  // as ROLE 3, plus rkv-done (lane 8) for the shift writer
     const int c0 = col_off + (tile - tstart) * 64;
-    if (!sy.rkv_gran) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (sy.rkv_gran) {
-    } else if (c0 < 3 * sy.C) {
-      // (test hook as in sync_arrive: the first workgroup to find *drop set skips its arrival)
-      if (threadIdx.x == 0 &&
-          !(sy.drop && __hip_atomic_exchange((gint_t*)sy.drop, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0))
+    if (c0 < 3 * sy.C) {
+      // (test hook as in sync_arrive: a workgroup that takes a pending drop skips its arrival)
+      if (threadIdx.x == 0 && !(sy.drop && take_drop(sy.drop)))
         __hip_atomic_fetch_add((gint_t*)(sy.cnt + kSyncStride * (kAttHead + ((c0 % sy.C) >> 6))), 1,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else if (threadIdx.x < kLnReplicas) {
@@ -1316,7 +1312,7 @@ __global__ __launch_bounds__(256) void k_gemm2_lnrow(GemmArgs a, LnMixArgs lo) {
 bool launch_gemm_lnrow(const GemmArgs& a, const LnMixArgs& lo, hipStream_t st) {
   // one row, the head's shape: one segment of 16-bit planes, 512-wide K-slices, no XCD remap;
   // ln_out's: C = 1024, 16 partial slabs, no row remap beyond row 0
-  if (a.M != 1 || a.nseg != 1 || a.kslice != 512 || a.xmode != kXPlanes || a.q_fmt || a.stamps || a.exp ||
+  if (a.M != 1 || a.nseg != 1 || a.kslice != 512 || a.xmode != kXPlanes || a.q_fmt || a.stamps ||
       a.allow_xmap || a.xalign > 0 || lo.C != 1024 || lo.n_part != 16 || lo.n_mix != 1 || lo.h_out != nullptr ||
       a.f16 != lo.f16)
     return false;
@@ -1446,7 +1442,7 @@ __global__ __launch_bounds__(256, 2) void k_wkv(WkvArgs a) {
   float S[16];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const float4_ v4 = (a.exp & 4) ? (float4_){0.f, 0.f, 0.f, 0.f} : *(const float4_*)(Sg + q * 4);
+    const float4_ v4 = *(const float4_*)(Sg + q * 4);
     S[q * 4 + 0] = v4[0]; S[q * 4 + 1] = v4[1]; S[q * 4 + 2] = v4[2]; S[q * 4 + 3] = v4[3];
   }
   const int Dall = a.Dw + a.Da + a.Dv + a.Dg;
@@ -1457,7 +1453,7 @@ __global__ __launch_bounds__(256, 2) void k_wkv(WkvArgs a) {
 #pragma unroll
     for (int p = 0; p < MAXP; ++p) {
       const float* pp = prow + p * a.part_stride;
-      const bool on = p < a.n_part && !(a.exp & 2);
+      const bool on = p < a.n_part;
       hp0[p] = (on && tid < Dtot) ? pp[3 * C + tid] : 0.f;
       hp1[p] = (on && tid + 256 < Dtot) ? pp[3 * C + tid + 256] : 0.f;
       rp[p] = on ? pp[co] : 0.f;
@@ -1646,17 +1642,16 @@ static void launch_gemm_t(const GemmArgs& a, dim3 grid, hipStream_t st) {
   // generic fallback (other slab counts) and the debug-stamp build
   // (quantised weights exist only in k_gemm2: debug stamps / experiments are ignored for them)
   const bool nx_ok = a.x_nsplit == 4 || a.x_nsplit == 2 || (a.x_nsplit == 1 && a.q_fmt);
-  if ((a.xmode == kXPlanes || nx_ok) && ((a.stamps == nullptr && a.exp == 0) || a.q_fmt)) {
+  if ((a.xmode == kXPlanes || nx_ok) && (a.stamps == nullptr || a.q_fmt)) {
     const int ms = a.nseg > 1 ? (a.n_tinfo > 0 ? 2 : 1) : 0;
     GemmArgs b = a;
     b.xmap = 0;
-    static const bool no_xmap = getenv("RWKVTTS_NO_XMAP") != nullptr;  // A/B timing switch
-    if (grid.z == 1 && a.xalign > 0 && !no_xmap) {
+    if (grid.z == 1 && a.xalign > 0) {
       b.xmap = 2;
       b.ntiles = (int)grid.x;
       const int groups = ((int)grid.x + a.xalign - 1) / a.xalign;
       grid = dim3(8 * ((groups + 7) / 8) * a.xalign * a.k_split);
-    } else if (grid.z == 1 && a.allow_xmap && (a.k_split % 8 == 0 || 8 % a.k_split == 0) && !no_xmap) {
+    } else if (grid.z == 1 && a.allow_xmap && (a.k_split % 8 == 0 || 8 % a.k_split == 0)) {
       b.xmap = 1;
       b.ntiles = (int)grid.x;
       if (a.k_split >= 8) {
@@ -1666,15 +1661,12 @@ static void launch_gemm_t(const GemmArgs& a, dim3 grid, hipStream_t st) {
         grid = dim3(8 * b.tiles_per_xcd);
       }
     }
-    // prefill steps: several row groups per workgroup (weights loaded once); RWKVTTS_GEMM_RPW
-    // sets the groups per workgroup (1: one each), default: as many as keep >= 4 workgroups per CU
+    // prefill steps: several row groups per workgroup (weights loaded once), as many as keep >= 4
+    // workgroups per CU (measured over 1 / 2 / 4 / 8 / 10 / 20 / 40 groups per workgroup on a
+    // 1280-row step: 9.3 / 8.5 / 8.3 / 8.1 / 8.1 / 8.0 / 10.0 ms)
     if (grid.z > 1 && !a.q_fmt) {
-      static const int rpw_env = getenv("RWKVTTS_GEMM_RPW") ? atoi(getenv("RWKVTTS_GEMM_RPW")) : 0;
-      int rpw = rpw_env;
-      if (rpw <= 0) {
-        const int per_group = (int)(grid.x * grid.y);
-        rpw = std::max(1, (int)grid.z * per_group / 1024);
-      }
+      const int per_group = (int)(grid.x * grid.y);
+      const int rpw = std::max(1, (int)grid.z * per_group / 1024);
       grid.z = (grid.z + rpw - 1) / rpw;
     }
 #define G2(F, XM, NX_, MS_)                                                               \
@@ -1734,44 +1726,22 @@ void launch_relu2_planes(const float* part, int nx, int64_t pstride, int ld, int
 // (the caller runs the three launches). ln / key / val: the three launches' arguments as built by
 // the engine; cnt / cnt_prev: this and the previous layer's counter blocks ((1 + kFfnSlices) x
 // kSyncStride ints, zero before this layer's first use); err: the give-up word.
-// Holds of the dispatch-time prefetches (FfnSync::d_w / d_late / d_s). Default: the rkv / key
-// weight streams wait 1 µs, so the LayerNorm rows at the head of each persistent launch load their
-// slabs with less traffic beside them while the weights still land before the LayerNorm ends
-// (same-box decode A/B at B = 32: 771-776 -> 756-764 µs per step, tokens unchanged; holding the
-// value / Wo weights or the WKV state is slower, profiles/r04h_pf_hold_ab.txt).
-// RWKVTTS_PF_HOLD="rkv,wo,state,value[,key]" (10 ns ticks; key defaults to rkv) overrides; read once per process (A/B switch).
-struct PfHolds {
-  int h[5];
-};
+// Holds of the dispatch-time prefetches (FfnSync::d_w / d_k / d_late / d_s / d_v, 10 ns ticks).
+// The rkv / key weight streams wait 1 us, so the LayerNorm rows at the head of each persistent
+// launch load their slabs with less traffic beside them while the weights still land before the
+// LayerNorm ends (same-box decode A/B at B = 32: 771-776 -> 756-764 us per step, tokens unchanged;
+// holding the value / Wo weights or the WKV state is slower, profiles/r04h_pf_hold_ab.txt).
+constexpr int kHoldRkv = 100, kHoldKey = 100;
 // The row-fused (one-row) forms hold the Wo and the FFN value weight streams instead (the rkv /
 // key ones feed the first GEMM there): 4 / 1 us (same-box B = 1 A/B: 525 -> 513-517 us per step,
-// round 5). RWKVTTS_PF_HOLD1="wo,value" overrides.
-struct PfHolds1 {
-  int wo, val;
-};
-static const PfHolds1& prefetch_holds1() {
-  static const PfHolds1 ph = [] {
-    PfHolds1 p{400, 100};
-    if (const char* e = getenv("RWKVTTS_PF_HOLD1")) sscanf(e, "%d,%d", &p.wo, &p.val);
-    return p;
-  }();
-  return ph;
-}
+// round 5, profiles/r05u_holds1_ab.txt).
+constexpr int kHold1Wo = 400, kHold1Value = 100;
 static void prefetch_holds(FfnSync& sy) {
-  // parsed once, by a thread-safe static initialiser (engines on several devices may launch from
-  // their owner threads at the same time)
-  static const PfHolds ph = [] {
-    PfHolds p{{100, 0, 0, 0, 100}};
-    if (const char* e = getenv("RWKVTTS_PF_HOLD"))
-      if (sscanf(e, "%d,%d,%d,%d,%d", &p.h[0], &p.h[1], &p.h[2], &p.h[3], &p.h[4]) < 5) p.h[4] = p.h[0];
-    return p;
-  }();
-  const int* h = ph.h;
-  sy.d_w = h[0];
-  sy.d_late = h[1];
-  sy.d_s = h[2];
-  sy.d_v = h[3];
-  sy.d_k = h[4];
+  sy.d_w = kHoldRkv;
+  sy.d_late = 0;
+  sy.d_s = 0;
+  sy.d_v = 0;
+  sy.d_k = kHoldKey;
 }
 
 struct FfnPrep {
@@ -1785,7 +1755,7 @@ static bool prep_ffn_persist(const LnMixArgs& ln, const GemmArgs& key, const Gem
   if (ln.C != 1024 || !ln.shift || ln.n_mix != 1 || ln.n_part != 8 || ln.emb || R < 1 || R > 32 ||
       key.xmode != kXPlanes || val.xmode != kXRelu2 || val.x_nsplit != 4 || key.kslice != 256 ||
       val.kslice != 256 || key.M != R || val.M != R || key.nseg != 1 || val.nseg != 1 || key.q_fmt || val.q_fmt ||
-      key.stamps || val.stamps || key.exp || val.exp || key.xalign <= 0 || key.f16 != val.f16 || key.f16 != ln.f16 ||
+      key.stamps || val.stamps || key.xalign <= 0 || key.f16 != val.f16 || key.f16 != ln.f16 ||
       cnt == cnt_prev)
     return false;
   const int kt = (key.seg[0].N + 63) / 64, vt = (val.seg[0].N + 63) / 64;
@@ -1837,7 +1807,7 @@ static bool ffn_setup(const LnMixArgs& ln, const GemmArgs& key, const GemmArgs& 
     P.sy.n_ln_blocks = 0;
     P.sy.d_k = 0;
     P.sy.opts &= ~1;  // (no LayerNorm rows for the value workgroups to wait for)
-    P.sy.d_v = prefetch_holds1().val;
+    P.sy.d_v = kHold1Value;
     n_fix = 1;
     // the granule key -> value hand-off: four key splits (the value role's NX), one segment
     if (gran && epoch && key.k_split == 4 && key.nseg == 1 && ln.layer < 64) {
@@ -2582,80 +2552,11 @@ __device__ __attribute__((always_inline)) void wkv6_body(const WkvArgs& a, const
 #pragma unroll
     for (int u = 0; u < 9; ++u) lw[u] = pl[u * 256 + t];
     load_state(slot);
-    if constexpr (ROLE == 3) {
-      // rkv -> WKV granules (one row): each thread polls a few of the granules the workgroup needs
-      // -- the r / k / v of its channel in split qq, and two-granule pieces of the LoRA hidden
-      // columns -- until every wave sees this pass's tag (votes through LDS, two slots), then the
-      // values go through LDS into load_parts' register layout (the same numbers, the same sums)
-      __shared__ float s_rkv[NP][3][N];
-      __shared__ float s_hidp[NP][DALL];
-      __shared__ int s_ok[2][4];
-      constexpr int NHL = NP * DALL / 2;  // 16-byte hidden loads (two granules each)
-      const uint32_t tag = gran_tag(sy);
-      const auto rs = wt_rsrc(sy.gran);
-      const int ld = sy.gran_ld;
-      float gr_v[3], gh_v[3][2];
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      for (int round = 0;; round ^= 1) {
-        bool ok = true;
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {
-          const uint64_t g = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(
-                                                              rs, (qq * ld + q * C + c) * 8, 0, 16));
-          gr_v[q] = __builtin_bit_cast(float, (uint32_t)g);
-          ok = ok && (uint32_t)(g >> 32) == tag;
-        }
-#pragma unroll
-        for (int u = 0; u < 3; ++u) {
-          const int j = t + 256 * u;
-          if (j < NHL) {
-            const int p = j / (DALL / 2), col = 3 * C + 2 * (j % (DALL / 2));
-            const u64x2_ g = __builtin_bit_cast(u64x2_, ld_sc1_b128(rs, (p * ld + col) * 8));
-            gh_v[u][0] = __builtin_bit_cast(float, (uint32_t)g.x);
-            gh_v[u][1] = __builtin_bit_cast(float, (uint32_t)g.y);
-            ok = ok && (uint32_t)(g.x >> 32) == tag && (uint32_t)(g.y >> 32) == tag;
-          }
-        }
-        const bool wok = __all(ok);
-        if (lane == 0) s_ok[round][wave] = wok ? 1 : 0;
-        __syncthreads();
-        if (s_ok[round][0] && s_ok[round][1] && s_ok[round][2] && s_ok[round][3]) break;
-        __builtin_amdgcn_s_sleep(1);
-        if (__builtin_amdgcn_s_memrealtime() - t0 > 5000000ull) {
-          if (t == 0) __hip_atomic_fetch_or((gint_t*)sy.err, 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < 3; ++q) s_rkv[qq][q][i] = gr_v[q];
-#pragma unroll
-      for (int u = 0; u < 3; ++u) {
-        const int j = t + 256 * u;
-        if (j < NHL) {
-          const int p = j / (DALL / 2), hc = 2 * (j % (DALL / 2));
-          s_hidp[p][hc] = gh_v[u][0];
-          s_hidp[p][hc + 1] = gh_v[u][1];
-        }
-      }
-      __syncthreads();
-#pragma unroll
-      for (int p = 0; p < NP; ++p) {
-        rp[p] = s_rkv[p][0][i];
-        kp[p] = s_rkv[p][1][i];
-        vp[p] = s_rkv[p][2][i];
-        hp[p] = *(const float4_*)&s_hidp[p][hid_thread ? 4 * t : 0];
-      }
-      sync_stamp(sy, 1);
-      vf = a.layer > 0 ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                     wt_rsrc(a.v_first + (int64_t)r_begin * a.ldv), c * 4, 0, 16))
-                       : 0.f;
-    } else {
     sync_wait(sy.cnt + kSyncStride * (kAttHead + h), sy.head_target, sy.err, 16, sy.opts);
     sync_wait(sy.cnt + kSyncStride * (kAttLora + (blockIdx.x & (kLnReplicas - 1))), sy.lora_target, sy.err, 32,
               sy.opts);
     sync_stamp(sy, 1);
     load_parts(r_begin);
-    }
   } else {
   load_parts(spec);
 #pragma unroll
@@ -2794,7 +2695,7 @@ __device__ __attribute__((always_inline)) void wkv6_body(const WkvArgs& a, const
     const float mean = ((s_red[2][0] + s_red[2][1]) + (s_red[2][2] + s_red[2][3])) * (1.0f / N);
     const float var =
         fmaxf(((s_red[3][0] + s_red[3][1]) + (s_red[3][2] + s_red[3][3])) * (1.0f / N) - mean * mean, 0.f);
-    if constexpr (ROLE == 2 || ROLE == 3) {
+    if constexpr (ROLE == 2) {
       // granule form: the channel's split as ONE granule {hi | lo << 16, tag} (same expression
       // and threads as below, so the same bits) -- the Wo workgroups poll these directly
       if (qq == 0) {
@@ -2894,8 +2795,7 @@ __global__ __launch_bounds__(256, RWKVTTS_ATT_WPC) void k_att_persist(LnMixArgs 
     else gemm2_body<2, 8, kXPlanes, F16, 1, 2, false, 3>(ga, b % sy.rkv_tiles, b / sy.rkv_tiles, sy);
   } else if ((b -= sy.n_key) < sy.n_wkv) {
     if constexpr (FUSED && !EMB) {
-      if (sy.rkv_gran) wkv6_body<F16, 3>(wa, b, 0, sy);
-      else if (sy.gran) wkv6_body<F16, 2>(wa, b, 0, sy);
+      if (sy.gran) wkv6_body<F16, 2>(wa, b, 0, sy);
       else wkv6_body<F16, 1>(wa, b, 0, sy);
     } else {
       wkv6_body<F16, 1>(wa, b, 0, sy);
@@ -2931,11 +2831,11 @@ static bool prep_att_persist(const LnMixArgs& ln, const GemmArgs& rkv, const Wkv
   const int lora_tiles = rkv_tiles - 3 * ln.C / 64;
   if (ln.C != 1024 || H != 16 || !ln.shift || ln.n_mix != 6 || ln.n_part != (emb ? 0 : 16) || R < 1 || R > 32 ||
       rkv.xmode != kXPlanes || rkv.n_tinfo != rkv_tiles || rkv.kslice != 256 || rkv.k_split != 4 || rkv.M != R ||
-      rkv.q_fmt || rkv.stamps || rkv.exp || rkv.xalign || lora_tiles < 1 || rkv.ldo != wkv.ldp ||
+      rkv.q_fmt || rkv.stamps || rkv.xalign || lora_tiles < 1 || rkv.ldo != wkv.ldp ||
       wkv.perm != 2 || wkv.n_part != 4 || wkv.multi_row || !wkv.allow_xmap || wkv.n_seg != R || wkv.stamps ||
-      wkv.exp || wkv.Dw != 64 || wkv.Da != 64 || wkv.Dv != 32 || wkv.Dg != 128 ||
+      wkv.Dw != 64 || wkv.Da != 64 || wkv.Dv != 32 || wkv.Dg != 128 ||
       wo.xmode != kXPlanes || wo.kslice != 128 || wo.k_split != 8 || wo.nseg != 1 || wo.M != R || wo.q_fmt ||
-      wo.stamps || wo.exp || (wo.seg[0].N + 63) / 64 != 16 ||
+      wo.stamps || (wo.seg[0].N + 63) / 64 != 16 ||
       rkv.f16 != ln.f16 || wo.f16 != ln.f16 || wkv.f16 != ln.f16 || cnt == cnt_prev)
     return false;
   LnMixArgs& l = P.l;
@@ -2985,22 +2885,15 @@ static bool att_setup(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs& w
   if (fused) {
     P.sy.n_ln_blocks = 0;
     P.sy.d_w = 0;  // (the hold only kept the weight streams off the LayerNorm rows' loads)
-    P.sy.d_late = prefetch_holds1().wo;
+    P.sy.d_late = kHold1Wo;
     n_fix = 1;
-    // the granule hand-offs (rkv -> WKV, WKV -> Wo): four rkv splits (the WKV's NP), 64-channel
-    // heads, 128-channel Wo K-slices (its granule role's KS)
-    if (gran && epoch && rkv.k_split == 4 && wkv.C == 16 * 64 && wo.k_split == 8 && ln.layer < 64 &&
-        wkv.ldp >= 3 * wkv.C + 288) {
+    // the granule hand-off WKV -> Wo: 64-channel heads, 128-channel Wo K-slices (its granule role's KS)
+    if (gran && epoch && wkv.C == 16 * 64 && wo.k_split == 8 && ln.layer < 64) {
       P.sy.gran = gran;
-      P.sy.zgran = gran + (int64_t)4 * wkv.ldp;
-      P.sy.gran_ld = wkv.ldp;
+      P.sy.zgran = gran;
+      P.sy.gran_ld = 0;
       P.sy.epoch = epoch;
       P.sy.layer = ln.layer;
-      // rkv -> WKV as granules too (RWKVTTS_RKV_GRAN=1; the WKV role's quad-split sweep): measured
-      // slower than the counter hand-off (B = 1: 530-535 vs 513-517 us per step; the WKV workgroups
-      // see the last granule 1.7 us after the last rkv workgroup ends, the counters 0.4 us), off
-      static const int rkv_gran = getenv("RWKVTTS_RKV_GRAN") ? atoi(getenv("RWKVTTS_RKV_GRAN")) : 0;
-      P.sy.rkv_gran = rkv_gran != 0;
     }
   }
   return true;
@@ -3036,92 +2929,8 @@ bool launch_att_persist(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs&
   return true;
 }
 
-// ------------------------------------------------------------------------------------
-// layer1_persist: one decode row, layers > 0 -- the row-fused, granule-hand-off attention half and
-// FFN half of a layer as ONE launch:
-//   [0, n_rkv)            rkv + LoRA-down (ROLE 5: own LayerNorm 1)
-//   [+, +n_wkv)           WKV (z granules out)
-//   [+, +n_wo)            Wo (ROLE 8: z granules in), then count into wo_done (8 replicas)
-//   +1                    attention shift writer (residual h1 + token shift), counts into wo_done
-//   [+, +n_key)           FFN key (ROLE 9: weights at dispatch, waits for wo_done, own LayerNorm 2
-//                         from this launch's h1 and Wo slabs by sc1 loads, granules out)
-//   [+, +n_val)           FFN value (ROLE 7: key granules in)
-//   +1                    FFN shift writer (residual h0 + token shift, sc1 loads)
-// The FFN workgroups are dispatched as attention workgroups retire, so their weight streams run
-// beside the attention chain's tail instead of after a launch boundary. Every dependency points to
-// a lower block index. Outputs: the two launches', bit for bit.
-template <bool F16>
-__global__ __launch_bounds__(256, RWKVTTS_ATT_WPC) void k_layer1_persist(LnMixArgs ln, GemmArgs ga, WkvArgs wa,
-                                                                          GemmArgs1 go, LnMixArgs lf, GemmArgs1 ka,
-                                                                          GemmArgs1 va, FfnSync sy, FfnSync sf) {
-  int b = blockIdx.x;
-  tl_begin(ln.tl);
-  const int n_att = sy.n_key + sy.n_wkv + 16 * go.k_split + 1;
-  if (b < n_att) {
-    if (b < sy.n_key) {
-      gemm2_body<1, 8, kXPlanes, F16, 1, 2, false, 5>(ga, b % sy.rkv_tiles, b / sy.rkv_tiles, sy, &ln);
-    } else if ((b -= sy.n_key) < sy.n_wkv) {
-      if (sy.rkv_gran) wkv6_body<F16, 3>(wa, b, 0, sy);
-      else wkv6_body<F16, 2>(wa, b, 0, sy);
-    } else if ((b -= sy.n_wkv) < 16 * go.k_split) {
-      gemm2_body<1, 4, kXPlanes, F16, 1, 0, false, 8>(go, b, 0, sy);
-    } else {  // attention shift writer
-      if (threadIdx.x < sy.n_prev) sy.cnt_prev[threadIdx.x * kSyncStride] = 0;
-      sync_wait(sy.cnt + kSyncStride * kAttRkvDone, sy.n_key, sy.err, 2048, sy.opts);
-      ln1024_body<F16, 1, 0, 16>(ln, 0);
-      sync_arrive(sy.wo_done, kLnReplicas);
-    }
-  } else if ((b -= n_att) < sf.n_key) {
-    gemm2_body<1, 8, kXPlanes, F16, 1, 0, false, 9>(ka, b, 0, sf, &lf);
-  } else if ((b -= sf.n_key) < sf.n_val) {
-    gemm2_body<1, 8, kXRelu2, F16, 4, 0, false, 7>(va, b, 0, sf);
-  } else {  // FFN shift writer (its residual and slabs are this launch's: sc1 loads)
-    if (threadIdx.x < sf.n_prev) sf.cnt_prev[threadIdx.x * kSyncStride] = 0;
-    sync_wait(sf.cnt + kSyncStride * kFfnKeyDone, sf.n_key, sf.err, 1024, sf.opts);
-    ln1024_body<F16, 1, 0, 8, false, true>(lf, 0);
-  }
-  tl_end(ln.tl);
-}
-
-bool launch_layer1_persist(const LnMixArgs& ln, const GemmArgs& rkv, const WkvArgs& wkv, const GemmArgs& wo,
-                           const LnMixArgs& lf, const GemmArgs& key, const GemmArgs& val, int* acnt, int* acnt_prev,
-                           int* fcnt, int* fcnt_prev, int* err, int H, hipStream_t st, int aopts, int fopts,
-                           uint64_t* agran, uint64_t* fgran, const int* epoch) {
-  AttPrep A;
-  FfnPrep F;
-  int na = 0, nf = 0;
-  if (!att_setup(ln, rkv, wkv, wo, acnt, acnt_prev, err, 1, H, nullptr, aopts, nullptr, true, nullptr, agran, epoch,
-                 A, na) ||
-      !ffn_setup(lf, key, val, fcnt, fcnt_prev, err, 1, nullptr, fopts, true, fgran, epoch, F, nf))
-    return false;
-  // both halves in their one-row form with the granule hand-offs; the FFN K-slice counters are then
-  // unused and carry the attention half's "published" count (8 replicas)
-  if (na != 1 || nf != 1 || !A.sy.gran || !F.sy.gran || ln.emb != nullptr || wo.nseg != 1 || key.nseg != 1 ||
-      val.nseg != 1)
-    return false;
-  int* wo_done = fcnt + kSyncStride * kLnReplicas;
-  A.sy.wo_done = wo_done;
-  // (RWKVTTS_L1_KHOLD: hold the FFN key weight streams of the workgroups resident at dispatch;
-  // 4 / 7 / 10 us measured slower, 526 -> 540 / 554 / 592 us per step at B = 1)
-  static const int khold = getenv("RWKVTTS_L1_KHOLD") ? atoi(getenv("RWKVTTS_L1_KHOLD")) : 0;
-  F.sy.d_k = khold;
-  F.sy.dep = wo_done;
-  F.sy.dep_target = 16 * wo.k_split + 1;
-  static_assert(kFfnSlices >= kLnReplicas, "the Wo-done replicas live in the K-slice counters");
-  const GemmArgs1 go1 = gemm_args1(A.gw), ka1 = gemm_args1(F.ka), va1 = gemm_args1(F.va);
-  static_assert(sizeof(LnMixArgs) * 2 + sizeof(GemmArgs) + sizeof(WkvArgs) + 3 * sizeof(GemmArgs1) +
-                        2 * sizeof(FfnSync) <= 4096, "k_layer1_persist's arguments must fit 4 KB");
-  const int n_att = A.sy.n_key + A.sy.n_wkv + 16 * wo.k_split + 1;
-  const dim3 grid(n_att + F.sy.n_key + F.nv + 1);
-  const size_t lds = (size_t)2 * 16 * (8 * 32 + 8) * 2 * 2;
-  if (ln.f16) RT_LAUNCH((k_layer1_persist<true>), grid, dim3(256), lds, st, A.l, A.ga, A.wa, go1, F.l, ka1, va1, A.sy, F.sy);
-  else RT_LAUNCH((k_layer1_persist<false>), grid, dim3(256), lds, st, A.l, A.ga, A.wa, go1, F.l, ka1, va1, A.sy, F.sy);
-  return true;
-}
-
 int wkv_perm_layout(int Dw, int Da, int Dv, int Dg, int n_part, int max_slots, int variant) {
   if (!(Dw == 64 && Da == 64 && Dv == 32 && Dg == 128 && n_part == 4)) return 0;
-  if (const char* e = getenv("RWKVTTS_WKV_LAYOUT")) variant = atoi(e);  // A/B timing override
   if (variant == 1 || variant == 2) return variant;
   // auto: k_wkv6 (measured, timeline of a graph-replayed 32-slot step: 4.85 vs 5.33 us per
   // launch once its loads are issued in need order and the XCD-aware grid keeps a head's
@@ -3132,9 +2941,8 @@ int wkv_perm_layout(int Dw, int Da, int Dv, int Dg, int n_part, int max_slots, i
 int launch_wkv(const WkvArgs& a, int n_seg, int H, hipStream_t st) {
   const dim3 grid(n_seg, H);
   if (a.Dw == 64 && a.Da == 64 && a.Dv == 32 && a.Dg == 128 && a.n_part == 4 && (a.perm == 1 || a.perm == 2)) {
-    static const bool no_xmap = getenv("RWKVTTS_NO_XMAP") != nullptr;  // A/B timing switch
     WkvArgs b = a;
-    b.xmap = (H % 8 == 0 && a.allow_xmap && !no_xmap) ? 1 : 0;
+    b.xmap = (H % 8 == 0 && a.allow_xmap) ? 1 : 0;
     b.n_seg = n_seg;
     const dim3 g = b.xmap ? dim3(n_seg * H) : grid;
     if (a.perm == 2) {

@@ -543,6 +543,7 @@ void Worker::run(rwkvtts_engine_desc desc, const void* w, size_t bytes) {
     rc = eng.serve(*this);
     progress(eng);
     if (rc != RWKVTTS_OK && eng.take_recovered()) {
+      persistent = eng.persistent() ? 1 : 0;  // (0 once the engine left the persistent forms)
       // a persistent hand-off timed out: serve failed the unit's jobs (dynamic_batch_manager.rs:387-392:
       // a failed inference fails its own requests) and reset the engine, which keeps serving its inbox
       fprintf(stderr, "rwkvtts manager: engine %d (device %d): %s\n", idx_, desc.device, rwkvtts_last_error());

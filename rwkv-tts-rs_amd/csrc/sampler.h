@@ -68,12 +68,12 @@ struct AdvanceArgs {
   int n_rows;
   unsigned long long* tl;  // debug timeline slot (null in production)
   int cert;              // set by launch_advance: 1 certified fast path allowed (sample_cert)
-  uint64_t* stamps;      // debug: [rows][16] s_memtime phase stamps (RWKVTTS_ADV_STAMPS; null in production)
+  uint64_t* stamps;      // debug: [rows][16] s_memtime phase stamps (RWKVTTS_DEBUG_STAMPS adv=; null in production)
 };
 
 size_t wide_scratch_bytes(int n);
 void launch_sample_rows(const SampleRowArgs& a, int rows, hipStream_t st);
-// cert_override: -1 = RWKVTTS_SAMPLER_EXACT decides; 0 = exact walk; 1 = certified fast path allowed
-int launch_advance(const AdvanceArgs& a, hipStream_t st, int cert_override = -1);
+// cert: 1 = the certified fast path allowed (the default), 0 = the exact walk always
+int launch_advance(const AdvanceArgs& a, hipStream_t st, int cert = 1);
 
 }  // namespace rwkvtts

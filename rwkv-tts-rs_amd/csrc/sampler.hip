@@ -1939,11 +1939,9 @@ __global__ __launch_bounds__(kSampleThreads, 2) void k_advance(AdvanceArgs a) {
   tl_end(a.tl);
 }
 
-int launch_advance(const AdvanceArgs& a0, hipStream_t st, int cert_override) {
+int launch_advance(const AdvanceArgs& a0, hipStream_t st, int cert) {
   AdvanceArgs a = a0;
-  // RWKVTTS_SAMPLER_EXACT=1: always walk the exact sequential sum (A/B switch for sample_cert)
-  static const bool exact = getenv("RWKVTTS_SAMPLER_EXACT") != nullptr;
-  a.cert = cert_override >= 0 ? cert_override : (exact ? 0 : 1);
+  a.cert = cert;  // 0: always walk the exact sequential sum (RWKVTTS_FORM_EXACT_SAMPLER)
   RT_LAUNCH(k_advance, dim3(a.n_rows), dim3(kSampleThreads), smem_bytes<kSampleThreads>(RWKVTTS_EOS_TOKEN + 1),
                      st, a);
   return a.n_rows;

@@ -11,6 +11,26 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # RWKVTTS_LIB: an alternative build of the same library (A/B timing tools only)
 LIB_PATH = os.environ.get("RWKVTTS_LIB") or os.path.join(_HERE, "librwkvtts.so")
 
+
+def build_id() -> str:
+    """Identity of the in-tree library's build: sha256 over the sources it is built from
+    (csrc/*.hip, *.cpp, *.h, the Makefile and include/*.h, in name order), first 16 hex digits.
+    Profile summaries under profiles/ carry it (tools/), so bench.py cites only summaries that were
+    measured on the library it runs."""
+    import glob
+    import hashlib
+    csrc = os.path.join(_HERE, "..", "csrc")
+    inc = os.path.join(_HERE, "..", "..", "include")
+    files = sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.cpp")) +
+                   glob.glob(os.path.join(csrc, "*.h")) + [os.path.join(csrc, "Makefile")] +
+                   glob.glob(os.path.join(inc, "*.h")), key=os.path.basename)
+    h = hashlib.sha256()
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
 EOS_TOKEN = 8192
 TAG_0, TAG_1, TAG_2 = 8193, 8194, 8195
 GLOBAL_TOKEN_OFFSET = 8196
@@ -35,7 +55,16 @@ class EngineDesc(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("max_slots", ctypes.c_int32),
                 ("token_chunk_size", ctypes.c_int32), ("use_graphs", ctypes.c_int32),
                 ("wkv_variant", ctypes.c_int32), ("quant_layers", ctypes.c_int32),
-                ("quant_type", ctypes.c_int32)]
+                ("quant_type", ctypes.c_int32), ("forms", ctypes.c_uint32)]
+
+
+# rwkvtts_engine_desc.forms (include/rwkvtts.h RWKVTTS_FORM_*): each bit switches one fused decode form
+# back to the launches it replaces (bitwise-equal outputs; verification and A/B timing only)
+FORM_SEPARATE_ATT, FORM_SEPARATE_FFN, FORM_LN_ROWS, FORM_SLAB_HANDOFF = 1, 2, 4, 8
+FORM_SEPARATE_LNOUT, FORM_SEPARATE_EMBED, FORM_EXACT_SAMPLER = 16, 32, 64
+# codec weight paths and forms (RWKVTTS_CODEC_WEIGHTS_* / RWKVTTS_CODEC_FORM_*)
+CODEC_WEIGHTS_AUTO, CODEC_WEIGHTS_BF16, CODEC_WEIGHTS_HILO = 0, 1, 2
+CODEC_FORM_SEPARATE_RESUNIT, CODEC_FORM_CHANNEL_LAST = 1, 2
 
 
 QUANT_NONE, QUANT_INT8, QUANT_NF4, QUANT_SF4 = 0, 1, 2, 3
@@ -142,6 +171,9 @@ EXPORTS = {
     "rwkvtts_codec_synth_weights": (ctypes.c_int, [ctypes.POINTER(CodecDims), ctypes.c_uint64, ctypes.c_void_p]),
     "rwkvtts_codec_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(CodecDims), ctypes.c_void_p,
                                             ctypes.POINTER(ctypes.c_void_p)]),
+    "rwkvtts_codec_create_ex": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(CodecDims), ctypes.c_void_p,
+                                               ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    "rwkvtts_codec_set_forms": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32]),
     "rwkvtts_codec_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "rwkvtts_codec_decode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                                             ctypes.c_void_p]),

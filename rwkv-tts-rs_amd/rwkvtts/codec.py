@@ -60,14 +60,21 @@ def synth_codec_blob_f32(d: dict, seed: int = 20251205, rel: float = 2.0 ** -12)
 class BiCodecDetokenizer:
     """One decoder per GPU (replaces the 4-session ORT pool of src/onnx_session_pool.rs:204-279)."""
 
-    def __init__(self, weights: np.ndarray, dims: Optional[dict] = None, device: int = 0):
+    def __init__(self, weights: np.ndarray, dims: Optional[dict] = None, device: int = 0,
+                 weight_path: int = 0):
+        """weight_path: _ffi.CODEC_WEIGHTS_AUTO (hi + lo weight planes iff some conv weight is not
+        bf16-exact), CODEC_WEIGHTS_BF16 or CODEC_WEIGHTS_HILO (rwkvtts_codec_create_ex)."""
         self.dims = dict(dims or CODEC_DIMS_FULL)
         self._cd = make_codec_dims(self.dims)
         w = np.ascontiguousarray(weights, dtype=np.float32)
         h = ctypes.c_void_p()
-        check(lib().rwkvtts_codec_create(device, ctypes.byref(self._cd), w.ctypes.data_as(ctypes.c_void_p),
-                                         ctypes.byref(h)), "codec_create")
+        check(lib().rwkvtts_codec_create_ex(device, ctypes.byref(self._cd), w.ctypes.data_as(ctypes.c_void_p),
+                                            int(weight_path), ctypes.byref(h)), "codec_create")
         self._h = h
+
+    def set_forms(self, forms: int):
+        """Verification forms of later decode calls (_ffi.CODEC_FORM_*; 0 = shipping, PCM bitwise equal)."""
+        check(lib().rwkvtts_codec_set_forms(self._h, int(forms)), "codec_set_forms")
 
     def close(self):
         if self._h:

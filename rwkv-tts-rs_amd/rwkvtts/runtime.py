@@ -146,17 +146,18 @@ def quant_config(quant_layers: int, quant_type) -> tuple:
 
 class SharedRwkvRuntime:
     """One engine per GPU: weights resident in HBM, `max_concurrent_batches` state slots.
-    quant_layers / quant_type: the server's --quant-layers / --quant-type (web-rwkv Quant)."""
+    quant_layers / quant_type: the server's --quant-layers / --quant-type (web-rwkv Quant).
+    forms: rwkvtts_engine_desc.forms (_ffi.FORM_*; 0 = the shipping decode forms)."""
 
     def __init__(self, weights: np.ndarray, device: int = 0, max_slots: int = 10,
                  token_chunk_size: int = 512, use_graphs: bool = True, weights_on_device: bool = False,
                  device_ptr: Optional[int] = None, wkv_variant: int = 0, quant_layers: int = 0,
-                 quant_type="none"):
+                 quant_type="none", forms: int = 0):
         # the C ABI serialises calls per engine; this lock also keeps Python-side buffers of one
         # call from interleaving with another thread's
         self._lock = threading.RLock()
         ql, qt = quant_config(quant_layers, quant_type)
-        desc = _ffi.EngineDesc(device, max_slots, token_chunk_size, 1 if use_graphs else 0, wkv_variant, ql, qt)
+        desc = _ffi.EngineDesc(device, max_slots, token_chunk_size, 1 if use_graphs else 0, wkv_variant, ql, qt, forms)
         h = ctypes.c_void_p()
         if device_ptr is not None:
             check(lib().rwkvtts_engine_create(ctypes.byref(desc), ctypes.c_void_p(device_ptr),
@@ -369,7 +370,7 @@ class DynamicBatchManager:
     def __init__(self, weights: np.ndarray, config: Optional[DynamicBatchConfig] = None,
                  devices: Sequence[int] = (0,), max_slots: int = 32, token_chunk_size: int = 512,
                  use_graphs: bool = True, wkv_variant: int = 0, tokenizer=None, quant_layers: int = 0,
-                 quant_type="none"):
+                 quant_type="none", forms: int = 0):
         self.config = config or DynamicBatchConfig()
         devices = list(devices)
         if not 1 <= len(devices) <= _ffi.MAX_ENGINES:
@@ -379,7 +380,7 @@ class DynamicBatchManager:
         for i, dev in enumerate(devices):
             d.devices[i] = dev
         ql, qt = quant_config(quant_layers, quant_type)
-        d.engine = _ffi.EngineDesc(0, max_slots, token_chunk_size, 1 if use_graphs else 0, wkv_variant, ql, qt)
+        d.engine = _ffi.EngineDesc(0, max_slots, token_chunk_size, 1 if use_graphs else 0, wkv_variant, ql, qt, forms)
         d.max_batch_size = self.config.max_batch_size
         d.collect_timeout_ms = self.config.collect_timeout_ms
         w = np.ascontiguousarray(weights)
@@ -424,19 +425,19 @@ class DynamicBatchManager:
             if self._closing or not getattr(self, "_h", None):
                 return
             self._closing = True
-            # wait until every call in flight is a waiter blocked inside the native wait (destroy
-            # returns those); a failing stats poll ends the wait -- destroy runs in any case once
-            # _closing is set, so the native manager, its threads and device memory never leak
-            try:
-                while True:
-                    s = _ffi.ManagerStats()
-                    if lib().rwkvtts_manager_get_stats(self._h, ctypes.byref(s)) != _ffi.OK:
-                        break
+            # destroy only once every call in flight is a waiter blocked inside the native wait
+            # (destroy returns those before it frees the handle); if the stats poll fails, once no
+            # call is in flight at all. An interrupt here (KeyboardInterrupt in the wait) propagates
+            # with _closing kept and the handle NOT destroyed: a leak, never a destroy that overlaps
+            # the start of another call (rwkvtts.h rwkvtts_manager_destroy)
+            while True:
+                s = _ffi.ManagerStats()
+                if lib().rwkvtts_manager_get_stats(self._h, ctypes.byref(s)) == _ffi.OK:
                     if self._inflight <= s.waiters:
                         break
-                    gate.wait(0.005)
-            except BaseException:
-                pass
+                elif self._inflight == 0:
+                    break
+                gate.wait(0.005)
         try:
             lib().rwkvtts_manager_destroy(self._h)
         finally:

@@ -11,6 +11,7 @@ import os
 import numpy as np
 import pytest
 
+import rwkvtts
 from rwkvtts import codec
 
 pytestmark = pytest.mark.gpu
@@ -118,16 +119,10 @@ def test_full_dims_bench_shape_512_frames_vs_oracle(oracle_mod):
 
 
 def _decoder(w, d, wlo=None):
-    """A decoder with the conv path forced (RWKVTTS_CODEC_WLO, read at creation) or automatic."""
-    old = os.environ.pop("RWKVTTS_CODEC_WLO", None)
-    if wlo is not None:
-        os.environ["RWKVTTS_CODEC_WLO"] = "1" if wlo else "0"
-    try:
-        return codec.BiCodecDetokenizer(w, d)
-    finally:
-        os.environ.pop("RWKVTTS_CODEC_WLO", None)
-        if old is not None:
-            os.environ["RWKVTTS_CODEC_WLO"] = old
+    """A decoder with the conv weight path forced (rwkvtts_codec_create_ex) or automatic."""
+    F = rwkvtts._ffi
+    path = F.CODEC_WEIGHTS_AUTO if wlo is None else (F.CODEC_WEIGHTS_HILO if wlo else F.CODEC_WEIGHTS_BF16)
+    return codec.BiCodecDetokenizer(w, d, weight_path=path)
 
 
 def test_weight_lo_path_bit_identical_on_bf16_weights():
@@ -190,7 +185,7 @@ def test_full_dims_f32_weights_vs_oracle(oracle_mod):
 def test_fused_residual_unit_bit_identical():
     """The 96-channel residual units as one launch (conv7 -> Snake -> conv1 -> + residual, the
     intermediate planes kept in LDS) give bitwise the two-launch result: same products, same
-    per-element accumulation order (RWKVTTS_NO_RESFUSE switches the fusion off per call)."""
+    per-element accumulation order (RWKVTTS_CODEC_FORM_SEPARATE_RESUNIT switches the fusion off)."""
     rs = np.random.default_rng(96)
     for d, T in ((codec.CODEC_DIMS_TINY, 41), (codec.CODEC_DIMS_FULL, 7)):
         w = codec.synth_codec_blob(d, seed=9)
@@ -198,11 +193,9 @@ def test_fused_residual_unit_bit_identical():
         c = codec.BiCodecDetokenizer(w, d)
         try:
             fused = c.decode_audio_batch(items)
-            os.environ["RWKVTTS_NO_RESFUSE"] = "1"
-            try:
-                plain = c.decode_audio_batch(items)
-            finally:
-                del os.environ["RWKVTTS_NO_RESFUSE"]
+            c.set_forms(rwkvtts._ffi.CODEC_FORM_SEPARATE_RESUNIT)
+            plain = c.decode_audio_batch(items)
+            c.set_forms(0)
             for x, y in zip(fused, plain):
                 assert np.array_equal(x, y)
         finally:
@@ -211,7 +204,7 @@ def test_fused_residual_unit_bit_identical():
 
 def test_channel_blocked_planes_bit_identical():
     """The WaveGenerator's activation planes channel-blocked ([C / 32][rows][32], the default) or
-    channel-last (RWKVTTS_CODEC_BLK=0, read per call): only addresses change, so PCM is bitwise
+    channel-last (RWKVTTS_CODEC_FORM_CHANNEL_LAST): only addresses change, so PCM is bitwise
     equal -- with and without the fused residual units, the weight-lo kernels, ragged lengths."""
     rs = np.random.default_rng(32)
     for d, T, wlo in ((codec.CODEC_DIMS_TINY, 41, None), (codec.CODEC_DIMS_FULL, 9, None),
@@ -221,14 +214,11 @@ def test_channel_blocked_planes_bit_identical():
         c = _decoder(w, d, wlo)
         try:
             outs = []
-            for env in ({}, {"RWKVTTS_CODEC_BLK": "0"}, {"RWKVTTS_NO_RESFUSE": "1"},
-                        {"RWKVTTS_CODEC_BLK": "0", "RWKVTTS_NO_RESFUSE": "1"}):
-                os.environ.update(env)
-                try:
-                    outs.append(c.decode_audio_batch(items))
-                finally:
-                    for k in env:
-                        del os.environ[k]
+            F = rwkvtts._ffi
+            for forms in (0, F.CODEC_FORM_CHANNEL_LAST, F.CODEC_FORM_SEPARATE_RESUNIT,
+                          F.CODEC_FORM_CHANNEL_LAST | F.CODEC_FORM_SEPARATE_RESUNIT):
+                c.set_forms(forms)
+                outs.append(c.decode_audio_batch(items))
             for o in outs[1:]:
                 for x, y in zip(outs[0], o):
                     assert np.array_equal(x, y)

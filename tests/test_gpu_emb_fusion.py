@@ -1,9 +1,7 @@
 """Decode steps run the token embedding inside layer 0's LayerNorm launch (lm_kernels.hip
 k_ln1024 EMB form, engine.hip launch_forward); prefill steps and engines created with
-RWKVTTS_NO_EMB_FUSE=1 run k_embed as its own launch. Both must give the same bits: the same
+forms = RWKVTTS_FORM_SEPARATE_EMBED run k_embed as its own launch. Both must give the same bits: the same
 token streams and bitwise-identical recurrent state after generation."""
-import os
-
 import numpy as np
 import pytest
 
@@ -21,12 +19,8 @@ def test_fused_embedding_is_bitwise_identical(dt):
     reqs = [make_request(synth_text(300 + i), seed=70 + i, max_tokens=40) for i in range(3)]
     out, states = [], []
     for off in (False, True):
-        if off:
-            os.environ["RWKVTTS_NO_EMB_FUSE"] = "1"
-        try:
-            rt = rwkvtts.SharedRwkvRuntime(blob, max_slots=4, token_chunk_size=128, use_graphs=True)
-        finally:
-            os.environ.pop("RWKVTTS_NO_EMB_FUSE", None)
+        rt = rwkvtts.SharedRwkvRuntime(blob, max_slots=4, token_chunk_size=128, use_graphs=True,
+                                       forms=rwkvtts._ffi.FORM_SEPARATE_EMBED if off else 0)
         try:
             out.append(rt.generate_batch(reqs))
             states.append([rt.read_slot(s) for s in range(len(reqs))])

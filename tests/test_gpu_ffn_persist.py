@@ -4,10 +4,8 @@ embedding folded in), rkv + LoRA-down, WKV, Wo -- with in-launch write-through h
 the launches they replace: the same bodies and reduction orders, so token streams must be
 identical bit for bit -- at the bench shape (32 slots, 0.4B bf16, graph replay), with fewer rows
 than slots (R < 32: padded LayerNorm blocks), eager launches, the fp16 model, two engines on one
-GPU, and against the oracle. RWKVTTS_FFN_PERSIST / RWKVTTS_ATT_PERSIST are read when an engine
-is created (0 = the separate launches)."""
-import os
-
+GPU, and against the oracle. The forms are selected per engine by rwkvtts_engine_desc.forms
+(RWKVTTS_FORM_*: each bit switches one fused form back to the launches it replaces)."""
 import numpy as np
 import pytest
 
@@ -18,41 +16,24 @@ from helpers import make_request, synth_text, to_struct
 pytestmark = pytest.mark.gpu
 
 
-# (RWKVTTS_PERSIST_MIN_ROWS=1, the default since round 4: the persistent forms at every row count)
-# "both": both halves persistent (two launches per layer, the production decode path). The one-launch
-# per layer / per step variants were measured slower in round 4 and removed in round 5.
-_M = {"RWKVTTS_PERSIST_MIN_ROWS": "1"}
-MODES = {"off": dict(_M, RWKVTTS_FFN_PERSIST="0", RWKVTTS_ATT_PERSIST="0"),
-         "ffn": dict(_M, RWKVTTS_FFN_PERSIST="5", RWKVTTS_ATT_PERSIST="0"),
-         "att": dict(_M, RWKVTTS_FFN_PERSIST="0", RWKVTTS_ATT_PERSIST="5"),
-         "both": dict(_M, RWKVTTS_FFN_PERSIST="5", RWKVTTS_ATT_PERSIST="5"),
+# "both": both halves persistent (two launches per layer, the production decode path, forms 0). The
+# one-launch per layer / per step variants and the rkv -> WKV granule hand-off were measured slower
+# (rounds 4 and 5) and removed from the library in round 6 (tools/experiments/r06_shelved_forms.patch).
+_F = rwkvtts._ffi
+_SEP = _F.FORM_SEPARATE_ATT | _F.FORM_SEPARATE_FFN
+MODES = {"off": _SEP,
+         "ffn": _F.FORM_SEPARATE_ATT,
+         "att": _F.FORM_SEPARATE_FFN,
+         "both": 0,
          # one-row steps without the row-fused LayerNorm form (its LayerNorm rows as at R > 1)
-         "both_rows": dict(_M, RWKVTTS_FFN_PERSIST="5", RWKVTTS_ATT_PERSIST="5", RWKVTTS_FUSE_LN1="0"),
-         # the row-fused form with the key -> value hand-off through partial slabs + counters
-         # instead of data-tagged granules
-         "both_slabs": dict(_M, RWKVTTS_FFN_PERSIST="5", RWKVTTS_ATT_PERSIST="5", RWKVTTS_GRAN="0"),
-         # the one-row form as one launch per layer (off by default: measured slower)
-         "both_layer1": dict(_M, RWKVTTS_FFN_PERSIST="5", RWKVTTS_ATT_PERSIST="5", RWKVTTS_LAYER1="1"),
-         # the rkv -> WKV hand-off as granules as well (off by default: measured slower)
-         "both_rkvgran": dict(_M, RWKVTTS_FFN_PERSIST="5", RWKVTTS_ATT_PERSIST="5", RWKVTTS_RKV_GRAN="1"),
+         "both_rows": _F.FORM_LN_ROWS,
+         # the row-fused form with the key -> value / WKV -> Wo hand-offs through partial slabs +
+         # counters instead of data-tagged granules
+         "both_slabs": _F.FORM_SLAB_HANDOFF,
          # separate launches with ln_out as its own launch (not folded into the one-row head GEMM)
-         "off_lnout": dict(_M, RWKVTTS_FFN_PERSIST="0", RWKVTTS_ATT_PERSIST="0", RWKVTTS_FUSE_LNOUT="0")}
-
-
-class _env:
-    def __init__(self, kv):
-        self.kv = kv
-
-    def __enter__(self):
-        self.old = {k: os.environ.get(k) for k in self.kv}
-        os.environ.update(self.kv)
-
-    def __exit__(self, *a):
-        for k, v in self.old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+         "off_lnout": _SEP | _F.FORM_SEPARATE_LNOUT,
+         # the shipping forms with the exact sampler walk (no certificate): the same tokens
+         "both_exact": _F.FORM_EXACT_SAMPLER}
 
 
 def _runtime(blob, mode, **kw):
@@ -60,8 +41,7 @@ def _runtime(blob, mode, **kw):
         mode = "both"
     elif mode is False:
         mode = "off"
-    with _env(MODES[mode]):
-        return rwkvtts.SharedRwkvRuntime(blob, **kw)
+    return rwkvtts.SharedRwkvRuntime(blob, forms=MODES[mode], **kw)
 
 
 def _both(blob, reqs, modes=("off", "ffn", "att", "both"), **kw):
@@ -121,14 +101,14 @@ def test_persist_one_row_fused_layernorm_bitwise(dtype):
     workgroups: every rkv / key workgroup computes the row's LayerNorm itself, a trailing workgroup
     stores the residual and the token-shift row; the FFN key -> value hand-off as data-tagged
     granules; ln_out folded into the head GEMM). Bitwise the separate launches' (ln_out as its own
-    launch, and folded), the LayerNorm-row form's, the slab hand-off's and the one-launch-per-layer
-    form's tokens and recurrent state, graph replay and eager."""
+    launch, and folded), the LayerNorm-row form's, the slab hand-off's and the exact sampler's
+    tokens and recurrent state, graph replay and eager."""
     dt = rwkvtts._ffi.DTYPE_F16 if dtype == "f16" else rwkvtts._ffi.DTYPE_BF16
     blob = W.synth_blob(W.DIMS_04B, seed=11, dtype=dt)
     reqs = [make_request(synth_text(500), seed=5, fixed=40)]
     for graphs in (True, False):
-        outs, _ = _both(blob, reqs, modes=("off_lnout", "off", "both", "both_rows", "both_slabs", "both_rkvgran", "both_layer1"), max_slots=4,
-                        token_chunk_size=512, use_graphs=graphs)
+        outs, _ = _both(blob, reqs, modes=("off_lnout", "off", "both", "both_rows", "both_slabs", "both_exact"),
+                        max_slots=4, token_chunk_size=512, use_graphs=graphs)
         assert all(o == outs[0] for o in outs[1:]), graphs
 
 
@@ -144,9 +124,8 @@ def test_persist_under_the_manager_two_engines_one_device(blob04):
     device holds the persistent slot (claim_persistent: two persistent launches in flight on one GPU
     can deadlock); the second runs the separate launches beside it, so one persistent launch and
     separate launches are in flight together -- asserted through the manager's per-engine flag."""
-    with _env(MODES["both"]):
-        m = rwkvtts.DynamicBatchManager(blob04, rwkvtts.DynamicBatchConfig(max_batch_size=64, collect_timeout_ms=5),
-                                        devices=[0, 0], max_slots=32, token_chunk_size=512)
+    m = rwkvtts.DynamicBatchManager(blob04, rwkvtts.DynamicBatchConfig(max_batch_size=64, collect_timeout_ms=5),
+                                    devices=[0, 0], max_slots=32, token_chunk_size=512, forms=MODES["both"])
     try:
         reqs = [make_request(synth_text(400 + i), seed=90 + i, fixed=20) for i in range(48)]
         got = m.generate_tts_batch(reqs)

@@ -112,7 +112,14 @@ def _explain(blob, rt, req, e, got, zero_shot):
             "oracle_token": (g_ref if phase == "global" else s_ref)[step],
             "oracle_sampler_on_gpu_logits": int(samp_gpu), "max_logit_gap_prefix": max(gaps),
             "logit_gap_at_divergence": gaps[-1],
-            "logit_gap_at_divergence_head": float(np.abs(np.nan_to_num(gl - orl, posinf=0, neginf=0)).max())}
+            "logit_gap_at_divergence_head": _finite_gap(gl, orl)}
+
+
+def _finite_gap(a, b):
+    """max |a - b| over the entries finite in both (masked -inf entries compared first, so no
+    -inf - -inf = nan is ever formed)"""
+    m = np.isfinite(a) & np.isfinite(b)
+    return float(np.abs(a[m] - b[m]).max()) if m.any() else 0.0
 
 
 def _check(reports, key):

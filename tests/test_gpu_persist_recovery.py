@@ -1,8 +1,9 @@
 """A persistent decode launch whose hand-off never completes is recoverable (VERDICT r4 next #2,
 ADVICE r4 medium), and the persistent slot is one per GPU across processes.
 
-RWKVTTS_TEST_DROP_ARRIVE=1 at engine creation arms a device word: the first rkv workgroup of a
-persistent attention launch that finds it set clears it and skips its head arrival, so that head's
+RWKVTTS_TEST_DROP_ARRIVE=n at engine creation arms a device word: the rkv workgroup of a
+persistent attention launch that takes it skips its head arrival (re-armed after each recovery until n
+units have failed), so that head's
 WKV workgroups time out (~50 ms bounded wait), the give-up code reaches the unit's control-block
 snapshot and the unit fails (Engine::finish_unit). The engine then zeroes the give-up word and every
 hand-off counter block (Engine::reset_persistent); the failed requests' slots are reset when they
@@ -92,6 +93,39 @@ def test_one_row_form_recovers_after_a_timed_out_handoff():
         assert ei.value.code == rwkvtts._ffi.EHIP, ei.value
         assert rt.generate_batch([req]) == ref
         assert rt.generate_batch([req]) == ref
+    finally:
+        rt.close()
+
+
+def test_second_timeout_degrades_to_separate_launches(mid):
+    """a second timed-out hand-off soon after the first (the deadlock condition recurring,
+    e.g. another process running persistent launches on this GPU without sharing the lock directory)
+    makes the engine leave the persistent forms for good: its persistent flag drops to 0, the device's
+    slot is released, and the requests after it are token-exact with no further fault -- the drop
+    hook is armed again after the second recovery, which only a persistent launch could take."""
+    import oracle
+    with _env(RWKVTTS_TEST_DROP_ARRIVE=3):
+        rt = rwkvtts.SharedRwkvRuntime(mid, device=0, max_slots=8, token_chunk_size=512, use_graphs=True)
+    try:
+        assert rt.stats()["persistent"] == 1
+        reqs = [make_request(synth_text(140 + i), seed=160 + i, fixed=5) for i in range(4)]
+        for _ in range(2):  # first timeout: reset, still persistent; second: degraded
+            with pytest.raises(rwkvtts._ffi.RwkvTtsError) as ei:
+                rt.generate_batch(reqs)
+            assert ei.value.code == rwkvtts._ffi.EHIP, ei.value
+        assert rt.stats()["persistent"] == 0, "the engine must run the separate launches now"
+        om = oracle.Model(mid)
+        for _ in range(2):
+            out = rt.generate_batch(reqs)
+            assert all(st == 0 for st in rt.last_status), rt.last_status
+            for i in range(4):
+                assert out[i] == _oracle(om, reqs[i]), i
+        # the slot was released: a new engine on the device takes it
+        c = rwkvtts.SharedRwkvRuntime(mid, device=0, max_slots=2, token_chunk_size=512, use_graphs=True)
+        try:
+            assert c.stats()["persistent"] == 1
+        finally:
+            c.close()
     finally:
         rt.close()
 

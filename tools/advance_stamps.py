@@ -1,12 +1,12 @@
 """Per-phase s_memrealtime stamps (10 ns ticks) of k_advance (the device sampler + phase controller) in the last
-decode step of a 32-request 0.4B batch (RWKVTTS_ADV_STAMPS debug hook). Usage: advance_stamps.py [S]"""
+decode step of a 32-request 0.4B batch (RWKVTTS_DEBUG_STAMPS adv=path debug hook). Usage: advance_stamps.py [S]"""
 import os
 import sys
 import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 path = os.path.join(tempfile.gettempdir(), "adv_stamps.bin")
-os.environ["RWKVTTS_ADV_STAMPS"] = path
+os.environ["RWKVTTS_DEBUG_STAMPS"] = "adv=" + path
 sys.path.insert(0, os.path.join(ROOT, "rwkv-tts-rs_amd"))
 import numpy as np  # noqa: E402
 import rwkvtts  # noqa: E402

@@ -3,7 +3,7 @@ replay. Prints decode ms/step from the engine's own HIP events and a token check
 change that keeps the arithmetic must keep the checksum). Usage: decode_bench.py [S] [reps].
 Env: DB_B requests (default 32), DB_F16=1 fp16 weights, DB_ZS=1 zero-shot prompts (32 reference
 global tokens + 128 reference semantic tokens per request), DB_QUANT=int8|nf4 (every layer quantised,
-the server's --quant-layers 24 --quant-type ...)."""
+the server's --quant-layers 24 --quant-type ...), DB_FORMS=n (rwkvtts_engine_desc.forms: RWKVTTS_FORM_* bits)."""
 import hashlib
 import os
 import sys
@@ -22,7 +22,8 @@ zs = os.environ.get("DB_ZS", "0") == "1"
 blob = W.synth_blob(W.DIMS_04B, seed=20251205, **({"dtype": rwkvtts._ffi.DTYPE_F16} if f16 else {}))
 qt = os.environ.get("DB_QUANT", "none")
 rt = rwkvtts.SharedRwkvRuntime(blob, max_slots=max(B, 1), token_chunk_size=512, use_graphs=True,
-                               quant_layers=W.DIMS_04B["n_layer"] if qt != "none" else 0, quant_type=qt)
+                               quant_layers=W.DIMS_04B["n_layer"] if qt != "none" else 0, quant_type=qt,
+                               forms=int(os.environ.get("DB_FORMS", "0")))
 del blob
 import numpy as np  # noqa: E402
 reqs = []

@@ -78,6 +78,8 @@ def main(src, dst):
     if tot:
         out["dominant"] = max(tot, key=tot.get)
         out["dominant_rule"] = "largest B=32 total time among the decode kernels with a byte model (as bench.py)"
+    from rwkvtts import _ffi
+    out["build"] = _ffi.build_id()  # the library this trace was measured on (bench.py matches it)
     json.dump(out, open(dst, "w"), indent=1)
     print(json.dumps(out, indent=1))
 

@@ -6,7 +6,7 @@ for r in 1 2; do
   for v in A B; do
     if [ $v = A ]; then L=$1; P=$3; else L=$2; P=$4; fi
     echo "== $v"
-    RWKVTTS_LIB=$PWD/$L RWKVTTS_TIMELINE=$PWD/gpurun_out/ab/tl_$v.txt timeout -k 10 120 python -u tools/decode_bench.py 256 1 | grep rep && python3 tools/timeline_summary.py gpurun_out/ab/tl_$v.txt || exit 1
+    RWKVTTS_LIB=$PWD/$L RWKVTTS_DEBUG_STAMPS=timeline=$PWD/gpurun_out/ab/tl_$v.txt timeout -k 10 120 python -u tools/decode_bench.py 256 1 | grep rep && python3 tools/timeline_summary.py gpurun_out/ab/tl_$v.txt || exit 1
     RWKVTTS_LIB=$PWD/$P timeout -k 10 120 python -u tools/decode_bench.py 256 2 | grep rep || exit 1
   done
 done

@@ -49,5 +49,7 @@ for name, e in out["kernels"].items():
     if name in per:
         e["algorithmic_bytes"] = per[name]
         e["traffic_over_algorithmic"] = round(e["traffic_bytes"] / per[name], 3)
+from rwkvtts import _ffi  # noqa: E402
+out["build"] = _ffi.build_id()  # the library these counters were measured on (bench.py matches it)
 json.dump(out, open(sys.argv[3], "w"), indent=1)
 print(json.dumps(out["kernels"], indent=1))

@@ -6,8 +6,14 @@ flops per cycle. util = busy / (1024 SIMDs x kernel cycles); kernel cycles = dur
 the clock taken from GRBM_GUI_ACTIVE (summed over the 8 XCDs) / duration of the same kernel class. Usage: pmc_dir kt_dir."""
 import csv
 import glob
+import os
 import sys
 from collections import defaultdict
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "rwkv-tts-rs_amd"))
+from rwkvtts import _ffi  # noqa: E402
+
+print(f"# build {_ffi.build_id()}")  # the library these counters were measured on (bench.py matches it)
 
 
 def short(name):

@@ -3,7 +3,7 @@
 # kernel-trace pass of the same commands for durations. Output under gpurun_out/mfma/.
 set -o pipefail
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/mfma
+O=${MFMA_OUT:-$R/gpurun_out/mfma}
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 export LM_GRAPHS=0

@@ -1,5 +1,5 @@
 # Kernel-trace A/B of the decode microbenchmark: per-kernel duration and preceding gap for each
-# environment setting given (e.g. "X=1" "RWKVTTS_NO_XMAP=1"). Usage: bash tools/prof_ab.sh ENV...
+# environment setting given (e.g. "X=1" "DB_FORMS=1"). Usage: bash tools/prof_ab.sh ENV...
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd /tmp && export TMPDIR=/tmp

@@ -9,7 +9,7 @@ for r in 1 2; do
   for v in ref new; do
     if [ $v = ref ]; then L=$PWD/$1; else L=$PWD/build/tl/librwkvtts.so; fi
     echo "== $v"
-    RWKVTTS_LIB=$L RWKVTTS_TIMELINE=$PWD/gpurun_out/samp/tl_$v.txt timeout -k 10 120 python -u tools/decode_bench.py 256 1 | grep rep && python3 tools/timeline_summary.py gpurun_out/samp/tl_$v.txt | grep -E "span|advance|head" || exit 1
+    RWKVTTS_LIB=$L RWKVTTS_DEBUG_STAMPS=timeline=$PWD/gpurun_out/samp/tl_$v.txt timeout -k 10 120 python -u tools/decode_bench.py 256 1 | grep rep && python3 tools/timeline_summary.py gpurun_out/samp/tl_$v.txt | grep -E "span|advance|head" || exit 1
   done
 done
 for lib in "$2" ""; do

@@ -1,4 +1,4 @@
-"""Summarise a RWKVTTS_TIMELINE dump: per launch class, mean duration and the mean idle gap
+"""Summarise a RWKVTTS_DEBUG_STAMPS timeline= dump: per launch class, mean duration and the mean idle gap
 before it (its start minus the previous launch's end), and the per-step totals."""
 import sys
 from collections import defaultdict

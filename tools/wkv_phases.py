@@ -1,4 +1,4 @@
-"""WKV (k_wkv6 by default; RWKVTTS_WKV_VARIANT-style env of the engine picks k_wkv4) phase breakdown: runs 32 requests through the engine with RWKVTTS_WKV_STAMPS set
+"""WKV (k_wkv6 by default; RWKVTTS_WKV_VARIANT-style env of the engine picks k_wkv4) phase breakdown: runs 32 requests through the engine with RWKVTTS_DEBUG_STAMPS wkv=path set
 (layer 5 of the last decode step records per-workgroup stamps) and prints the launch-wide span,
 the workgroup start ramp and mean / max core-clock cycles per phase."""
 import os
@@ -9,7 +9,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "rwkv-tts-rs_amd"))
 path = os.path.join(ROOT, "gpurun_out", "wkv_stamps.bin")
-os.environ["RWKVTTS_WKV_STAMPS"] = path
+os.environ["RWKVTTS_DEBUG_STAMPS"] = "wkv=" + path
 import rwkvtts  # noqa: E402
 from rwkvtts import weights as W  # noqa: E402
 
