@@ -2974,4 +2974,21 @@ int launch_wkv(const WkvArgs& a, int n_seg, int H, hipStream_t st) {
   return n_seg * H;
 }
 
+void persist_footprint(int* vgpr_alloc, int* lds_bytes) {
+  const size_t dyn = (size_t)2 * 16 * (8 * 32 + 8) * 2 * 2;  // the launches' dynamic LDS (the rkv / key X image)
+  int v = 0;
+  size_t l = 0;
+  for (const void* fn : {(const void*)k_att_persist<false, false, false>, (const void*)k_att_persist<false, false, true>,
+                         (const void*)k_att_persist<true, false, false>, (const void*)k_att_persist<true, false, true>,
+                         (const void*)k_ffn_persist<false, false>, (const void*)k_ffn_persist<false, true>,
+                         (const void*)k_ffn_persist<true, false>, (const void*)k_ffn_persist<true, true>}) {
+    hipFuncAttributes fa{};
+    if (hipFuncGetAttributes(&fa, fn) != hipSuccess) continue;
+    v = std::max(v, (fa.numRegs + 7) & ~7);  // (numRegs is the request; the hardware allocates by 8)
+    l = std::max(l, fa.sharedSizeBytes + dyn);
+  }
+  *vgpr_alloc = v;
+  *lds_bytes = (int)l;
+}
+
 }  // namespace rwkvtts

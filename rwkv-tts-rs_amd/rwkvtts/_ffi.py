@@ -206,6 +206,8 @@ def lib():
                                "(the HIP extension is required; there is no CPU fallback)")
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in EXPORTS.items():
+            if os.environ.get("RWKVTTS_LIB") and not hasattr(L, name):
+                continue  # (an A/B build of an earlier revision: entry points it predates stay unbound)
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args

@@ -38,6 +38,7 @@ static rwkvtts_manager* make(int n_engines, int slots, int collect_ms) {
   d.max_batch_size = 8;
   d.collect_timeout_ms = collect_ms;
   static char w[4096];
+  for (size_t i = 0; i < sizeof(w); ++i) w[i] = (char)((i * 31 + 7) & 255);  // checked by every stub engine
   rwkvtts_manager* m = nullptr;
   EXPECT(rwkvtts_manager_create(&d, w, sizeof(w), &m) == RWKVTTS_OK);
   return m;
@@ -155,7 +156,34 @@ static void scenario_dead_engine() {
   EXPECT(rwkvtts_manager_destroy(m) == RWKVTTS_OK);
 }
 
+// weight distribution over distinct devices: by the RCCL broadcast when a librccl.so.1 is loadable
+// (the stub of tests/native/stub/rccl: STUB_EXPECT_RCCL=1) and RCCL is not disabled, else by peer
+// copies; every engine checks its copy (stub/engine.h)
+static void scenario_broadcast() {
+  const bool want = getenv("STUB_EXPECT_RCCL") != nullptr;
+  rwkvtts_manager* m = make(4, 2, 2);
+  if (!m) return;
+  rwkvtts_manager_stats st;
+  EXPECT(rwkvtts_manager_get_stats(m, &st) == RWKVTTS_OK);
+  EXPECT(st.bcast_ranks == 4);
+  EXPECT(st.bcast_rccl == (want ? 1 : 0));
+  std::vector<uint64_t> tk(8);
+  for (int i = 0; i < 8; ++i) {
+    rwkvtts_request q = req(500 + i, 3);
+    EXPECT(rwkvtts_manager_submit(m, &q, &tk[i]) == RWKVTTS_OK);
+  }
+  std::vector<int32_t> sem(RWKVTTS_SEMANTIC_LIMIT);
+  for (int i = 0; i < 8; ++i) {
+    rwkvtts_result r;
+    memset(&r, 0, sizeof(r));
+    r.semantic_tokens = sem.data();
+    EXPECT(rwkvtts_manager_wait(m, tk[i], -1, &r) == RWKVTTS_OK && r.status == 0);
+  }
+  EXPECT(rwkvtts_manager_destroy(m) == RWKVTTS_OK);
+}
+
 int main() {
+  scenario_broadcast();
   scenario_concurrent(false);
   setenv("STUB_FAIL_EVERY", "2", 1);
   scenario_concurrent(true);

@@ -71,6 +71,11 @@ class Engine {
  public:
   int init(const rwkvtts_engine_desc& desc, const void* w, size_t bytes, int) {
     RT_CHECK(w && bytes > 0, RWKVTTS_EINVAL, "stub: no weights");
+    // the blob every engine receives (after the manager's broadcast) is the caller's, byte for byte
+    // (manager_tsan_main.cpp fills it with (i * 31 + 7) & 255)
+    for (size_t i = 0; i < bytes; ++i)
+      RT_CHECK(((const uint8_t*)w)[i] == (uint8_t)((i * 31 + 7) & 255), RWKVTTS_EINVAL,
+               "stub: an engine's weights differ from the caller's blob");
     device_ = desc.device;
     S_ = desc.max_slots > 0 ? desc.max_slots : 4;
     if (const char* e = getenv("STUB_FAIL_EVERY")) fail_every_ = atoi(e);

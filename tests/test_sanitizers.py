@@ -56,8 +56,23 @@ def test_manager_under_tsan(tmp_path):
                            os.path.join(ROOT, "tests", "native", "manager_tsan_main.cpp"), str(tmp_path / "manager.cpp"),
                            "-ldl", "-lpthread"])
     env = dict(os.environ, RWKVTTS_MANAGER_NO_RCCL="1", TSAN_OPTIONS="halt_on_error=1:second_deadlock_stack=1")
-    for k in ("STUB_FAIL_EVERY", "STUB_DEAD_ENGINE"):
+    for k in ("STUB_FAIL_EVERY", "STUB_DEAD_ENGINE", "STUB_EXPECT_RCCL"):
         env.pop(k, None)
     out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300, env=env)
     assert out.returncode == 0 and "manager_tsan: ok" in out.stdout, (out.stdout[-2000:], out.stderr[-6000:])
     assert "ThreadSanitizer" not in out.stderr, out.stderr[-6000:]
+    # the multi-rank RCCL weight broadcast (only ever run with one device): the
+    # manager over four distinct devices with RCCL enabled, against the host-memory RCCL stand-in
+    # (tests/native/stub/rccl/stub_rccl.cpp, found by the manager's dlopen of librccl.so.1): one
+    # ncclCommInitAll over the four devices, four broadcasts in one group, every engine's copy checked
+    libdir = tmp_path / "rccl"
+    libdir.mkdir()
+    subprocess.check_call([CLANG, "-std=c++17", "-O1", "-g", "-fsanitize=thread", "-shared", "-fPIC",
+                           "-I", os.path.join(stub, "rccl"), "-o", str(libdir / "librccl.so.1"),
+                           os.path.join(stub, "rccl", "stub_rccl.cpp")])
+    env2 = dict(env, STUB_EXPECT_RCCL="1", LD_LIBRARY_PATH=str(libdir) + ":" + os.environ.get("LD_LIBRARY_PATH", ""))
+    env2.pop("RWKVTTS_MANAGER_NO_RCCL")
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300, env=env2)
+    assert out.returncode == 0 and "manager_tsan: ok" in out.stdout, (out.stdout[-2000:], out.stderr[-6000:])
+    assert "ThreadSanitizer" not in out.stderr, out.stderr[-6000:]
+    assert "stub_rccl: grouped broadcast of 4096 bytes to 4 ranks" in out.stderr, out.stderr[-3000:]
