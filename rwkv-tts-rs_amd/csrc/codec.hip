@@ -109,13 +109,6 @@ __device__ inline void glds16(const void* g, void* l) {
                                    (__attribute__((address_space(3))) void*)l, 16, 0, 0);
 }
 
-// Co-residency policy of the vocoder's conv launches beside the token generator (Codec::coresident_shm):
-// 0 none; 1 cap every launch's workgroups per CU so that one decode workgroup fits beside them;
-// 2 + pointwise convs in 64-wide tiles (80 VGPRs: three workgroups per CU beside a decode wave, where
-// the 96-wide ones at 168 VGPRs allow one); 3 + ConvTranspose in 64-wide tiles; 4 + 7-tap convs in
-// 48-wide tiles (LDS room for a decode workgroup at every dilation)
-constexpr int kCodecResv = 2;
-
 // Workgroup = NWV waves along time, each 32 rows x TN channels (2 x TN/16 MFMA 16x16x32 tiles).
 // Per 32-channel chunk the workgroup stages (double-buffered, async global->LDS) the input
 // window that ALL taps read -- TM + (ntaps - 1) * |tap stride| rows of the hi and lo planes --
@@ -661,10 +654,6 @@ class Codec {
   bf16_t* wlb = nullptr; // lo part (f32 - hi), read by the WLO conv kernels
   bool wlo = false;      // some conv weight is not bf16-exact: three MFMAs per product
   uint32_t forms = 0;    // RWKVTTS_CODEC_FORM_* of later decode calls (rwkvtts_codec_set_forms)
-  // co-residency with the token generator (set at init from persist_footprint): VGPRs per lane and
-  // LDS bytes one persistent decode workgroup needs per SIMD / per CU; 0: no reservation
-  int dec_vgpr = 0, dec_lds = 0;
-  int resv = kCodecResv;
   int cap_n = 0, cap_T = 0;
   int *d_tok = nullptr, *d_glob = nullptr, *d_ntok = nullptr;
   // prenet: x f32 residual stream [n][T][P]; zp/up/hp planes [n][T][L|P|I]
@@ -749,7 +738,6 @@ class Codec {
     wlo = weight_path == RWKVTTS_CODEC_WEIGHTS_AUTO ? !conv_weights_bf16_exact(host_w)
                                                     : weight_path == RWKVTTS_CODEC_WEIGHTS_HILO;
     if (wlo) RT_HIP(hipMalloc(&wlb, n * sizeof(bf16_t)));
-    persist_footprint(&dec_vgpr, &dec_lds);
     RT_HIP(hipMemcpy(wf, host_w, n * sizeof(float), hipMemcpyHostToDevice));
     k_f32_split_bf16<<<2048, 256, 0, stream>>>(wf, wb, wlb, n);
     RT_HIP(hipGetLastError());
@@ -846,29 +834,6 @@ class Codec {
     int act = 0;
     int64_t y_bs = -1;  // per-utterance stride of y / planes / res (-1: same as the input's)
   };
-  // Co-residency with the token generator. The decode steps of the next batch run beside this decoder
-  // (their own, higher-priority stream); a persistent decode workgroup needs one wave of dec_vgpr
-  // VGPRs on every SIMD and dec_lds bytes of LDS. A conv launch that fills the CUs (e.g. the
-  // pointwise convs: three 168-VGPR waves per SIMD) leaves a decode launch waiting for whole vocoder
-  // workgroups to retire -- beside them decode launches took up to 1.7 ms instead of 17 us
-  // (profiles/r06d_outliers.txt). Each launch is therefore capped, by padding its LDS request, at the
-  // workgroups per CU whose VGPRs leave one decode wave per SIMD free, with room for the decode
-  // workgroup's LDS beside them. Kernels that cannot leave that room (8-wave 168-VGPR tiles) are
-  // unchanged. Timing only: the arithmetic does not depend on the LDS size.
-  size_t coresident_shm(const void* fn, int nwv, size_t shm) {
-    if (resv < 1 || dec_vgpr <= 0) return shm;
-    hipFuncAttributes fa{};
-    if (hipFuncGetAttributes(&fa, fn) != hipSuccess || fa.numRegs <= 0) return shm;
-    const int alloc = (fa.numRegs + 7) & ~7;
-    const int wps = std::max(1, nwv / 4);  // this kernel's waves per SIMD per workgroup
-    const int by_vgpr = (512 - dec_vgpr) / (alloc * wps);
-    if (by_vgpr < 1) return shm;
-    const size_t lds_cu = 160 * 1024;
-    const size_t lo = lds_cu / (by_vgpr + 1) + 256;          // by_vgpr + 1 workgroups do not fit
-    const size_t hi = (lds_cu - (size_t)dec_lds) / by_vgpr;  // by_vgpr of them leave the decode room
-    if (shm >= lo || lo > hi) return shm;
-    return lo;
-  }
   std::string stage_name(const char* base, int C) { return profiling ? std::string(base) + "@" + std::to_string(C) : std::string(); }
   int conv(int n, int Tmax, const std::string& name, Planes x, int64_t bs, int Ci, int tin_mul, const bf16_t* w,
            int K, int Co, int mode, int dil, int pad, int s, const float* bias, const ConvOut& o) {
@@ -879,7 +844,7 @@ class Codec {
     // pointwise (memory-bound) convs: 96-wide column tiles read the input window fewer times
     // (conv1 @ 192 / 384 / 768: 6.9 / 4.1 / 2.2 -> 5.3 / 3.5 / 2.0 ms per batch with the XCD-aware
     // order below; 192-wide tiles halve the occupancy and are slower)
-    if (K == 1 && Co % 96 == 0 && resv < 2) TN = 96;
+    if (K == 1 && Co % 96 == 0) TN = 96;
     const int ntaps_max = mode == 1 ? (K + s - 1) / s : K;
     const int span = (ntaps_max - 1) * (mode == 1 ? 1 : dil);
     const int KT = ntaps_max <= 1 ? 1 : (ntaps_max <= 3 ? 3 : 7);
@@ -898,8 +863,12 @@ class Codec {
       // spread, for +1.5 ms of vocoder time; 64 stays.
       // ConvTranspose: 96-wide tiles measured faster at 96 and 384 output channels (2.54 -> 2.14,
       // 2.30 -> 2.10 ms per batch), slower at 192 (2.51 -> 2.62), equal at 768
-      if (mode == 1 && KT == 3 && (Co == 96 || Co == 384) && resv < 3) TN = 96;
-      if (KT == 7 && mode == 0 && resv >= 4 && Co % 48 == 0) TN = 48;
+      if (mode == 1 && KT == 3 && (Co == 96 || Co == 384)) TN = 96;
+      // (Round 6: capping every conv launch's workgroups per CU, by padding its LDS request, so that a
+      // persistent decode workgroup always fits beside them -- with the pointwise convs in 64-wide
+      // tiles, the ConvTranspose ones too, the 7-tap ones in 48-wide tiles -- left the decode step
+      // beside the vocoder unchanged, 0.806-0.816 ms, and the vocoder alone 3-10 ms slower:
+      // profiles/r06e_coresidency_ab.txt, tools/experiments/r06_codec_coresidency.patch)
     }
     int nwv = conv_waves(KT);
     const int wplanes = wlo ? 2 : 1;  // weight planes staged per chunk
@@ -926,15 +895,8 @@ class Codec {
       nwv = bw;
     }
     const int TM = 32 * nwv;
-    size_t shm = shm_of(TN, nwv);
+    const size_t shm = shm_of(TN, nwv);
     RT_CHECK(fits(TN, nwv) && ntaps_max <= 7 && Ci <= 4096, RWKVTTS_EINVAL, "codec conv: tile window too large");
-    const void* fn = nullptr;
-#define RT_CONV_FN(TN_, KT_, WLO_, NWV_) \
-    if (!fn && TN == TN_ && KT == KT_ && wlo == WLO_ && nwv == NWV_) fn = (const void*)k_conv<TN_, KT_, WLO_, NWV_>;
-    RT_CONV_KERNELS(RT_CONV_FN)
-#undef RT_CONV_FN
-    RT_CHECK(fn, RWKVTTS_EINVAL, "codec conv: no kernel for this tile shape");
-    shm = coresident_shm(fn, nwv, shm);
     ConvArgs a{};
     a.xh = x.h; a.xl = x.l; a.x_bs = bs; a.Ci = Ci; a.tin_mul = tin_mul; a.w = w; a.wl = wlb ? wlb + (w - wb) : nullptr; a.K = K; a.Co = Co;
     a.mode = mode; a.dil = dil; a.pad = pad; a.s = s; a.bias = bias; a.rbias = o.rbias; a.rb_bs = o.rb_bs;

@@ -153,10 +153,4 @@ inline LaunchTiming& launch_timing() {
     }                                                                                                \
   } while (0)
 
-// The footprint of one persistent decode workgroup (the largest over the k_att_persist /
-// k_ffn_persist instances, lm_kernels.hip): VGPRs allocated per lane (one wave per SIMD) and LDS
-// bytes. A kernel that runs beside the token generator (the vocoder, codec.hip) leaves this much
-// free on each CU so that a decode launch never waits for its workgroups to retire.
-void persist_footprint(int* vgpr_alloc, int* lds_bytes);
-
 }  // namespace rwkvtts

@@ -674,12 +674,17 @@ __device__ inline uint32_t gran_tag(const FfnSync& sy) {
   const int ep = __hip_atomic_load((gint_t*)sy.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return (((uint32_t)__builtin_amdgcn_readfirstlane(ep) * 64u + (uint32_t)sy.layer) & 0x7FFFFFFFu) | 0x80000000u;
 }
-// one polled granule: a relaxed agent-scope 64-bit atomic load (global_load_dwordx2 sc1). The poll
-// loops re-read granules with these only: an atomic load is re-issued on every pass (a plain load in
-// a spin loop may legally be merged or hoisted) and is single-copy atomic over its 8 bytes, so the
-// {data, tag} pair is never torn (a 16-byte load's halves carry no such guarantee)
-__device__ inline uint64_t ld_gran(const uint64_t* p) {
-  return __hip_atomic_load((const gu64_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// the poll loops re-read their granules with volatile (cache-policy bit 31) 16-byte sc1 buffer loads
+// through a wave-uniform resource, two granules per load: a volatile load is re-issued on every pass
+// (a plain load in a spin loop may legally be merged or hoisted out of it; the disassembly shows
+// the loads inside the loop), sc1 serves it from L2, never a stale L1. Each 8-byte {data, tag}
+// granule is written by ONE 8-byte sc1 store and read untorn within the 16-byte load (observed on
+// gfx950 / ROCm 7.2, MI355X_MICROARCH.md "R2's granule": not an architectural guarantee -- a torn
+// read would fail the tag compare of the half that lags and the poll simply runs another pass).
+// (One 64-bit atomic load per granule instead: B = 1 decode 521-523 vs 514-520 us per step,
+// profiles/r06f_granule_poll_ab.txt.)
+__device__ inline u64x2_ ld_gran2(__amdgpu_buffer_rsrc_t r, int off_bytes) {
+  return __builtin_bit_cast(u64x2_, __builtin_amdgcn_raw_buffer_load_b128(r, off_bytes, 0, (int)0x80000010u));
 }
 __device__ inline void gran_store_bits(uint64_t* p, uint32_t bits, uint32_t tag) {
   __hip_atomic_store((gu64_t*)p, ((uint64_t)tag << 32) | bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -694,7 +699,7 @@ __device__ inline void hold_until(int ticks) {
   while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)ticks) __builtin_amdgcn_s_sleep(2);
 }
 // handed-off bytes are read with sc1 (L1-bypassing) buffer loads only (after the hand-off's counter
-// wait: never as the polled word itself -- polls are atomic loads, sync_wait / ld_gran)
+// wait: never as the polled word itself -- polls are atomic / volatile loads, sync_wait / ld_gran2)
 __device__ inline u32x4_ ld_sc1_b128(__amdgpu_buffer_rsrc_t r, int off_bytes) {
   return __builtin_amdgcn_raw_buffer_load_b128(r, off_bytes, 0, 16);
 }
@@ -924,12 +929,13 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
     load_w();
     if (threadIdx.x < 64) {
       const uint32_t tag = gran_tag(sy);
-      const uint64_t* zp = sy.zgran + kbeg + 2 * lane;
+      const auto zr = wt_rsrc(sy.zgran);
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       uint64_t q0, q1;
       for (;;) {
-        q0 = ld_gran(zp);
-        q1 = ld_gran(zp + 1);
+        const u64x2_ qq = ld_gran2(zr, (kbeg + 2 * lane) * 8);
+        q0 = qq.x;
+        q1 = qq.y;
         const bool ok = (uint32_t)(q0 >> 32) == tag && (uint32_t)(q1 >> 32) == tag;
         if (__all(ok)) break;
         __builtin_amdgcn_s_sleep(1);
@@ -1020,16 +1026,20 @@ __device__ __attribute__((always_inline)) void gemm2_body(const GA& a, const int
       for (int u = 0; u < PERR; ++u) xr[p][u] = (float4_){0.f, 0.f, 0.f, 0.f};
     if (wave == 0) {
       const uint32_t tag = gran_tag(sy);
+      const auto gr = wt_rsrc(sy.gran);
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       for (;;) {
         bool ok = true;
 #pragma unroll
         for (int p = 0; p < NX; ++p) {
-          // four granules {data | tag << 32} per split, each one atomic 64-bit load (ld_gran)
-          const uint64_t* gp = sy.gran + (int64_t)p * sy.gran_ld + kbeg + 4 * lane;
+          // four granules {data | tag << 32} per split, two per volatile 16-byte load (ld_gran2)
           uint64_t q[4];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) q[e] = ld_gran(gp + e);
+          for (int e = 0; e < 2; ++e) {
+            const u64x2_ qq = ld_gran2(gr, (p * sy.gran_ld + kbeg + 4 * lane + 2 * e) * 8);
+            q[2 * e] = qq.x;
+            q[2 * e + 1] = qq.y;
+          }
           xr[p][0] = (float4_){__builtin_bit_cast(float, (uint32_t)q[0]), __builtin_bit_cast(float, (uint32_t)q[1]),
                                __builtin_bit_cast(float, (uint32_t)q[2]), __builtin_bit_cast(float, (uint32_t)q[3])};
 #pragma unroll
@@ -2972,23 +2982,6 @@ int launch_wkv(const WkvArgs& a, int n_seg, int H, hipStream_t st) {
   else if (units <= 20 && a.n_part <= 4) RT_LAUNCH((k_wkv<20, 4>), grid, dim3(256), 0, st, a);
   else RT_LAUNCH((k_wkv<32, 8>), grid, dim3(256), 0, st, a);
   return n_seg * H;
-}
-
-void persist_footprint(int* vgpr_alloc, int* lds_bytes) {
-  const size_t dyn = (size_t)2 * 16 * (8 * 32 + 8) * 2 * 2;  // the launches' dynamic LDS (the rkv / key X image)
-  int v = 0;
-  size_t l = 0;
-  for (const void* fn : {(const void*)k_att_persist<false, false, false>, (const void*)k_att_persist<false, false, true>,
-                         (const void*)k_att_persist<true, false, false>, (const void*)k_att_persist<true, false, true>,
-                         (const void*)k_ffn_persist<false, false>, (const void*)k_ffn_persist<false, true>,
-                         (const void*)k_ffn_persist<true, false>, (const void*)k_ffn_persist<true, true>}) {
-    hipFuncAttributes fa{};
-    if (hipFuncGetAttributes(&fa, fn) != hipSuccess) continue;
-    v = std::max(v, (fa.numRegs + 7) & ~7);  // (numRegs is the request; the hardware allocates by 8)
-    l = std::max(l, fa.sharedSizeBytes + dyn);
-  }
-  *vgpr_alloc = v;
-  *lds_bytes = (int)l;
 }
 
 }  // namespace rwkvtts
