@@ -2754,10 +2754,242 @@ __device__ __attribute__((always_inline)) void wkv6_body(const WkvArgs& a, const
   }
 }
 
-template <bool F16, bool MULTI_ROW = false>  // MULTI_ROW: the same code, a distinct symbol for prefill steps
-__global__ __launch_bounds__(256) void k_wkv6(WkvArgs a) {
+// ------------------------------------------------------------------------------------
+// wkv6_rows: k_wkv6's arithmetic for steps whose segments hold several rows (prefill and mixed
+// steps), in three phases per chunk of kRowsChunk rows instead of one whole row at a time
+// (SURVEY §2.1 K5p):
+//  A  everything that does not depend on the state, kRowsGroup rows per pair of barriers: the LoRA
+//     hidden nonlinearities, the LoRA-up dot products, decay / in-context rate / key / value
+//     mixing, the key-norm and bonus sums -> per-row vectors in LDS;
+//  B  the recurrence alone, row after row: the state update and y = S r from registers and those
+//     vectors, with no barrier (a state row lives in one quad of one wave);
+//  C  the GroupNorm, bonus and gate of kRowsGroup rows per pair of barriers, z planes out.
+// Every element takes the one-row code's expressions and reduction orders (the quad sums, the wave
+// sums, the four waves' partials combined (0 + 1) + (2 + 3)), so the z planes and the state are
+// bitwise those of wkv6_body's row loop (the prefill chunk- and batch-invariance tests compare
+// prefill rows with graph-replayed decode rows, whose WKV is wkv6_body).
+constexpr int kRowsChunk = 16, kRowsGroup = 2;
+template <bool F16>
+__device__ __attribute__((always_inline)) void wkv6_rows(const WkvArgs& a, const int bx, const int by) {
+  constexpr int N = 64, DW = 64, DA = 64, DV = 32, DG = 128, DALL = DW + DA + DV + DG, NP = 4;
+  constexpr int CH = kRowsChunk, G = kRowsGroup;
+  __shared__ __attribute__((aligned(16))) float s_hidG[G][DALL];
+  __shared__ float s_redG[G][4][4];
+  __shared__ __attribute__((aligned(16))) float s_vecC[CH][5][N];  // w, kk (unnormalised), a, k, r
+  __shared__ float s_vC[CH][N], s_gC[CH][N], s_yC[CH][N];        // mixed v, gate, y per channel
+  __shared__ float s_invC[CH], s_bonC[CH];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, i = t >> 2, qq = t & 3;
+  int seg_i = bx, h = by;
+  if (a.xmap) {  // 1-D grid: head h's workgroups share one XCD (as wkv6_body)
+    const int b = bx, xcd = b & 7, j = b >> 3;
+    h = xcd + 8 * (j / a.n_seg);
+    seg_i = j % a.n_seg;
+  }
+  const int C = a.C, c = h * N + i;
+  const int4 sg = a.segs[seg_i];
+  const int slot = sg.x, r_begin = sg.y, n_rows = sg.z;
+  uint4 lw[9];  // 8 bf16 per entry: w 0..1 | a 2..3 | v 4 | g 5..8 (launch_pack_lora6)
+  {
+    const uint4* pl = (const uint4*)(a.lup + (int64_t)h * 9 * 256 * 8);
+#pragma unroll
+    for (int u = 0; u < 9; ++u) lw[u] = pl[u * 256 + t];
+  }
+  const float w0 = a.w0[c], a0 = a.a0[c], v0 = a.v0[c], kkc = a.k_k[c], kac = a.k_a[c];
+  const float rkc = a.r_k[c], lnw = a.lnx_w[c], lnb = a.lnx_b[c];
+  const int64_t soff = a.layer_off + (int64_t)h * N * N + (int64_t)t * 4;
+  float4_ S4[4];
+  {
+    const float4_* Sp = (const float4_*)(a.state + (int64_t)slot * a.slot_stride + soff);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) S4[q] = Sp[q * 256];
+  }
+  const bool hid_thread = t < DALL / 4;
+  auto quad_sum = [](float x) {
+    x += dpp_mov<0xB1>(x);
+    return x + dpp_mov<0x4E>(x);
+  };
+  auto dot = [&](float2_ acc, const uint4 q, const float* hsrc) {
+    const float4_ h0 = *(const float4_*)hsrc;
+    const float4_ h1 = *(const float4_*)(hsrc + 4);
+    acc += w2f<F16>(q.x) * (float2_){h0[0], h0[1]};
+    acc += w2f<F16>(q.y) * (float2_){h0[2], h0[3]};
+    acc += w2f<F16>(q.z) * (float2_){h1[0], h1[1]};
+    acc += w2f<F16>(q.w) * (float2_){h1[2], h1[3]};
+    return acc;
+  };
+  for (int cb = 0; cb < n_rows; cb += CH) {
+    const int nr = min(CH, n_rows - cb);
+    // ---- A: the state-independent part, G rows per round
+    for (int g0 = 0; g0 < nr; g0 += G) {
+      float4_ hp[G][NP];
+      float rp[G][NP], kp[G][NP], vp[G][NP], vf[G];
+#pragma unroll
+      for (int gi = 0; gi < G; ++gi) {
+        const int row = r_begin + cb + g0 + min(gi, nr - g0 - 1);  // (past the chunk: the last row again)
+        const float* prow = a.part + (int64_t)row * a.ldp;
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+          const float* pp = prow + p * a.part_stride;
+          hp[gi][p] = *(const float4_*)(pp + 3 * C + (hid_thread ? 4 * t : 0));
+          rp[gi][p] = pp[c];
+          kp[gi][p] = pp[C + c];
+          vp[gi][p] = pp[2 * C + c];
+        }
+        vf[gi] = a.layer > 0 ? a.v_first[(int64_t)row * a.ldv + c] : 0.f;
+      }
+#pragma unroll
+      for (int gi = 0; gi < G; ++gi) {
+        if (hid_thread) {
+          float4_ x = hp[gi][0];
+#pragma unroll
+          for (int p = 1; p < NP; ++p) x += hp[gi][p];
+          float4_ y;
+          if (t < DW / 4) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) y[e] = ftanh(x[e]);
+          } else if (t < (DW + DA + DV) / 4) {
+            y = x;
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) y[e] = fsigm(x[e]);
+          }
+          *(float4_*)(&s_hidG[gi][4 * t]) = y;
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int gi = 0; gi < G; ++gi) {
+        if (g0 + gi >= nr) break;
+        const int rc = g0 + gi, row = r_begin + cb + rc;
+        float r = rp[gi][0], k = kp[gi][0], v = vp[gi][0];
+#pragma unroll
+        for (int p = 1; p < NP; ++p) {
+          r += rp[gi][p];
+          k += kp[gi][p];
+          v += vp[gi][p];
+        }
+        const float* sh = s_hidG[gi];
+        float2_ l0 = {0.f, 0.f}, l1 = {0.f, 0.f}, l2 = {0.f, 0.f}, l3 = {0.f, 0.f};
+#pragma unroll
+        for (int u = 0; u < 2; ++u) l0 = dot(l0, lw[u], sh + qq * (DW / 4) + u * 8);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) l1 = dot(l1, lw[2 + u], sh + DW + qq * (DA / 4) + u * 8);
+        l2 = dot(l2, lw[4], sh + DW + DA + qq * (DV / 4));
+#pragma unroll
+        for (int u = 0; u < 4; ++u) l3 = dot(l3, lw[5 + u], sh + DW + DA + DV + qq * (DG / 4) + u * 8);
+        const float lo0 = quad_sum(l0[0] + l0[1]), lo1 = quad_sum(l1[0] + l1[1]);
+        const float lo2 = quad_sum(l2[0] + l2[1]), lo3 = quad_sum(l3[0] + l3[1]);
+        const float w = fexp(-0.60653066f * fsigm(w0 + lo0));
+        const float av = fsigm(a0 + lo1);
+        const float kk = k * kkc;
+        k = k * (1.0f + (av - 1.0f) * kac);
+        if (a.layer == 0) {
+          if (qq == 0) a.v_first[(int64_t)row * a.ldv + c] = v;
+        } else {
+          v = v + (vf[gi] - v) * fsigm(v0 + lo2);
+        }
+        {
+          const float ksq = wave_sum(qq == 0 ? kk * kk : 0.f);
+          const float bon = wave_sum(qq == 0 ? r * k * rkc : 0.f);
+          if (lane == 0) { s_redG[gi][0][wave] = ksq; s_redG[gi][1][wave] = bon; }
+        }
+        if (qq == 0) {
+          s_vecC[rc][0][i] = w; s_vecC[rc][1][i] = kk; s_vecC[rc][2][i] = av; s_vecC[rc][3][i] = k;
+          s_vecC[rc][4][i] = r;
+          s_vC[rc][i] = v;
+          s_gC[rc][i] = lo3;
+        }
+      }
+      __syncthreads();
+      if (t < G && g0 + t < nr) {  // the row's key-norm reciprocal and bonus, as every thread forms them
+        const float* r0 = s_redG[t][0];
+        const float* r1 = s_redG[t][1];
+        s_invC[g0 + t] = __builtin_amdgcn_rcpf(fmaxf(sqrtf((r0[0] + r0[1]) + (r0[2] + r0[3])), 1e-12f));
+        s_bonC[g0 + t] = (r1[0] + r1[1]) + (r1[2] + r1[3]);
+      }
+    }
+    __syncthreads();
+    // ---- B: the recurrence, row after row, registers and LDS only
+    for (int rc = 0; rc < nr; ++rc) {
+      const float inv = s_invC[rc];
+      const float v = s_vC[rc][i];
+      const float* vj = &s_vecC[rc][0][qq * 16];
+      float2_ sa2 = {0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4_ kq = *(const float4_*)(vj + N + q * 4);
+        sa2 += (float2_){S4[q][0], S4[q][1]} * (float2_){kq[0], kq[1]};
+        sa2 += (float2_){S4[q][2], S4[q][3]} * (float2_){kq[2], kq[3]};
+      }
+      const float sa = quad_sum((sa2[0] + sa2[1]) * inv);
+      float2_ y2 = {0.f, 0.f};
+      const float2_ sav = {sa * inv, sa * inv}, vv = {v, v};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4_ wq = *(const float4_*)(vj + q * 4);
+        const float4_ kq = *(const float4_*)(vj + N + q * 4);
+        const float4_ aq = *(const float4_*)(vj + 2 * N + q * 4);
+        const float4_ k4 = *(const float4_*)(vj + 3 * N + q * 4);
+        const float4_ rq = *(const float4_*)(vj + 4 * N + q * 4);
+#pragma unroll
+        for (int e = 0; e < 4; e += 2) {
+          float2_ sv = (float2_){S4[q][e], S4[q][e + 1]} * (float2_){wq[e], wq[e + 1]};
+          sv -= sav * ((float2_){kq[e], kq[e + 1]} * (float2_){aq[e], aq[e + 1]});
+          sv += vv * (float2_){k4[e], k4[e + 1]};
+          S4[q][e] = sv[0];
+          S4[q][e + 1] = sv[1];
+          y2 += sv * (float2_){rq[e], rq[e + 1]};
+        }
+      }
+      const float y = quad_sum(y2[0] + y2[1]);
+      if (qq == 0) s_yC[rc][i] = y;
+    }
+    __syncthreads();
+    // ---- C: GroupNorm + bonus + gate, G rows per round, z planes out
+    for (int g0 = 0; g0 < nr; g0 += G) {
+#pragma unroll
+      for (int gi = 0; gi < G; ++gi) {
+        if (g0 + gi >= nr) break;
+        const float y = s_yC[g0 + gi][i];
+        const float s1 = wave_sum(qq == 0 ? y : 0.f);
+        const float s2 = wave_sum(qq == 0 ? y * y : 0.f);
+        if (lane == 0) { s_redG[gi][2][wave] = s1; s_redG[gi][3][wave] = s2; }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int gi = 0; gi < G; ++gi) {
+        if (g0 + gi >= nr) break;
+        const int rc = g0 + gi, row = r_begin + cb + rc;
+        const float mean = ((s_redG[gi][2][0] + s_redG[gi][2][1]) + (s_redG[gi][2][2] + s_redG[gi][2][3])) * (1.0f / N);
+        const float var =
+            fmaxf(((s_redG[gi][3][0] + s_redG[gi][3][1]) + (s_redG[gi][3][2] + s_redG[gi][3][3])) * (1.0f / N) - mean * mean, 0.f);
+        if (qq == 0) {
+          const float y = s_yC[rc][i], v = s_vC[rc][i], lo3 = s_gC[rc][i], bonus = s_bonC[rc];
+          const float gn = (y - mean) * __builtin_amdgcn_rsqf(var + 64e-5f) * lnw + lnb;
+          split_store((gn + bonus * v) * lo3, a.z_hi, a.z_lo, (int64_t)row * a.ldz + c, F16);
+        }
+      }
+      __syncthreads();  // (s_redG / the chunk's LDS rows are reused)
+    }
+  }
+  if (a.wt) {
+    const auto rs = wt_rsrc(a.state + (int64_t)slot * a.slot_stride + a.layer_off + (int64_t)h * N * N);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) store_wt(rs, (q * 256 + t) * 16, S4[q]);
+  } else {
+    float4_* Srow = (float4_*)(a.state + (int64_t)slot * a.slot_stride + soff);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) Srow[q * 256] = S4[q];
+  }
+}
+
+// (multi-row steps: two workgroups per CU -- without the bound the compiler took 256 VGPRs + 2 AGPRs,
+// one wave per SIMD, so the 512 workgroups of a 32-slot prefill step ran in two rounds)
+template <bool F16, bool MULTI_ROW = false>  // MULTI_ROW: steps whose segments hold several rows (wkv6_rows)
+__global__ __launch_bounds__(256, MULTI_ROW ? 2 : 1) void k_wkv6(WkvArgs a) {
   tl_begin(a.tl);
-  wkv6_body<F16, 0>(a, blockIdx.x, blockIdx.y, FfnSync{});
+  if constexpr (MULTI_ROW) wkv6_rows<F16>(a, blockIdx.x, blockIdx.y);
+  else wkv6_body<F16, 0>(a, blockIdx.x, blockIdx.y, FfnSync{});
   tl_end(a.tl);
 }
 

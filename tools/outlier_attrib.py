@@ -66,6 +66,7 @@ def main():
     print(f"{len(dec)} decode-step launches, {len(voc)} vocoder launches; outliers: > {K:g} x class median")
     print(f"{'class':62s} {'n':>7s} {'med_us':>7s} {'alone':>7s} {'beside':>7s} {'mean':>7s} {'max':>9s} {'outl':>6s} {'excess_ms':>9s}")
     charge = defaultdict(lambda: [0, 0.0])
+    tax = defaultdict(lambda: [0, 0.0])  # every launch beside the vocoder: duration - the class's median alone
     worst = []
     for (n, g), ds in sorted(by_cls.items(), key=lambda kv: -len(kv[1])):
         if len(ds) < 20:
@@ -73,9 +74,15 @@ def main():
         du = [(d[1] - d[0]) / 1e3 for d in ds]
         med = statistics.median(du)
         alone, beside, nout, excess = [], [], 0, 0.0
-        for d, t in zip(ds, du):
-            ov = overlaps(d[0], d[1])
+        ovs = [overlaps(d[0], d[1]) for d in ds]
+        med_alone = statistics.median([t for t, ov in zip(du, ovs) if not ov] or du)
+        for d, t, ov in zip(ds, du, ovs):
             (beside if ov else alone).append(t)
+            if ov:
+                best = max(ov, key=lambda v: min(v[1], d[1]) - max(v[0], d[0]))
+                e = tax[(best[2], best[3])]
+                e[0] += 1
+                e[1] += t - med_alone
             if t > K * med:
                 nout += 1
                 excess += t - med
@@ -91,6 +98,12 @@ def main():
         fm = lambda x: f"{statistics.median(x):7.2f}" if x else "      -"
         print(f"{(n + ' g' + g)[:62]:62s} {len(ds):7d} {med:7.2f} {fm(alone)} {fm(beside)} {statistics.fmean(du):7.2f} "
               f"{max(du):9.1f} {nout:6d} {excess / 1e3:9.2f}")
+    print("\nthe decode tax: every decode-step launch overlapping a vocoder kernel, its duration minus its class's "
+          "median alone, charged to the vocoder class with the largest overlap:")
+    tot = sum(ex for _, ex in tax.values())
+    for (n, g), (c, ex) in sorted(tax.items(), key=lambda kv: -kv[1][1]):
+        print(f"  {c:7d} launches {ex / 1e3:9.2f} ms ({100 * ex / max(tot, 1e-9):5.1f} %)  {(n + ' g' + g)[:70]}")
+    print(f"  total {tot / 1e3:.2f} ms")
     print("\nexcess time of the outliers charged to the overlapping vocoder kernel class (largest overlap):")
     for (n, g), (c, ex) in sorted(charge.items(), key=lambda kv: -kv[1][1]):
         vd = [(v[1] - v[0]) / 1e3 for v in voc if v[2] == n and v[3] == g]
