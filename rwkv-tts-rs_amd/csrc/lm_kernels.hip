@@ -1310,6 +1310,127 @@ __global__ __launch_bounds__(256) void k_gemm2(GemmArgs a) {
   tl_end(a.tl);
 }
 
+// Prefill (multi-row) planes GEMMs of one segment, NB 64-column tiles per workgroup: each staged X
+// slice feeds NB x 64 columns instead of 64 (k_gemm2 re-reads a row group's X slice once per
+// 64-column tile: for a 1280-row step's 64-tile FFN key GEMM that is 335 MB of MALL reads). Every
+// output element takes k_gemm2's MFMA sequence (the hi and lo chains over the K-slice's 32-wide steps
+// in order, hi + lo at the end), so the partial slabs are bit-identical; rows past M are copies of
+// row M - 1 (as k_gemm2's plain launches) and are not stored.
+template <int KSTEPS, bool F16, int NB>
+__global__ __launch_bounds__(256) void k_gemm_wide(GemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int MT = 2, KS = KSTEPS * 32, LD = KS + 8, ROWS = MT * 16, CH = KS / 8, PERP = ROWS * CH / 256;
+  constexpr int LDT = NB * 64 + 4;
+  tl_begin(a.tl);
+  bf16_t* xh = (bf16_t*)smem;
+  bf16_t* xl = xh + ROWS * LD;
+  const int split = blockIdx.y, kbeg = split * KS;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
+  const GemmSeg& sg = a.seg[0];
+  const bf16_t* Xhi = sg.Xhi;
+  const bf16_t* Xlo = sg.Xlo;
+  const int ldx = sg.ldx, Nn = sg.N, nblk = (Nn + 15) >> 4;
+  const int colw = blockIdx.x * (NB * 64);  // the workgroup's first column within the segment
+  const int nrg = (a.M + ROWS - 1) / ROWS;
+  int rg = blockIdx.z;
+  short8 vh[PERP], vl[PERP];
+  auto load_x = [&](int rg_) {
+#pragma unroll
+    for (int u = 0; u < PERP; ++u) {
+      const int c = threadIdx.x + u * 256;
+      const int r = c / CH, k8 = (c % CH) * 8;
+      const int64_t o = (int64_t)min(rg_ * ROWS + r, a.M - 1) * ldx + kbeg + k8;
+      vh[u] = *(const short8*)(Xhi + o);
+      vl[u] = *(const short8*)(Xlo + o);
+    }
+  };
+  load_x(rg);
+  short8 b[NB][KSTEPS];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int nb = min((colw + j * 64 + wave * 16) >> 4, nblk - 1);
+    const bf16_t* wp = sg.W + (((int64_t)nb * (a.K >> 5) + (kbeg >> 5)) * 64 + lane) * 8;
+#pragma unroll
+    for (int t = 0; t < KSTEPS; ++t) b[j][t] = __builtin_nontemporal_load((const short8*)(wp + t * 512));
+  }
+  for (;;) {
+    const int row0 = rg * ROWS;
+#pragma unroll
+    for (int u = 0; u < PERP; ++u) {
+      const int c = threadIdx.x + u * 256;
+      const int r = c / CH, k8 = (c % CH) * 8;
+      *(short8*)(xh + r * LD + k8) = vh[u];
+      *(short8*)(xl + r * LD + k8) = vl[u];
+    }
+    __syncthreads();
+    const int rg_next = rg + (int)gridDim.z;
+    if (rg_next < nrg) load_x(rg_next);  // in flight during this group's MFMAs and stores
+    float4_ acc_h[NB][MT], acc_l[NB][MT];
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+      for (int m = 0; m < MT; ++m) acc_h[j][m] = acc_l[j][m] = (float4_){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < KSTEPS; ++t) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        const int o = (m * 16 + li) * LD + t * 32 + g * 8;
+        const short8 ah = *(const short8*)(xh + o);
+        const short8 al = *(const short8*)(xl + o);
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          if constexpr (F16) {
+            acc_h[j][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, ah),
+                                                                 __builtin_bit_cast(f16x8, b[j][t]), acc_h[j][m], 0, 0, 0);
+            acc_l[j][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, al),
+                                                                 __builtin_bit_cast(f16x8, b[j][t]), acc_l[j][m], 0, 0, 0);
+          } else {
+            acc_h[j][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ah),
+                                                                  __builtin_bit_cast(bf16x8, b[j][t]), acc_h[j][m], 0, 0, 0);
+            acc_l[j][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, al),
+                                                                  __builtin_bit_cast(bf16x8, b[j][t]), acc_l[j][m], 0, 0, 0);
+          }
+        }
+      }
+    }
+    // store: the tile staged in LDS (D layout: col = lane & 15, row = 4 (lane >> 4) + jj), then whole
+    // 16-byte pieces per lane (write-through where asked, as k_gemm2)
+    float* st = (float*)smem;
+    __syncthreads();  // every wave is done reading its X fragments
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+          st[(m * 16 + 4 * g + jj) * LDT + j * 64 + wave * 16 + li] = acc_h[j][m][jj] + acc_l[j][m][jj];
+    __syncthreads();
+    float* outp = a.out + (int64_t)split * a.split_stride + sg.col_off;
+    const auto rs = wt_rsrc(a.out);
+    for (int q = threadIdx.x; q < ROWS * NB * 16; q += 256) {
+      const int r = q / (NB * 16), c4 = (q % (NB * 16)) * 4, row = row0 + r, col = colw + c4;
+      if (row >= a.M || col >= Nn) continue;
+      const int64_t o = (int64_t)row * a.ldo + col;
+      const float4_ v = *(const float4_*)(st + r * LDT + c4);
+      float* dst = outp + o;
+      if (a.wt) {
+        const int64_t ob = dst - a.out;  // element offset from the buffer start
+        if (col + 4 <= Nn && (ob & 3) == 0) {
+          store_wt(rs, (int)(ob * 4), v);
+        } else {
+          for (int e = 0; e < 4 && col + e < Nn; ++e) store_wt(rs, (int)((ob + e) * 4), v[e]);
+        }
+      } else {
+        for (int e = 0; e < 4 && col + e < Nn; ++e) dst[e] = v[e];
+      }
+    }
+    if (rg_next >= nrg) break;
+    rg = rg_next;
+    __syncthreads();  // every wave is done with the LDS X image / store staging
+  }
+  tl_end(a.tl);
+}
+
 // the head GEMM of a one-row step with ln_out folded in (gemm2_body ROLE 10): one launch and one
 // launch boundary fewer per step; logits bit for bit those of ln_out + k_gemm2
 template <bool F16>
@@ -1670,6 +1791,23 @@ static void launch_gemm_t(const GemmArgs& a, dim3 grid, hipStream_t st) {
         b.tiles_per_xcd = (int)((grid.x * a.k_split + 7) / 8);
         grid = dim3(8 * b.tiles_per_xcd);
       }
+    }
+    // prefill steps of one segment with planes X (FFN key / value, Wo): k_gemm_wide, several
+    // 64-column tiles per workgroup (bit-identical slabs)
+    // (KSTEPS 8: the FFN key / value GEMMs, 47 -> 42 us per launch on a 1280-row step; the Wo GEMM's
+    // 4-step slices measured 18 -> 19 us at four tiles per workgroup and keep k_gemm2)
+    constexpr int kWideNB = 2;
+    if constexpr (MT == 2 && KSTEPS == 8) {
+    if (grid.z > 1 && !a.q_fmt && a.xmode == kXPlanes && a.nseg == 1 && a.seg[0].tile_start == 0 &&
+        (int)grid.x % kWideNB == 0 && b.xmap == 0) {
+      dim3 gw((int)grid.x / kWideNB, grid.y, grid.z);
+      const int rpw = std::max(1, (int)gw.z * (int)(gw.x * gw.y) / 1024);
+      gw.z = (gw.z + rpw - 1) / rpw;
+      const size_t lw = std::max(lds, (size_t)MT * 16 * (kWideNB * 64 + 4) * 4);
+      if (a.f16) RT_LAUNCH((k_gemm_wide<KSTEPS, true, kWideNB>), gw, dim3(256), lw, st, b);
+      else RT_LAUNCH((k_gemm_wide<KSTEPS, false, kWideNB>), gw, dim3(256), lw, st, b);
+      return;
+    }
     }
     // prefill steps: several row groups per workgroup (weights loaded once), as many as keep >= 4
     // workgroups per CU (measured over 1 / 2 / 4 / 8 / 10 / 20 / 40 groups per workgroup on a
