@@ -85,6 +85,10 @@ __device__ inline void split_store(bf16_t* h, bf16_t* l, int64_t o, float v) {
 // 92-104 KB at 128 rows) leaves room for one workgroup per CU only, so a 4-wave workgroup would
 // run one wave per SIMD and expose every wait; 8 waves share the same weight tiles.
 constexpr int conv_waves(int KT) { return KT == 7 ? 8 : 4; }
+// 16-row staging blocks per wave and chunk (one buffer offset register each): 17 for the 4-wave
+// fused residual unit, whose dilation-9 window (192 rows, hi + lo) and 7-tap weights are 66 blocks
+constexpr int conv_maxb(int nwv, bool fuse) { return fuse && nwv == 4 ? 17 : 16; }
+template <int NWV, bool FUSE> struct ConvMaxB { static constexpr int v = FUSE && NWV == 4 ? 17 : 16; };
 
 // every k_conv instantiation the host dispatches: (column tile, taps class, weight lo plane, waves)
 #define RT_CONV_KERNELS(X)                                                                       \
@@ -164,14 +168,15 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? 1 : 2) void k_conv(ConvArgs a)
   // (this utterance's input hi / lo plane, the weights' hi / lo plane); a chunk adds a scalar
   // offset (the input's chunk stride, or 32 channels of weights). Out-of-range window rows get
   // an offset past the resources' range, which the buffer load returns as zeros.
-  constexpr int MAXB = 16;
+  constexpr int MAXB = ConvMaxB<NWV, FUSE>::v;
   constexpr uint32_t kOob = 0x80000000u;
   auto rsrc = [](const void* base) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7fffffff, 0x00020000);
   };
   const __amdgpu_buffer_rsrc_t rxh = rsrc(a.xh + xoff), rxl = rsrc(a.xl + xoff), rwh = rsrc(a.w),
                                rwl = rsrc(WLO ? a.wl : a.w);
-  uint32_t voff[MAXB];
+  static_assert(MAXB <= 17, "staging offsets");
+  uint32_t voff[17];  // (a constant bound: a template-dependent one made hipcc drop every k_conv host stub)
 #pragma unroll
   for (int u = 0; u < MAXB; ++u) {
     const int b = wave + NWV * u;
@@ -949,7 +954,7 @@ class Codec {
       const size_t chunk = 2 * (size_t)(2 * wr + 7 * 96) * 64;
       const size_t fused = (size_t)3 * 2 * 32 * nw * 64 + 3 * 96 * 64;
       const size_t epi = (size_t)nw * 32 * 100 * sizeof(float);
-      if (std::max(std::max(chunk, fused), epi) <= 160 * 1024 && (2 * wr + 7 * 96) / 16 <= 16 * nw) {
+      if (std::max(std::max(chunk, fused), epi) <= 160 * 1024 && (2 * wr + 7 * 96) / 16 <= conv_maxb(nw, true) * nw) {
         nwv = nw;
         break;
       }
